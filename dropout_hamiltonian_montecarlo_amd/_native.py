@@ -1,0 +1,181 @@
+"""ctypes binding of libhmcx.so (include/hmcx.h).
+
+The HIP library is the only compute path of this package: if it is missing or no
+HIP device is visible, every entry point raises — there is no CPU fallback.
+torch is imported first so that the process has exactly one HIP runtime (torch's
+libamdhip64.so.7 satisfies libhmcx.so's NEEDED entry by soname).
+"""
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libhmcx.so")
+
+HMCX_F32, HMCX_F64 = 0, 1
+NOISE_BUFFER, NOISE_PHILOX = 0, 1
+
+c_int, c_double, c_void_p = ctypes.c_int, ctypes.c_double, ctypes.c_void_p
+c_i64p = ctypes.POINTER(ctypes.c_int64)
+c_i32p = ctypes.POINTER(ctypes.c_int32)
+c_dblp = ctypes.POINTER(ctypes.c_double)
+c_u8p = ctypes.POINTER(ctypes.c_uint8)
+
+
+class SamplerArgs(ctypes.Structure):
+    _fields_ = [("dtype", c_int), ("B", c_int), ("D", c_int), ("K", c_int), ("C", c_int),
+                ("n_steps", c_int), ("alpha", c_double), ("log_prior", c_double),
+                ("X", c_void_p), ("Y", c_void_p), ("row0", c_i64p), ("eps", c_dblp),
+                ("n_iter", c_i32p), ("u_accept", c_dblp), ("want_ll", c_u8p),
+                ("noise_mode", c_int), ("noise", c_void_p), ("noise_off", c_i64p),
+                ("seed", ctypes.c_uint64), ("chain0", ctypes.c_uint32), ("step_base", ctypes.c_uint32),
+                ("W", c_void_p), ("b", c_void_p), ("out_A", c_void_p), ("out_accepted", c_void_p),
+                ("out_ll", c_void_p), ("out_E", c_void_p)]
+
+
+class MvnArgs(ctypes.Structure):
+    _fields_ = [("dim", c_int), ("C", c_int), ("n_steps", c_int), ("mu", c_void_p), ("prec", c_void_p),
+                ("nlp_const", c_double), ("eps", c_dblp), ("n_iter", c_i32p), ("u_accept", c_dblp),
+                ("noise_mode", c_int), ("noise", c_void_p), ("noise_off", c_i64p),
+                ("seed", ctypes.c_uint64), ("chain0", ctypes.c_uint32), ("step_base", ctypes.c_uint32),
+                ("x", c_void_p), ("out_A", c_void_p), ("out_accepted", c_void_p), ("out_nlp", c_void_p),
+                ("out_trace", c_void_p)]
+
+
+# Every symbol include/hmcx.h declares (checked by tests/test_capi.py).
+EXPORTS = ("hmcx_version", "hmcx_create", "hmcx_destroy", "hmcx_last_error", "hmcx_set_stream",
+           "hmcx_synchronize", "hmcx_set_graph_mode", "hmcx_philox_uniforms", "hmcx_philox_normals",
+           "hmcx_softmax_grad", "hmcx_softmax_loglik", "hmcx_softmax_predict", "hmcx_sghmc_run",
+           "hmcx_sgld_run", "hmcx_hmc_mvn_run")
+
+_lib = None
+_lock = threading.Lock()
+
+
+class HmcxError(RuntimeError):
+    pass
+
+
+def load_library():
+    """Load libhmcx.so (no GPU needed); raise if it has not been built."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise HmcxError("libhmcx.so not built (%s): run `python -c 'import __graft_entry__ as g; g.build()'`"
+                            % LIB_PATH)
+        lib = ctypes.CDLL(LIB_PATH)
+        lib.hmcx_version.restype = c_int
+        lib.hmcx_create.argtypes = [c_int, ctypes.POINTER(c_void_p)]
+        lib.hmcx_destroy.argtypes = [c_void_p]
+        lib.hmcx_last_error.argtypes = [c_void_p]
+        lib.hmcx_last_error.restype = ctypes.c_char_p
+        lib.hmcx_set_stream.argtypes = [c_void_p, c_void_p]
+        lib.hmcx_synchronize.argtypes = [c_void_p]
+        lib.hmcx_set_graph_mode.argtypes = [c_void_p, c_int]
+        lib.hmcx_philox_uniforms.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                             ctypes.c_uint32, c_dblp]
+        lib.hmcx_philox_uniforms.restype = None
+        lib.hmcx_philox_normals.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                            ctypes.c_uint32, ctypes.c_uint32, c_dblp]
+        lib.hmcx_philox_normals.restype = None
+        lib.hmcx_softmax_grad.argtypes = [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                                          c_void_p, c_void_p, c_double, c_void_p, c_void_p]
+        lib.hmcx_softmax_loglik.argtypes = [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                                            c_void_p, c_void_p, c_void_p]
+        lib.hmcx_softmax_predict.argtypes = [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int,
+                                             c_void_p, c_void_p, c_void_p]
+        lib.hmcx_sghmc_run.argtypes = [c_void_p, ctypes.POINTER(SamplerArgs)]
+        lib.hmcx_sgld_run.argtypes = [c_void_p, ctypes.POINTER(SamplerArgs)]
+        lib.hmcx_hmc_mvn_run.argtypes = [c_void_p, ctypes.POINTER(MvnArgs)]
+        _lib = lib
+        return lib
+
+
+class Context:
+    """One hmcx context per HIP device; calls run on torch's current stream."""
+
+    def __init__(self, device):
+        lib = load_library()
+        if not torch.cuda.is_available():
+            raise HmcxError("no HIP device visible: the HIP engine has no CPU fallback")
+        self.lib = lib
+        self.device = torch.device("cuda", device if isinstance(device, int) else (device.index or 0))
+        h = c_void_p()
+        with torch.cuda.device(self.device):
+            rc = lib.hmcx_create(self.device.index, ctypes.byref(h))
+        if rc != 0:
+            raise HmcxError("hmcx_create failed (%d)" % rc)
+        self.h = h
+
+    def bind_stream(self):
+        s = torch.cuda.current_stream(self.device)
+        self.lib.hmcx_set_stream(self.h, c_void_p(s.cuda_stream))
+
+    def check(self, rc, what):
+        if rc != 0:
+            msg = self.lib.hmcx_last_error(self.h)
+            raise HmcxError("%s failed (%d): %s" % (what, rc, msg.decode() if msg else ""))
+
+    def set_graph_mode(self, on):
+        self.check(self.lib.hmcx_set_graph_mode(self.h, 1 if on else 0), "hmcx_set_graph_mode")
+
+    def __del__(self):
+        try:
+            if getattr(self, "h", None) and self.h.value:
+                self.lib.hmcx_destroy(self.h)
+        except Exception:
+            pass
+
+
+_ctxs = {}
+
+
+def context(device=None):
+    """Context for `device` (default: torch's current device)."""
+    if device is None:
+        device = torch.cuda.current_device() if torch.cuda.is_available() else 0
+    idx = device if isinstance(device, int) else (torch.device(device).index or 0)
+    with _lock:
+        ctx = _ctxs.get(idx)
+    if ctx is None:
+        ctx = Context(idx)
+        with _lock:
+            _ctxs[idx] = ctx
+    ctx.bind_stream()
+    return ctx
+
+
+def ptr(t):
+    return c_void_p(t.data_ptr()) if t is not None else c_void_p()
+
+
+def dtype_code(dt):
+    if dt == torch.float64:
+        return HMCX_F64
+    if dt == torch.float32:
+        return HMCX_F32
+    raise HmcxError("unsupported dtype %s (float32/float64)" % dt)
+
+
+def philox_uniforms(seed, chain, step, slot, n):
+    import numpy as np
+    lib = load_library()
+    out = np.empty(n, dtype=np.float64)
+    lib.hmcx_philox_uniforms(seed, chain, step, slot, n, out.ctypes.data_as(c_dblp))
+    return out
+
+
+def philox_normals(seed, chain, step, slot, e0, n):
+    import numpy as np
+    lib = load_library()
+    out = np.empty(n, dtype=np.float64)
+    lib.hmcx_philox_normals(seed, chain, step, slot, e0, n, out.ctypes.data_as(c_dblp))
+    return out
+
+
+SLOT_PATH = 0xFFFFFFFE
+SLOT_ACCEPT = 0xFFFFFFFD

@@ -1,0 +1,101 @@
+// hmcx_common.h — shared device/host helpers for the MI355X (gfx950) SG-HMC engine.
+//
+//  * Philox4x32-10 counter-based RNG (host + device, bit-identical on both), used in
+//    HMCX_NOISE_PHILOX mode for momenta / SGHMC friction noise / SGLD noise and, on the
+//    host, for path lengths and accept uniforms.  The reference draws these from
+//    NumPy streams (cpu/sghmc.py:21,25,31,36; cpu/sgld.py:45); HMCX_NOISE_BUFFER mode
+//    replays host-drawn NumPy normals instead, bit for bit.
+//  * MFMA wrappers for the two dense GEMMs of the softmax gradient (softmax.py:39,54):
+//    v_mfma_f64_16x16x4_f64 (parity dtype) and v_mfma_f32_16x16x4_f32 (fast dtype).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <math.h>
+
+namespace hmcx {
+
+// ---------------------------------------------------------------- Philox4x32-10
+struct u32x4 { uint32_t v[4]; };
+
+__host__ __device__ inline uint32_t mulhi32(uint32_t a, uint32_t b) {
+  return (uint32_t)(((uint64_t)a * (uint64_t)b) >> 32);
+}
+
+__host__ __device__ inline u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
+  const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    uint32_t hi0 = mulhi32(M0, c.v[0]), lo0 = M0 * c.v[0];
+    uint32_t hi1 = mulhi32(M1, c.v[2]), lo1 = M1 * c.v[2];
+    u32x4 n;
+    n.v[0] = hi1 ^ c.v[1] ^ k0;
+    n.v[1] = lo1;
+    n.v[2] = hi0 ^ c.v[3] ^ k1;
+    n.v[3] = lo0;
+    c = n;
+    k0 += W0;
+    k1 += W1;
+  }
+  return c;
+}
+
+// 53-bit uniform in [0,1) from two 32-bit words.
+__host__ __device__ inline double u53(uint32_t a, uint32_t b) {
+  return (double)(((uint64_t)a << 21) ^ (uint64_t)(b >> 11)) * (1.0 / 9007199254740992.0);
+}
+
+// Counter layout: {element pair, slot, step, chain}; key = seed.
+// slot 0 = momentum / SGLD noise, slot i+1 = leapfrog iteration i noise,
+// SLOT_PATH / SLOT_ACCEPT = per-step uniforms.
+constexpr uint32_t SLOT_PATH = 0xFFFFFFFEu;
+constexpr uint32_t SLOT_ACCEPT = 0xFFFFFFFDu;
+
+__host__ __device__ inline double philox_uniform(uint64_t seed, uint32_t chain, uint32_t step,
+                                                 uint32_t slot, uint32_t idx) {
+  u32x4 c = {{idx, slot, step, chain}};
+  u32x4 r = philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+  return u53(r.v[0], r.v[1]);
+}
+
+// Standard normal for element `e` (Box–Muller on one Philox block, two normals per block).
+__host__ __device__ inline double philox_normal(uint64_t seed, uint32_t chain, uint32_t step,
+                                                uint32_t slot, uint32_t e) {
+  u32x4 c = {{e >> 1, slot, step, chain}};
+  u32x4 r = philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+  double u1 = 1.0 - u53(r.v[0], r.v[1]);  // (0,1]
+  double u2 = u53(r.v[2], r.v[3]);
+  double rad = sqrt(-2.0 * log(u1));
+  double th = 6.283185307179586 * u2;
+  return (e & 1u) ? rad * sin(th) : rad * cos(th);
+}
+
+// ---------------------------------------------------------------- MFMA 16x16x4
+// A[i][k]: lane l holds i = l&15, k = l>>4; B[k][j]: k = l>>4, j = l&15 (both dtypes).
+// C/D: f32: row = (l>>4)*4 + r, col = l&15;  f64: row = (l>>4) + 4*r, col = l&15.
+typedef double d4 __attribute__((ext_vector_type(4)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+template <typename T> struct mfma16;
+template <> struct mfma16<double> {
+  typedef d4 acc_t;
+  __device__ static inline acc_t zero() { return acc_t{0.0, 0.0, 0.0, 0.0}; }
+  __device__ static inline acc_t fma(double a, double b, acc_t c) {
+    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+  }
+  __device__ static inline int row(int lane, int r) { return (lane >> 4) + 4 * r; }
+};
+template <> struct mfma16<float> {
+  typedef f4 acc_t;
+  __device__ static inline acc_t zero() { return acc_t{0.f, 0.f, 0.f, 0.f}; }
+  __device__ static inline acc_t fma(float a, float b, acc_t c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+  }
+  __device__ static inline int row(int lane, int r) { return (lane >> 4) * 4 + r; }
+};
+
+// NaN-propagating min/max with NumPy semantics (np.minimum / np.maximum / np.max).
+template <typename T> __device__ inline T np_min(T a, T b) { return (a != a) ? a : ((b < a) ? b : a); }
+template <typename T> __device__ inline T np_max(T a, T b) { return (a != a) ? a : ((b > a) ? b : a); }
+template <typename T> __device__ inline T max_nan(T m, T z) { return (z > m || z != z) ? z : m; }
+
+}  // namespace hmcx

@@ -1,0 +1,356 @@
+// hmcx_ctx.hip — context, workspace, staging, hipGraph capture, the C ABI (include/hmcx.h),
+// and the full-batch HMC kernel for the MVN model (config 1).
+#include "hmcx_common.h"
+#include "hmcx_internal.h"
+#include <new>
+#include <cstring>
+
+namespace hmcx {
+
+int set_error(hmcx_ctx* ctx, int code, const std::string& msg) {
+  if (ctx) ctx->err = msg;
+  return code;
+}
+
+bool Workspace::retry() {
+  if (off <= ctx->ws_cap) return false;
+  if (ctx->ws) {
+    if (hipStreamSynchronize(ctx->stream) != hipSuccess) { failed = true; return false; }
+    (void)hipFree(ctx->ws);
+    ctx->ws = nullptr;
+    ctx->ws_cap = 0;
+  }
+  const size_t want = off + off / 4 + (1 << 20);
+  if (hipMalloc((void**)&ctx->ws, want) != hipSuccess) {
+    ctx->ws = nullptr;
+    failed = true;
+    set_error(ctx, HMCX_ENOMEM, "hipMalloc workspace failed");
+    return false;
+  }
+  ctx->ws_cap = want;
+  return true;
+}
+
+void begin_call(hmcx_ctx* ctx) {
+  if (ctx->stage_pending) {
+    (void)hipEventSynchronize(ctx->stage_ev);
+    ctx->stage_pending = false;
+  }
+  ctx->stage_off = 0;
+}
+
+int upload(hmcx_ctx* ctx, void* dst, const void* src, size_t bytes) {
+  if (bytes == 0) return HMCX_OK;
+  if (!src) return set_error(ctx, HMCX_EINVAL, "upload: null host array");
+  const size_t need = ctx->stage_off + ((bytes + 255) / 256) * 256;
+  if (need > ctx->stage_cap) {
+    // a grown staging buffer invalidates earlier offsets of this call: drain the stream first
+    HMCX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    char* nb = nullptr;
+    const size_t cap = std::max(need * 2, (size_t)1 << 20);
+    HMCX_HIP(ctx, hipHostMalloc((void**)&nb, cap, hipHostMallocDefault));
+    if (ctx->stage) (void)hipHostFree(ctx->stage);
+    ctx->stage = nb;
+    ctx->stage_cap = cap;
+    ctx->stage_off = 0;
+  }
+  char* h = ctx->stage + ctx->stage_off;
+  std::memcpy(h, src, bytes);
+  ctx->stage_off += ((bytes + 255) / 256) * 256;
+  HMCX_HIP(ctx, hipMemcpyAsync(dst, h, bytes, hipMemcpyHostToDevice, ctx->stream));
+  HMCX_HIP(ctx, hipEventRecord(ctx->stage_ev, ctx->stream));
+  ctx->stage_pending = true;
+  return HMCX_OK;
+}
+
+GraphScope::GraphScope(hmcx_ctx* c) : ctx(c) {
+  if (ctx->graph_mode && hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal) == hipSuccess)
+    capturing = true;
+}
+
+int GraphScope::finish() {
+  if (!capturing) return HMCX_OK;
+  capturing = false;
+  hipGraph_t graph = nullptr;
+  HMCX_HIP(ctx, hipStreamEndCapture(ctx->stream, &graph));
+  hipGraphExec_t exec = nullptr;
+  hipError_t e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+  if (e != hipSuccess) {
+    (void)hipGraphDestroy(graph);
+    return set_error(ctx, HMCX_EHIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(e));
+  }
+  e = hipGraphLaunch(exec, ctx->stream);
+  // The executable graph is destroyed only after it has run.
+  (void)hipStreamSynchronize(ctx->stream);
+  (void)hipGraphExecDestroy(exec);
+  (void)hipGraphDestroy(graph);
+  if (e != hipSuccess) return set_error(ctx, HMCX_EHIP, std::string("hipGraphLaunch: ") + hipGetErrorString(e));
+  return HMCX_OK;
+}
+
+GraphScope::~GraphScope() {
+  if (capturing) {
+    hipGraph_t g = nullptr;
+    (void)hipStreamEndCapture(ctx->stream, &g);
+    if (g) (void)hipGraphDestroy(g);
+  }
+}
+
+// ------------------------------------------------------------------ MVN full-batch HMC
+// cpu/hmc.py:39-71 with mvn_gaussian.py:14-31, one thread per chain, all steps in one launch.
+struct MvnArgs {
+  int dim, C, n_steps;
+  const double* mu; const double* prec; double nlp_const;
+  const double* eps; const int32_t* n_iter; const double* u;
+  int noise_mode; const double* noise; const int64_t* noff;
+  uint64_t seed; uint32_t chain0, step_base;
+  double* x; double* out_A; int32_t* out_acc; double* out_nlp; double* out_trace;
+};
+constexpr int MVN_MAXDIM = 16;
+
+__device__ inline void mvn_grad(const MvnArgs& a, const double* x, double* g) {
+  double dm[MVN_MAXDIM];
+  for (int i = 0; i < a.dim; ++i) dm[i] = x[i] - a.mu[i];
+  for (int j = 0; j < a.dim; ++j) {                     // np.dot(x - mu, inv(cov))
+    double s = dm[0] * a.prec[j];
+    for (int i = 1; i < a.dim; ++i) s = s + dm[i] * a.prec[i * a.dim + j];
+    g[j] = s;
+  }
+}
+
+__device__ inline double mvn_nlp(const MvnArgs& a, const double* x) {
+  double dm[MVN_MAXDIM], v[MVN_MAXDIM];
+  for (int i = 0; i < a.dim; ++i) dm[i] = x[i] - a.mu[i];
+  for (int j = 0; j < a.dim; ++j) {
+    double s = dm[0] * a.prec[j];
+    for (int i = 1; i < a.dim; ++i) s = s + dm[i] * a.prec[i * a.dim + j];
+    v[j] = s;
+  }
+  double q = v[0] * dm[0];
+  for (int j = 1; j < a.dim; ++j) q = q + v[j] * dm[j];
+  return (a.nlp_const + q) * 0.5;                        // mvn_gaussian.py:27-30
+}
+
+__global__ void k_hmc_mvn(MvnArgs a) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= a.C) return;
+  double x[MVN_MAXDIM], xn[MVN_MAXDIM], p[MVN_MAXDIM], p0[MVN_MAXDIM], g[MVN_MAXDIM];
+  for (int j = 0; j < a.dim; ++j) x[j] = a.x[c * a.dim + j];
+  for (int s = 0; s < a.n_steps; ++s) {
+    const double eps = a.eps[s];
+    const int n = a.n_iter[(size_t)s * a.C + c];
+    for (int j = 0; j < a.dim; ++j) {
+      double z;
+      if (a.noise_mode == HMCX_NOISE_BUFFER) z = a.noise[a.noff[(size_t)s * a.C + c] + j];
+      else z = philox_normal(a.seed, a.chain0 + c, a.step_base + s, 0u, (uint32_t)j);
+      p0[j] = z; p[j] = z; xn[j] = x[j];
+    }
+    mvn_grad(a, x, g);                                   // hmc.py:47
+    const double half = 0.5 * eps;
+    for (int it = 0; it < n; ++it) {                     // hmc.py:49-54 (one var)
+      for (int j = 0; j < a.dim; ++j) p[j] = p[j] - half * g[j];
+      for (int j = 0; j < a.dim; ++j) xn[j] = xn[j] + eps * p[j];
+      mvn_grad(a, xn, g);
+      for (int j = 0; j < a.dim; ++j) p[j] = p[j] - eps * g[j];
+    }
+    double k1 = 0.0, k0 = 0.0;
+    for (int j = 0; j < a.dim; ++j) { p[j] = -p[j]; k1 += p[j] * p[j]; k0 += p0[j] * p0[j]; }
+    const double Enew = mvn_nlp(a, xn) + (0.0 + 0.5 * k1);
+    const double Ecur = mvn_nlp(a, x) + (0.0 + 0.5 * k0);
+    const double ex = exp(Ecur - Enew);
+    const double A = (ex < 1.0) ? ex : 1.0;
+    const int acc = a.u[(size_t)s * a.C + c] < A;
+    if (acc) for (int j = 0; j < a.dim; ++j) x[j] = xn[j];
+    a.out_A[(size_t)s * a.C + c] = A;
+    a.out_acc[(size_t)s * a.C + c] = acc;
+    if (a.out_nlp) a.out_nlp[(size_t)s * a.C + c] = mvn_nlp(a, x);
+    if (a.out_trace)
+      for (int j = 0; j < a.dim; ++j) a.out_trace[((size_t)s * a.C + c) * a.dim + j] = x[j];
+  }
+  for (int j = 0; j < a.dim; ++j) a.x[c * a.dim + j] = x[j];
+}
+
+int hmc_mvn_run(hmcx_ctx* ctx, const hmcx_hmc_mvn_args* s) {
+  if (s->dim < 1 || s->dim > MVN_MAXDIM) return set_error(ctx, HMCX_EUNSUPPORTED, "mvn: dim must be 1..16");
+  const size_t nsc = (size_t)s->n_steps * s->C;
+  Workspace ws(ctx);
+  double *d_eps, *d_u;
+  int32_t* d_n;
+  int64_t* d_off;
+  do {
+    ws.reset();
+    d_eps = ws.take<double>(s->n_steps);
+    d_u = ws.take<double>(nsc);
+    d_n = ws.take<int32_t>(nsc);
+    d_off = ws.take<int64_t>(nsc);
+  } while (ws.retry());
+  if (ws.failed) return HMCX_ENOMEM;
+  begin_call(ctx);
+  int rc;
+  if ((rc = upload(ctx, d_eps, s->eps, s->n_steps * sizeof(double)))) return rc;
+  if ((rc = upload(ctx, d_u, s->u_accept, nsc * sizeof(double)))) return rc;
+  if ((rc = upload(ctx, d_n, s->n_iter, nsc * sizeof(int32_t)))) return rc;
+  if (s->noise_mode == HMCX_NOISE_BUFFER && (rc = upload(ctx, d_off, s->noise_off, nsc * sizeof(int64_t))))
+    return rc;
+  MvnArgs a{};
+  a.dim = s->dim; a.C = s->C; a.n_steps = s->n_steps;
+  a.mu = s->mu; a.prec = s->prec; a.nlp_const = s->nlp_const;
+  a.eps = d_eps; a.n_iter = d_n; a.u = d_u;
+  a.noise_mode = s->noise_mode; a.noise = s->noise; a.noff = d_off;
+  a.seed = s->seed; a.chain0 = s->chain0; a.step_base = s->step_base;
+  a.x = s->x; a.out_A = s->out_A; a.out_acc = s->out_accepted; a.out_nlp = s->out_nlp; a.out_trace = s->out_trace;
+  hipLaunchKernelGGL(k_hmc_mvn, dim3((s->C + 63) / 64), dim3(64), 0, ctx->stream, a);
+  HMCX_HIP(ctx, hipGetLastError());
+  return HMCX_OK;
+}
+
+}  // namespace hmcx
+
+// =================================================================== C ABI
+using namespace hmcx;
+
+#define HMCX_GUARD_CTX(ctx) \
+  if (!(ctx)) return HMCX_EINVAL;
+
+extern "C" {
+
+int hmcx_version(void) { return 10000; }
+
+int hmcx_create(int device, hmcx_ctx** out) {
+  if (!out) return HMCX_EINVAL;
+  *out = nullptr;
+  hmcx_ctx* c = new (std::nothrow) hmcx_ctx();
+  if (!c) return HMCX_ENOMEM;
+  c->device = device;
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->stage_ev, hipEventDisableTiming) != hipSuccess) {
+    delete c;
+    return HMCX_EHIP;
+  }
+  c->stream = c->own_stream;
+  *out = c;
+  return HMCX_OK;
+}
+
+int hmcx_destroy(hmcx_ctx* ctx) {
+  HMCX_GUARD_CTX(ctx);
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->ws) (void)hipFree(ctx->ws);
+  if (ctx->stage) (void)hipHostFree(ctx->stage);
+  if (ctx->stage_ev) (void)hipEventDestroy(ctx->stage_ev);
+  if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
+  delete ctx;
+  return HMCX_OK;
+}
+
+const char* hmcx_last_error(const hmcx_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int hmcx_set_stream(hmcx_ctx* ctx, void* stream) {
+  HMCX_GUARD_CTX(ctx);
+  ctx->stream = stream ? (hipStream_t)stream : ctx->own_stream;
+  return HMCX_OK;
+}
+
+int hmcx_synchronize(hmcx_ctx* ctx) {
+  HMCX_GUARD_CTX(ctx);
+  HMCX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return HMCX_OK;
+}
+
+int hmcx_set_graph_mode(hmcx_ctx* ctx, int enabled) {
+  HMCX_GUARD_CTX(ctx);
+  ctx->graph_mode = enabled ? 1 : 0;
+  return HMCX_OK;
+}
+
+void hmcx_philox_uniforms(uint64_t seed, uint32_t chain, uint32_t step, uint32_t slot, uint32_t n, double* out) {
+  for (uint32_t i = 0; i < n; ++i) out[i] = philox_uniform(seed, chain, step, slot, i);
+}
+
+void hmcx_philox_normals(uint64_t seed, uint32_t chain, uint32_t step, uint32_t slot, uint32_t e0, uint32_t n,
+                         double* out) {
+  for (uint32_t i = 0; i < n; ++i) out[i] = philox_normal(seed, chain, step, slot, e0 + i);
+}
+
+static int check_dims(hmcx_ctx* ctx, int dtype, int B, int D, int K, int C) {
+  if (dtype != HMCX_F32 && dtype != HMCX_F64) return set_error(ctx, HMCX_EINVAL, "dtype must be HMCX_F32/HMCX_F64");
+  if (B < 1 || D < 1 || K < 1 || C < 1) return set_error(ctx, HMCX_EINVAL, "B, D, K, C must be >= 1");
+  if (K > 64) return set_error(ctx, HMCX_EUNSUPPORTED, "K > 64 classes not built");
+  return HMCX_OK;
+}
+
+int hmcx_softmax_grad(hmcx_ctx* ctx, int dtype, const void* X, const void* Y, int B, int D, int K, int C,
+                      const void* W, const void* b, double alpha, void* gW, void* gb) {
+  HMCX_GUARD_CTX(ctx);
+  int rc = check_dims(ctx, dtype, B, D, K, C);
+  if (rc) return rc;
+  if (!X || !Y || !W || !b || !gW || !gb) return set_error(ctx, HMCX_EINVAL, "null pointer");
+  return dtype == HMCX_F64 ? softmax_grad_t<double>(ctx, X, Y, B, D, K, C, W, b, alpha, gW, gb)
+                           : softmax_grad_t<float>(ctx, X, Y, B, D, K, C, W, b, alpha, gW, gb);
+}
+
+int hmcx_softmax_loglik(hmcx_ctx* ctx, int dtype, const void* X, const void* Y, int B, int D, int K, int C,
+                        const void* W, const void* b, double* ll) {
+  HMCX_GUARD_CTX(ctx);
+  int rc = check_dims(ctx, dtype, B, D, K, C);
+  if (rc) return rc;
+  if (!X || !Y || !W || !b || !ll) return set_error(ctx, HMCX_EINVAL, "null pointer");
+  return dtype == HMCX_F64 ? softmax_loglik_t<double>(ctx, X, Y, B, D, K, C, W, b, ll)
+                           : softmax_loglik_t<float>(ctx, X, Y, B, D, K, C, W, b, ll);
+}
+
+int hmcx_softmax_predict(hmcx_ctx* ctx, int dtype, const void* X, int B, int D, int K, int C, const void* W,
+                         const void* b, void* prob) {
+  HMCX_GUARD_CTX(ctx);
+  int rc = check_dims(ctx, dtype, B, D, K, C);
+  if (rc) return rc;
+  if (!X || !W || !b || !prob) return set_error(ctx, HMCX_EINVAL, "null pointer");
+  return dtype == HMCX_F64 ? softmax_predict_t<double>(ctx, X, B, D, K, C, W, b, prob)
+                           : softmax_predict_t<float>(ctx, X, B, D, K, C, W, b, prob);
+}
+
+static int check_sampler(hmcx_ctx* ctx, const hmcx_sampler_args* a, bool sghmc) {
+  if (!a) return set_error(ctx, HMCX_EINVAL, "null args");
+  int rc = check_dims(ctx, a->dtype, a->B, a->D, a->K, a->C);
+  if (rc) return rc;
+  if (a->n_steps < 0) return set_error(ctx, HMCX_EINVAL, "n_steps < 0");
+  if (!a->X || !a->Y || !a->W || !a->b || !a->row0 || !a->eps) return set_error(ctx, HMCX_EINVAL, "null pointer");
+  if (sghmc && (!a->n_iter || !a->u_accept || !a->out_A || !a->out_accepted || !a->out_ll))
+    return set_error(ctx, HMCX_EINVAL, "sghmc: n_iter/u_accept/out_* required");
+  if (a->noise_mode == HMCX_NOISE_BUFFER && (!a->noise || !a->noise_off))
+    return set_error(ctx, HMCX_EINVAL, "BUFFER noise mode needs noise and noise_off");
+  if (a->noise_mode != HMCX_NOISE_BUFFER && a->noise_mode != HMCX_NOISE_PHILOX)
+    return set_error(ctx, HMCX_EINVAL, "bad noise_mode");
+  if ((long long)a->D * a->K + a->K > 0x7fffffffLL) return set_error(ctx, HMCX_EUNSUPPORTED, "too many parameters");
+  return HMCX_OK;
+}
+
+int hmcx_sghmc_run(hmcx_ctx* ctx, const hmcx_sampler_args* a) {
+  HMCX_GUARD_CTX(ctx);
+  int rc = check_sampler(ctx, a, true);
+  if (rc) return rc;
+  if (a->n_steps == 0) return HMCX_OK;
+  return a->dtype == HMCX_F64 ? sghmc_run_t<double>(ctx, a) : sghmc_run_t<float>(ctx, a);
+}
+
+int hmcx_sgld_run(hmcx_ctx* ctx, const hmcx_sampler_args* a) {
+  HMCX_GUARD_CTX(ctx);
+  int rc = check_sampler(ctx, a, false);
+  if (rc) return rc;
+  if (a->n_steps == 0) return HMCX_OK;
+  return a->dtype == HMCX_F64 ? sgld_run_t<double>(ctx, a) : sgld_run_t<float>(ctx, a);
+}
+
+int hmcx_hmc_mvn_run(hmcx_ctx* ctx, const hmcx_hmc_mvn_args* a) {
+  HMCX_GUARD_CTX(ctx);
+  if (!a || !a->mu || !a->prec || !a->x || !a->eps || !a->n_iter || !a->u_accept || !a->out_A || !a->out_accepted)
+    return set_error(ctx, HMCX_EINVAL, "hmc_mvn: null pointer");
+  if (a->C < 1 || a->n_steps < 0) return set_error(ctx, HMCX_EINVAL, "hmc_mvn: bad sizes");
+  if (a->noise_mode == HMCX_NOISE_BUFFER && (!a->noise || !a->noise_off))
+    return set_error(ctx, HMCX_EINVAL, "BUFFER noise mode needs noise and noise_off");
+  if (a->n_steps == 0) return HMCX_OK;
+  return hmc_mvn_run(ctx, a);
+}
+
+}  // extern "C"

@@ -1,0 +1,134 @@
+// hmcx_internal.h — context, workspace, kernel argument blocks (not part of the C ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+#include <vector>
+#include <algorithm>
+#include "hmcx.h"
+
+struct hmcx_ctx {
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  std::string err;
+  int graph_mode = 0;
+  // device workspace (grows; freed only after a stream sync)
+  char* ws = nullptr;
+  size_t ws_cap = 0;
+  // pinned host staging for per-call schedules
+  char* stage = nullptr;
+  size_t stage_cap = 0;
+  size_t stage_off = 0;
+  hipEvent_t stage_ev = nullptr;
+  bool stage_pending = false;
+};
+
+namespace hmcx {
+
+// softmax.py:40-41 clip bounds, exact float64 values (-log(eps), -log(1/tiny - 1)).
+constexpr double CLIP_HI = 0x1.205966f2b4f12p+5;    //  36.04365338911715
+constexpr double CLIP_LO = -0x1.6232bdd7abcd2p+9;   // -708.3964185322641
+
+int set_error(hmcx_ctx* ctx, int code, const std::string& msg);
+
+#define HMCX_HIP(ctx, expr)                                                                  \
+  do {                                                                                       \
+    hipError_t e_ = (expr);                                                                  \
+    if (e_ != hipSuccess)                                                                    \
+      return ::hmcx::set_error((ctx), HMCX_EHIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+// Sub-allocates one call's buffers from the context workspace (256-B aligned):
+//   Workspace ws(ctx); do { ws.reset(); p = ws.take<T>(n); ... } while (ws.retry());
+// retry() grows the workspace (after a stream sync) when the takes overflowed it.
+struct Workspace {
+  hmcx_ctx* ctx;
+  size_t off = 0;
+  bool failed = false;
+  explicit Workspace(hmcx_ctx* c) : ctx(c) {}
+  void reset() { off = 0; }
+  template <typename T> T* take(size_t n) {
+    const size_t bytes = ((n * sizeof(T) + 255) / 256) * 256 + 256;
+    T* p = (off + bytes <= ctx->ws_cap) ? reinterpret_cast<T*>(ctx->ws + off) : nullptr;
+    off += bytes;
+    return p;
+  }
+  bool retry();
+};
+
+struct Tiling {
+  int CB, NBLK, nCT, nRB, nDB;
+};
+Tiling make_tiling(int B, int D, int K, int C);
+
+enum FwdMode { FWD_GRAD = 0, FWD_SGHMC = 1, FWD_LL = 2, FWD_PRED = 3 };
+enum GradMode { GRAD_OUT = 0, GRAD_SGHMC = 1, GRAD_SGLD = 2 };
+
+template <typename T> struct FwdArgs {
+  const T* X; const T* Y; const T* W; const T* b; const T* pb;
+  int B, D, K, C, N, CB;
+  int mode;
+  T eps, clip_hi, clip_lo;
+  int iter;
+  const int32_t* n_iter;
+  T* diff; T* colsum_part; double* ll_part; T* prob;
+};
+
+template <typename T> struct GradArgs {
+  const T* X; const T* diff; const T* colsum_part;
+  int B, D, K, C, N, CB, nRB, P;
+  int mode;
+  T alpha, eps, one_minus_eps, noise_scale, m_half_eps;
+  int iter;
+  const int32_t* n_iter;
+  const T* Wsrc; const T* bsrc;
+  T* W; T* b; T* pW; T* pb; T* gW; T* gb;
+  int noise_mode; const double* noise; const int64_t* noff;
+  uint64_t seed; uint32_t chain0, step, slot;
+};
+
+template <typename T> struct InitArgs {
+  int D, K, C, N;
+  T eps;
+  const int32_t* n_iter;
+  int noise_mode; const double* noise; const int64_t* noff;
+  uint64_t seed; uint32_t chain0, step;
+  const T* W; const T* b;
+  T* Wwork; T* bwork; T* pW; T* pb; T* p0W; T* p0b;
+};
+
+template <typename T> struct AcceptArgs {
+  int D, K, C, N, nRB;
+  const int32_t* n_iter; const double* u;
+  double neg_inv_n, log_prior;
+  const T* p0W; const T* p0b; const T* pW; const T* pb;
+  const double* ll0_part; const double* ll1_part;
+  const T* Wwork; const T* bwork; T* W; T* b;
+  double* out_A; int32_t* out_acc; double* out_ll; double* out_E;
+};
+
+// Copy a host array to device through the context's pinned staging buffer (stream-ordered).
+int upload(hmcx_ctx* ctx, void* dst, const void* src, size_t bytes);
+void begin_call(hmcx_ctx* ctx);
+
+// Optional hipGraph capture of one run call (hmcx_set_graph_mode).
+struct GraphScope {
+  hmcx_ctx* ctx;
+  bool capturing = false;
+  explicit GraphScope(hmcx_ctx* c);
+  int finish();
+  ~GraphScope();
+};
+
+template <typename T> int softmax_grad_t(hmcx_ctx*, const void*, const void*, int, int, int, int, const void*,
+                                         const void*, double, void*, void*);
+template <typename T> int softmax_loglik_t(hmcx_ctx*, const void*, const void*, int, int, int, int, const void*,
+                                           const void*, double*);
+template <typename T> int softmax_predict_t(hmcx_ctx*, const void*, int, int, int, int, const void*, const void*,
+                                            void*);
+template <typename T> int sghmc_run_t(hmcx_ctx*, const hmcx_sampler_args*);
+template <typename T> int sgld_run_t(hmcx_ctx*, const hmcx_sampler_args*);
+int hmc_mvn_run(hmcx_ctx*, const hmcx_hmc_mvn_args*);
+
+}  // namespace hmcx

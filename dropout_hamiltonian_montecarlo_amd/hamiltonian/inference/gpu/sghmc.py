@@ -1,0 +1,125 @@
+"""SGHMC sampler — drop-in for hamiltonian/inference/{cpu,gpu}/sghmc.py.
+
+Reference step: /root/reference/hamiltonian/inference/cpu/sghmc.py:19-39, run with the A1
+completion: momentum ~ N(0,1) (cpu/hmc.py:82-87), MH accept
+A = min(1, exp(E_cur − E_new)) with E = negative_log_posterior + ½Σp² (cpu/hmc.py:67-79),
+the ``+ε·∇U`` momentum sign and 2ε noise std (sghmc.py:31,34), no momentum negation, and a
+NaN energy difference accepted (Python ``min``).  The dead ``grad(q)`` of sghmc.py:26 is not
+executed (it has no effect and consumes no randomness).
+
+The whole trajectory of every step runs inside libhmcx (hmcx_sghmc_run): per leapfrog
+iteration one k_fwd + one k_grad launch; the host only prepares the per-step schedule.
+"""
+import numpy as np
+import torch
+
+from dropout_hamiltonian_montecarlo_amd import _native as nat
+from dropout_hamiltonian_montecarlo_amd._native import HmcxError, ptr
+
+from .sgmcmc import RunResult, sgmcmc
+
+
+def _n_iter(path_length):
+    """len(np.arange(path_length - 1)) for the float path length of sghmc.py:25,28."""
+    if not np.isfinite(path_length):
+        raise HmcxError("non-finite path length (step size 0?)")
+    return max(0, int(np.ceil(path_length - 1)))
+
+
+class sghmc(sgmcmc):
+
+    def _check_vars(self):
+        if self.model._hmcx_model != 'softmax' or list(self.start.keys()) != ['weights', 'bias']:
+            raise HmcxError("sghmc: libhmcx implements the softmax model with start_p keys "
+                            "['weights', 'bias'] (in that order, sghmc.py:29)")
+
+    # ------------------------------------------------------------------ schedule
+    def _schedule(self, n_steps, eps, rng, P):
+        """Host-side randomness of n_steps steps, in the reference's draw order."""
+        n_iter = np.empty(n_steps, dtype=np.int32)
+        u = np.empty(n_steps, dtype=np.float64)
+        noise_off = np.zeros(n_steps, dtype=np.int64)
+        chunks = []
+        off = 0
+        for s in range(n_steps):
+            e = eps[s]
+            if self.noise == 'numpy':
+                # sghmc.py:21 momentum (rng) → :25 path length (global np.random) → :31 per-iteration
+                # noise rng.normal(0, 2ε) = 2ε·N(0,1) (scaled on the device) → :36 accept uniform.
+                L = np.ceil(2 * np.random.rand() * self.path_length / e)
+                ni = _n_iter(L)
+                z = rng.standard_normal(P * (1 + ni))
+                chunks.append(z)
+                noise_off[s] = off
+                off += z.size
+                u[s] = np.random.rand()
+            else:
+                g = (self.global_step + s) & 0xFFFFFFFF
+                uL = nat.philox_uniforms(self.seed, self.chain, g, nat.SLOT_PATH, 1)[0]
+                L = np.ceil(2 * uL * self.path_length / e)
+                ni = _n_iter(L)
+                u[s] = nat.philox_uniforms(self.seed, self.chain, g, nat.SLOT_ACCEPT, 1)[0]
+            n_iter[s] = ni
+            if self.trace is not None:
+                self.trace.append({'L': float(L), 'eps': float(e)})
+        noise = np.concatenate(chunks) if chunks else None
+        return n_iter, u, noise, noise_off
+
+    def _run(self, state, data, rows, eps, rng, batch_size):
+        Xd, Yd = data
+        W, b = state['weights'], state['bias']
+        D, K = W.shape
+        P = D * K + K
+        n_steps = len(rows)
+        n_iter, u, noise, noise_off = self._schedule(n_steps, eps, rng, P)
+        dev = self.model.device
+        noise_d = torch.from_numpy(noise).to(dev) if noise is not None else None
+        out_A = torch.empty(n_steps, dtype=torch.float64, device=dev)
+        out_acc = torch.empty(n_steps, dtype=torch.int32, device=dev)
+        out_ll = torch.empty(n_steps, dtype=torch.float64, device=dev)
+        out_E = torch.empty(2 * n_steps, dtype=torch.float64, device=dev)
+        row0 = np.asarray(rows, dtype=np.int64)
+        eps_a = np.asarray(eps, dtype=np.float64)
+        a = nat.SamplerArgs()
+        a.dtype = self.model.code
+        a.B, a.D, a.K, a.C = batch_size, D, K, 1
+        a.n_steps = n_steps
+        a.alpha = self.model.alpha
+        a.log_prior = self._log_prior()
+        a.X, a.Y = ptr(Xd), ptr(Yd)
+        a.row0 = row0.ctypes.data_as(nat.c_i64p)
+        a.eps = eps_a.ctypes.data_as(nat.c_dblp)
+        a.n_iter = n_iter.ctypes.data_as(nat.c_i32p)
+        a.u_accept = u.ctypes.data_as(nat.c_dblp)
+        a.noise_mode = nat.NOISE_BUFFER if self.noise == 'numpy' else nat.NOISE_PHILOX
+        a.noise = ptr(noise_d)
+        a.noise_off = noise_off.ctypes.data_as(nat.c_i64p)
+        a.seed, a.chain0, a.step_base = self.seed, self.chain, self.global_step & 0xFFFFFFFF
+        a.W, a.b = ptr(W), ptr(b)
+        a.out_A, a.out_accepted, a.out_ll, a.out_E = ptr(out_A), ptr(out_acc), ptr(out_ll), ptr(out_E)
+        ctx = nat.context(dev)
+        ctx.check(ctx.lib.hmcx_sghmc_run(ctx.h, a), "hmcx_sghmc_run")
+        self.global_step += n_steps
+        res = RunResult(out_A.cpu().numpy(), out_acc.cpu().numpy().astype(bool), out_ll.cpu().numpy(),
+                        out_E.cpu().numpy().reshape(n_steps, 2))
+        del noise_d
+        if self.trace is not None:
+            for s in range(n_steps):
+                t = self.trace[len(self.trace) - n_steps + s]
+                t['A'] = float(res.A[s])
+                t['accepted'] = bool(res.accepted[s])
+        return res
+
+    # ------------------------------------------------------------------ single step (API parity)
+    def step(self, state, momentum, rng, **args):                         # sghmc.py:19-39
+        """One SGHMC step on the given minibatch; returns (q, None, acceptprob).
+
+        q is a dict of device tensors.  The final momentum stays on the device (the reference
+        returns it but ``sample`` discards it; draw_momentum redraws it every step)."""
+        X, y = args['X_train'], args['y_train']
+        data = self._upload_data(X, y)
+        st = {var: torch.as_tensor(np.asarray(state[var]) if not isinstance(state[var], torch.Tensor)
+                                   else state[var]).to(self.model.device, self.model.dtype).contiguous().clone()
+              for var in self.start}
+        res = self._run(st, data, [0], [self.step_size], rng, data[0].shape[0])
+        return st, None, float(res.A[0])

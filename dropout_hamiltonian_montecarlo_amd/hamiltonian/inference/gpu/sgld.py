@@ -1,0 +1,75 @@
+"""SGLD sampler — drop-in for hamiltonian/inference/cpu/sgld.py.
+
+Reference step: /root/reference/hamiltonian/inference/cpu/sgld.py:31-46:
+    p = N(0, (2ε)²)  (draw_momentum, noise_scale = 2ε);  p += −½ε·∇U(q);  q += p.
+The CuPy file's variant p = ν⊙p_prev − ½ε∇U (gpu/sgld.py:11-20) is NOT the
+default; the NumPy semantics are the parity target.
+
+One SGLD step = one k_fwd + one k_grad launch (hmcx_sgld_run); the log-likelihood the
+reference prints every 10 minibatches costs one extra forward launch on those steps only.
+"""
+import numpy as np
+import torch
+
+from dropout_hamiltonian_montecarlo_amd import _native as nat
+from dropout_hamiltonian_montecarlo_amd._native import HmcxError, ptr
+
+from .sgmcmc import RunResult, sgmcmc
+
+
+class sgld(sgmcmc):
+
+    def _check_vars(self):
+        if self.model._hmcx_model != 'softmax' or list(self.start.keys()) != ['weights', 'bias']:
+            raise HmcxError("sgld: libhmcx implements the softmax model with start_p keys ['weights', 'bias']")
+
+    def _run(self, state, data, rows, eps, rng, batch_size):
+        Xd, Yd = data
+        W, b = state['weights'], state['bias']
+        D, K = W.shape
+        P = D * K + K
+        n_steps = len(rows)
+        dev = self.model.device
+        noise_off = np.arange(n_steps, dtype=np.int64) * P
+        noise_d = None
+        if self.noise == 'numpy':
+            # sgld.py:45: rng.normal(0, 2ε, shape) per var = 2ε·N(0,1) (scaled on the device)
+            noise_d = torch.from_numpy(rng.standard_normal(P * n_steps)).to(dev)
+        want = np.zeros(n_steps, dtype=np.uint8)
+        want[::self.log_every] = 1
+        want[-1] = 1
+        out_ll = torch.zeros(n_steps, dtype=torch.float64, device=dev)
+        row0 = np.asarray(rows, dtype=np.int64)
+        eps_a = np.asarray(eps, dtype=np.float64)
+        a = nat.SamplerArgs()
+        a.dtype = self.model.code
+        a.B, a.D, a.K, a.C = batch_size, D, K, 1
+        a.n_steps = n_steps
+        a.alpha = self.model.alpha
+        a.log_prior = self._log_prior()
+        a.X, a.Y = ptr(Xd), ptr(Yd)
+        a.row0 = row0.ctypes.data_as(nat.c_i64p)
+        a.eps = eps_a.ctypes.data_as(nat.c_dblp)
+        a.want_ll = want.ctypes.data_as(nat.c_u8p)
+        a.noise_mode = nat.NOISE_BUFFER if self.noise == 'numpy' else nat.NOISE_PHILOX
+        a.noise = ptr(noise_d)
+        a.noise_off = noise_off.ctypes.data_as(nat.c_i64p)
+        a.seed, a.chain0, a.step_base = self.seed, self.chain, self.global_step & 0xFFFFFFFF
+        a.W, a.b = ptr(W), ptr(b)
+        a.out_ll = ptr(out_ll)
+        ctx = nat.context(dev)
+        ctx.check(ctx.lib.hmcx_sgld_run(ctx.h, a), "hmcx_sgld_run")
+        self.global_step += n_steps
+        ll = out_ll.cpu().numpy()
+        if self.trace is not None:
+            self.trace.extend({'L': 1.0, 'A': 1.0, 'accepted': True, 'eps': float(e)} for e in eps)
+        return RunResult(np.ones(n_steps), np.ones(n_steps, dtype=bool), ll)
+
+    def step(self, state, momentum, rng, **args):                         # sgld.py:31-39
+        X, y = args['X_train'], args['y_train']
+        data = self._upload_data(X, y)
+        st = {var: torch.as_tensor(np.asarray(state[var]) if not isinstance(state[var], torch.Tensor)
+                                   else state[var]).to(self.model.device, self.model.dtype).contiguous().clone()
+              for var in self.start}
+        self._run(st, data, [0], [self.step_size], rng, data[0].shape[0])
+        return st, None

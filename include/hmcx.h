@@ -1,0 +1,147 @@
+/* hmcx.h — C ABI of the MI355X-native SG-HMC engine (libhmcx.so).
+ *
+ * The reference (sherna90/dropout_hamiltonian_montecarlo) has no FFI: its boundary is a
+ * duck-typed Python protocol.  This header is the boundary the Python host
+ * layer (dropout_hamiltonian_montecarlo_amd/hamiltonian/...) binds through ctypes; each
+ * entry point names the reference interface it replaces.
+ *
+ * Conventions
+ *  - All array pointers are DEVICE pointers (caller-owned, e.g. torch tensors), row-major
+ *    and contiguous, unless the comment says "host".
+ *  - C independent chains are stored chain-interleaved so the two gradient GEMMs see one
+ *    [rows x C*K] matrix: weights W[D][C][K], bias b[C][K]  (C = 1 is exactly the
+ *    reference's {'weights': [D,K], 'bias': [K]} layout).
+ *  - dtype: HMCX_F64 (the reference's float64) or HMCX_F32.
+ *  - Return 0 on success or a negative hmcx_status; hmcx_last_error() has the message.
+ *    No C++ exception crosses the ABI.  A context is bound to one device, owns its
+ *    workspace and (unless hmcx_set_stream is used) its HIP stream; it is not thread-safe.
+ *  - Every call is asynchronous on the context stream; results are ready after
+ *    hmcx_synchronize() (or any stream-ordered consumer).
+ */
+#ifndef HMCX_H
+#define HMCX_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct hmcx_ctx hmcx_ctx;
+
+enum hmcx_dtype { HMCX_F32 = 0, HMCX_F64 = 1 };
+enum hmcx_noise { HMCX_NOISE_BUFFER = 0, HMCX_NOISE_PHILOX = 1 };
+enum hmcx_status {
+  HMCX_OK = 0,
+  HMCX_EINVAL = -1,       /* bad argument / shape */
+  HMCX_EHIP = -2,         /* HIP runtime error */
+  HMCX_ENOMEM = -3,       /* device allocation failed */
+  HMCX_EUNSUPPORTED = -4  /* shape/dtype combination not built */
+};
+
+/* ------------------------------------------------------------------ context */
+int hmcx_version(void);
+int hmcx_create(int device, hmcx_ctx** out);
+int hmcx_destroy(hmcx_ctx* ctx);
+const char* hmcx_last_error(const hmcx_ctx* ctx);
+/* Use an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream); NULL restores the own stream. */
+int hmcx_set_stream(hmcx_ctx* ctx, void* hip_stream);
+int hmcx_synchronize(hmcx_ctx* ctx);
+/* Capture each hmcx_*_run call into a hipGraph and replay it (1) or launch eagerly (0). */
+int hmcx_set_graph_mode(hmcx_ctx* ctx, int enabled);
+
+/* Philox4x32-10 uniforms in [0,1), bit-identical to the device generator (host function). */
+void hmcx_philox_uniforms(uint64_t seed, uint32_t chain, uint32_t step, uint32_t slot,
+                          uint32_t n, double* out /* host [n] */);
+/* Philox standard normals for slot/element range (host function; used by tests). */
+void hmcx_philox_normals(uint64_t seed, uint32_t chain, uint32_t step, uint32_t slot,
+                         uint32_t e0, uint32_t n, double* out /* host [n] */);
+
+/* ------------------------------------------------------------------ softmax model
+ * Replaces hamiltonian/models/cpu/softmax.py:45-61 (grad) and gpu/softmax.py:53-69.
+ * X [B][D], Y [B][K] one-hot (dtype), W [D][C*K], b [C*K]  ->  gW [D][C*K], gb [C*K]
+ * grad = -(Xᵀ(Y - softmax(clip(XW+b))) - alpha*theta)                                  */
+int hmcx_softmax_grad(hmcx_ctx* ctx, int dtype, const void* X, const void* Y, int B, int D, int K,
+                      int C, const void* W, const void* b, double alpha, void* gW, void* gb);
+
+/* Replaces softmax.py:63-72 (log_likelihood): ll[c] = Σ_rows Σ_k y·(z − logsumexp z), z = clip(XW+b).
+ * ll: device double[C]. */
+int hmcx_softmax_loglik(hmcx_ctx* ctx, int dtype, const void* X, const void* Y, int B, int D, int K,
+                        int C, const void* W, const void* b, double* ll);
+
+/* Replaces softmax.py:38-43,82-89 (net / predict(prob=True)): prob [B][C*K]. */
+int hmcx_softmax_predict(hmcx_ctx* ctx, int dtype, const void* X, int B, int D, int K, int C,
+                         const void* W, const void* b, void* prob);
+
+/* ------------------------------------------------------------------ samplers
+ * One call enqueues n_steps consecutive sampler steps for C chains that share each
+ * minibatch; the minibatch of step s is rows [row0[s], row0[s]+B) of X / Y.
+ * noise_mode BUFFER: `noise` (device double) holds standard normals; the block of
+ * (step s, chain c) starts at noise_off[s*C+c] and is laid out exactly in the
+ * reference's draw order, P = D*K + K values per draw: SGHMC = momentum then one
+ * draw per leapfrog iteration (weights then bias each); SGLD = one draw per step.
+ * noise_mode PHILOX: normals come from Philox(seed, chain0+c, step_base+s, slot, elem). */
+typedef struct hmcx_sampler_args {
+  int dtype;
+  int B, D, K, C;          /* minibatch rows, features, classes, chains in this call   */
+  int n_steps;
+  double alpha;            /* Gaussian prior precision (hyper['alpha'])               */
+  double log_prior;        /* constant log_prior (cpu softmax.py:22-30), host-computed */
+  const void* X;           /* device [N][D] (dtype)                                    */
+  const void* Y;           /* device [N][K] (dtype, one-hot)                           */
+  const int64_t* row0;     /* host [n_steps]                                           */
+  const double* eps;       /* host [n_steps]  step size used by step s                */
+  const int32_t* n_iter;   /* host [n_steps*C] SGHMC leapfrog iterations max(0, L-1)   */
+  const double* u_accept;  /* host [n_steps*C] accept uniforms (SGHMC)                 */
+  const uint8_t* want_ll;  /* host [n_steps] or NULL: SGLD computes ll(q_new) after s  */
+  int noise_mode;
+  const double* noise;     /* device, BUFFER mode                                      */
+  const int64_t* noise_off;/* host [n_steps*C], BUFFER mode                            */
+  uint64_t seed;           /* PHILOX mode                                              */
+  uint32_t chain0;         /* PHILOX: global id of chain 0 of this call               */
+  uint32_t step_base;      /* PHILOX: global step id of step 0 of this call           */
+  void* W;                 /* device [D][C*K] state, updated in place                  */
+  void* b;                 /* device [C*K]                                              */
+  double* out_A;           /* device [n_steps*C] accept probability (SGHMC)            */
+  int32_t* out_accepted;   /* device [n_steps*C]                                       */
+  double* out_ll;          /* device [n_steps*C] log_likelihood(q_after, batch)        */
+  double* out_E;           /* device [n_steps*C*2] (E_current, E_new) or NULL          */
+} hmcx_sampler_args;
+
+/* Replaces hamiltonian/inference/{cpu,gpu}/sghmc.py:19-39 (step, with the A1 completion:
+ * momentum ~ N(0,1), MH accept min(1, exp(E_cur - E_new)) from cpu/hmc.py:67-87). */
+int hmcx_sghmc_run(hmcx_ctx* ctx, const hmcx_sampler_args* a);
+
+/* Replaces hamiltonian/inference/cpu/sgld.py:31-46 (step): p = N(0,(2ε)²) − ½ε∇U; q += p. */
+int hmcx_sgld_run(hmcx_ctx* ctx, const hmcx_sampler_args* a);
+
+/* ------------------------------------------------------------------ full-batch HMC, MVN model
+ * Replaces cpu/hmc.py:39-64 with models/cpu/mvn_gaussian.py (config 1).
+ * x [C][dim] state; mu [dim]; prec [dim][dim] = inv(cov); nlp_const = dim·log2π + log det cov,
+ * nlp(x) = 0.5·(nlp_const + (x−μ)ᵀ·prec·(x−μ))  (mvn_gaussian.py:27-30 op order).
+ * momentum/accept randomness as in hmcx_sampler_args (BUFFER: noise_off per step/chain, dim
+ * normals per step).  out_nlp = nlp(q after step). */
+typedef struct hmcx_hmc_mvn_args {
+  int dim, C, n_steps;
+  const double* mu;        /* device [dim] */
+  const double* prec;      /* device [dim][dim] */
+  double nlp_const;
+  const double* eps;       /* host [n_steps] */
+  const int32_t* n_iter;   /* host [n_steps*C] */
+  const double* u_accept;  /* host [n_steps*C] */
+  int noise_mode;
+  const double* noise;
+  const int64_t* noise_off;
+  uint64_t seed;
+  uint32_t chain0, step_base;
+  double* x;               /* device [C][dim] */
+  double* out_A;
+  int32_t* out_accepted;
+  double* out_nlp;
+  double* out_trace;       /* device [n_steps][C][dim] or NULL */
+} hmcx_hmc_mvn_args;
+int hmcx_hmc_mvn_run(hmcx_ctx* ctx, const hmcx_hmc_mvn_args* a);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HMCX_H */

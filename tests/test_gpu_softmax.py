@@ -1,0 +1,138 @@
+"""GPU parity: libhmcx softmax gradient / log-likelihood / predict vs the NumPy oracle
+(oracle/models.py, itself pinned bit-exact to the reference's golden vectors).
+
+Tolerances (stated per test): float64 kernels differ from NumPy only by GEMM summation
+order → rel 1e-12 of the |X|ᵀ|Ŷ−Y| + α|W| scale; float32 kernels → 2e-5 of that scale."""
+import ctypes
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from oracle import inputs as gi  # noqa: E402
+from oracle import models as om  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def model64():
+    from dropout_hamiltonian_montecarlo_amd.hamiltonian.models.gpu.softmax import softmax
+    return softmax({"alpha": 0.01}, dtype=torch.float64, device="cuda:0")
+
+
+@pytest.fixture(scope="module")
+def model32():
+    from dropout_hamiltonian_montecarlo_amd.hamiltonian.models.gpu.softmax import softmax
+    return softmax({"alpha": 0.01}, dtype=torch.float32, device="cuda:0")
+
+
+def _scale(X, Y, W, b, alpha):
+    m = om.softmax({"alpha": alpha})
+    R = np.abs(m.net({"weights": W, "bias": b}, X) - Y)
+    return np.abs(X).T @ R + alpha * np.abs(W), R.sum(0) + alpha * np.abs(b)
+
+
+@pytest.mark.parametrize("case", gi.GRAD_CASES + [(7, 500, 0.01, 2048, 38), (8, 77, 0.3, 33, 3)])
+def test_grad_f64(model64, case):
+    seed, B, ws = case[:3]
+    D, K = (case[3], case[4]) if len(case) > 3 else (784, 10)
+    X, Y, W, b = gi.softmax_inputs(seed, B, D=D, K=K, wscale=ws)
+    ref = om.softmax({"alpha": 0.01}).grad({"weights": W, "bias": b}, X_train=X, y_train=Y)
+    g = model64.grad({"weights": W, "bias": b}, X_train=X, y_train=Y)
+    sW, sb = _scale(X, Y, W, b, 0.01)
+    assert np.all(np.abs(g["weights"].cpu().numpy() - ref["weights"]) <= 1e-12 * sW + 1e-300)
+    assert np.all(np.abs(g["bias"].cpu().numpy() - ref["bias"]) <= 1e-12 * sb + 1e-300)
+
+
+@pytest.mark.parametrize("case", [(0, 500, 0.01), (1, 32, 0.01), (4, 64, 50.0)])
+def test_grad_f32(model32, case):
+    seed, B, ws = case
+    X, Y, W, b = gi.softmax_inputs(seed, B, wscale=ws)
+    ref = om.softmax({"alpha": 0.01}).grad({"weights": W, "bias": b}, X_train=X, y_train=Y)
+    g = model32.grad({"weights": W, "bias": b}, X_train=X, y_train=Y)
+    sW, sb = _scale(X, Y, W, b, 0.01)
+    assert np.all(np.abs(g["weights"].cpu().numpy() - ref["weights"]) <= 2e-5 * (sW + 1))
+    assert np.all(np.abs(g["bias"].cpu().numpy() - ref["bias"]) <= 2e-5 * (sb + 1))
+
+
+@pytest.mark.parametrize("case", [(0, 500, 0.01), (2, 32, 0.01), (3, 64, 5.0), (4, 64, 50.0), (5, 1, 0.01)])
+def test_loglik_nlp_predict_f64(model64, case):
+    seed, B, ws = case
+    X, Y, W, b = gi.softmax_inputs(seed, B, wscale=ws)
+    par = {"weights": W, "bias": b}
+    m = om.softmax({"alpha": 0.01})
+    ll_ref = m.log_likelihood(par, X_train=X, y_train=Y)
+    ll = model64.log_likelihood(par, X_train=X, y_train=Y)
+    assert abs(ll - ll_ref) <= 1e-12 * max(1.0, abs(ll_ref)) * np.sqrt(B)
+    nlp_ref = m.negative_log_posterior(par, X_train=X, y_train=Y)
+    assert abs(model64.negative_log_posterior(par, X_train=X, y_train=Y) - nlp_ref) <= 1e-11 * abs(nlp_ref)
+    assert model64.log_prior(par) == m.log_prior(par)
+    assert model64.loss(par, X_train=X, y_train=Y) == model64.negative_log_posterior(par, X_train=X, y_train=Y)
+    np.testing.assert_allclose(model64.predict(par, X, prob=True), m.predict(par, X, prob=True), rtol=1e-11, atol=1e-300)
+    np.testing.assert_array_equal(model64.predict(par, X), m.predict(par, X))
+
+
+def test_golden_vectors_direct(model64, golden_dir):
+    """The device gradient also matches the reference's own stored outputs."""
+    import json, os
+    d = np.load(os.path.join(golden_dir, "softmax_grad.npz"))
+    meta = json.loads(str(d["meta"]))
+    for i, (seed, B, ws) in enumerate(gi.GRAD_CASES):
+        if not meta["c%d" % i]["full"]:
+            continue
+        X, Y, W, b = gi.softmax_inputs(seed, B, wscale=ws)
+        g = model64.grad({"weights": W, "bias": b}, X_train=X, y_train=Y)
+        np.testing.assert_allclose(g["weights"].cpu().numpy(), d["c%d_gW" % i], rtol=1e-10, atol=1e-10)
+        np.testing.assert_allclose(g["bias"].cpu().numpy(), d["c%d_gb" % i], rtol=1e-10, atol=1e-10)
+
+
+def test_nan_propagates_like_numpy(model64):
+    X, Y, W, b = gi.softmax_inputs(0, 20, D=16, K=4)
+    W[3, 2] = np.nan
+    ref = om.softmax({"alpha": 0.01}).grad({"weights": W, "bias": b}, X_train=X, y_train=Y)
+    g = model64.grad({"weights": W, "bias": b}, X_train=X, y_train=Y)
+    np.testing.assert_array_equal(np.isnan(g["weights"].cpu().numpy()), np.isnan(ref["weights"]))
+
+
+@pytest.mark.parametrize("C", [1, 3, 8, 13])
+def test_multichain_layout(model64, C):
+    """C chains in the interleaved layout W[D][C][K] give C independent gradients."""
+    from dropout_hamiltonian_montecarlo_amd import _native as nat
+    rs = np.random.RandomState(C)
+    B, D, K = 100, 96, 10
+    X, Y, _, _ = gi.softmax_inputs(3, B, D=D, K=K)
+    Ws = rs.normal(0, 0.1, (C, D, K))
+    bs = rs.normal(0, 0.1, (C, K))
+    dev = torch.device("cuda:0")
+    Wd = torch.from_numpy(np.ascontiguousarray(Ws.transpose(1, 0, 2))).to(dev)
+    bd = torch.from_numpy(bs.copy()).to(dev)
+    Xd = torch.from_numpy(X).to(dev)
+    Yd = torch.from_numpy(Y).to(dev)
+    gW = torch.empty_like(Wd)
+    gb = torch.empty_like(bd)
+    ctx = nat.context(0)
+    ctx.check(ctx.lib.hmcx_softmax_grad(ctx.h, nat.HMCX_F64, nat.ptr(Xd), nat.ptr(Yd), B, D, K, C, nat.ptr(Wd),
+                                        nat.ptr(bd), 0.01, nat.ptr(gW), nat.ptr(gb)), "grad")
+    gWh = gW.cpu().numpy().transpose(1, 0, 2)
+    m = om.softmax({"alpha": 0.01})
+    for c in range(C):
+        ref = m.grad({"weights": Ws[c], "bias": bs[c]}, X_train=X, y_train=Y)
+        np.testing.assert_allclose(gWh[c], ref["weights"], rtol=1e-10, atol=1e-11)
+        np.testing.assert_allclose(gb.cpu().numpy()[c], ref["bias"], rtol=1e-10, atol=1e-11)
+    ll = torch.empty(C, dtype=torch.float64, device=dev)
+    ctx.check(ctx.lib.hmcx_softmax_loglik(ctx.h, nat.HMCX_F64, nat.ptr(Xd), nat.ptr(Yd), B, D, K, C, nat.ptr(Wd),
+                                          nat.ptr(bd), nat.ptr(ll)), "loglik")
+    for c in range(C):
+        ref = m.log_likelihood({"weights": Ws[c], "bias": bs[c]}, X_train=X, y_train=Y)
+        assert abs(ll[c].item() - ref) < 1e-10 * abs(ref)
+
+
+def test_bad_shapes_raise(model64):
+    from dropout_hamiltonian_montecarlo_amd._native import HmcxError
+    X, Y, W, b = gi.softmax_inputs(0, 8, D=16, K=4)
+    with pytest.raises(HmcxError):
+        model64.grad({"weights": W[:5], "bias": b}, X_train=X, y_train=Y)
+    with pytest.raises(HmcxError):
+        model64.grad({"weights": np.zeros((16, 70)), "bias": np.zeros(70)}, X_train=X, y_train=np.zeros((8, 70)))
