@@ -46,7 +46,7 @@ class MvnArgs(ctypes.Structure):
 
 # Every symbol include/hmcx.h declares (checked by tests/test_capi.py).
 EXPORTS = ("hmcx_version", "hmcx_create", "hmcx_destroy", "hmcx_last_error", "hmcx_set_stream",
-           "hmcx_synchronize", "hmcx_set_graph_mode", "hmcx_philox_uniforms", "hmcx_philox_normals",
+           "hmcx_synchronize", "hmcx_set_graph_mode", "hmcx_set_sghmc_path", "hmcx_philox_uniforms", "hmcx_philox_normals",
            "hmcx_softmax_grad", "hmcx_softmax_loglik", "hmcx_softmax_predict", "hmcx_sghmc_run",
            "hmcx_sgld_run", "hmcx_hmc_mvn_run")
 
@@ -76,6 +76,7 @@ def load_library():
         lib.hmcx_set_stream.argtypes = [c_void_p, c_void_p]
         lib.hmcx_synchronize.argtypes = [c_void_p]
         lib.hmcx_set_graph_mode.argtypes = [c_void_p, c_int]
+        lib.hmcx_set_sghmc_path.argtypes = [c_void_p, c_int]
         lib.hmcx_philox_uniforms.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                              ctypes.c_uint32, c_dblp]
         lib.hmcx_philox_uniforms.restype = None
@@ -119,6 +120,10 @@ class Context:
         if rc != 0:
             msg = self.lib.hmcx_last_error(self.h)
             raise HmcxError("%s failed (%d): %s" % (what, rc, msg.decode() if msg else ""))
+
+    def set_sghmc_path(self, path):
+        """0 auto, 1 kernel-per-phase, 2 persistent (see include/hmcx.h)."""
+        self.check(self.lib.hmcx_set_sghmc_path(self.h, int(path)), "hmcx_set_sghmc_path")
 
     def set_graph_mode(self, on):
         self.check(self.lib.hmcx_set_graph_mode(self.h, 1 if on else 0), "hmcx_set_graph_mode")

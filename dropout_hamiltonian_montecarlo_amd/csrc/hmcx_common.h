@@ -1,6 +1,6 @@
 // hmcx_common.h — shared device/host helpers for the MI355X (gfx950) SG-HMC engine.
 //
-//  * Philox4x32-10 counter-based RNG (host + device, bit-identical on both), used in
+//  * Philox4x32-10 counter-based RNG (host + device; uniforms bit-identical), used in
 //    HMCX_NOISE_PHILOX mode for momenta / SGHMC friction noise / SGLD noise and, on the
 //    host, for path lengths and accept uniforms.  The reference draws these from
 //    NumPy streams (cpu/sghmc.py:21,25,31,36; cpu/sgld.py:45); HMCX_NOISE_BUFFER mode
@@ -57,16 +57,42 @@ __host__ __device__ inline double philox_uniform(uint64_t seed, uint32_t chain, 
   return u53(r.v[0], r.v[1]);
 }
 
-// Standard normal for element `e` (Box–Muller on one Philox block, two normals per block).
-__host__ __device__ inline double philox_normal(uint64_t seed, uint32_t chain, uint32_t step,
-                                                uint32_t slot, uint32_t e) {
-  u32x4 c = {{e >> 1, slot, step, chain}};
+// Standard normals, four per Philox block: element e uses block e>>2; words (0,1) feed the
+// Box–Muller pair of elements 4b, 4b+1 (cos, sin) and words (2,3) that of 4b+2, 4b+3.
+// The same formula runs on the host (hmcx_philox_normals) up to transcendental rounding (the
+// device uses the hardware v_log/v_sin/v_cos approximations); device values are what the
+// samplers use.
+__host__ __device__ inline void box_muller(uint32_t w0, uint32_t w1, float& z0, float& z1) {
+  const float u1 = ((float)(w0 >> 8) + 1.0f) * 5.9604644775390625e-08f;  // (0,1]
+  const float u2 = (float)(w1 >> 8) * 5.9604644775390625e-08f;           // [0,1)
+  const float th = 6.28318530717958647692f * u2;
+#if defined(__HIP_DEVICE_COMPILE__)
+  const float rad = __fsqrt_rn(-2.0f * __logf(u1));
+  z0 = rad * __cosf(th);
+  z1 = rad * __sinf(th);
+#else
+  const float rad = sqrtf(-2.0f * logf(u1));
+  z0 = rad * cosf(th);
+  z1 = rad * sinf(th);
+#endif
+}
+
+__host__ __device__ inline void philox_normal4(uint64_t seed, uint32_t chain, uint32_t step, uint32_t slot,
+                                               uint32_t blk, float z[4]) {
+  u32x4 c = {{blk, slot, step, chain}};
   u32x4 r = philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
-  double u1 = 1.0 - u53(r.v[0], r.v[1]);  // (0,1]
-  double u2 = u53(r.v[2], r.v[3]);
-  double rad = sqrt(-2.0 * log(u1));
-  double th = 6.283185307179586 * u2;
-  return (e & 1u) ? rad * sin(th) : rad * cos(th);
+  box_muller(r.v[0], r.v[1], z[0], z[1]);
+  box_muller(r.v[2], r.v[3], z[2], z[3]);
+}
+
+__host__ __device__ inline float philox_normal(uint64_t seed, uint32_t chain, uint32_t step,
+                                               uint32_t slot, uint32_t e) {
+  u32x4 c = {{e >> 2, slot, step, chain}};
+  u32x4 r = philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+  float z0, z1;
+  if (e & 2u) box_muller(r.v[2], r.v[3], z0, z1);
+  else box_muller(r.v[0], r.v[1], z0, z1);
+  return (e & 1u) ? z1 : z0;
 }
 
 // ---------------------------------------------------------------- MFMA 16x16x4
@@ -97,5 +123,7 @@ template <> struct mfma16<float> {
 template <typename T> __device__ inline T np_min(T a, T b) { return (a != a) ? a : ((b < a) ? b : a); }
 template <typename T> __device__ inline T np_max(T a, T b) { return (a != a) ? a : ((b > a) ? b : a); }
 template <typename T> __device__ inline T max_nan(T m, T z) { return (z > m || z != z) ? z : m; }
+// softmax.py:40-41: np.maximum(np.minimum(z, hi), lo)
+template <typename T> __device__ inline T clipz(T z, T hi, T lo) { return np_max(np_min(z, hi), lo); }
 
 }  // namespace hmcx

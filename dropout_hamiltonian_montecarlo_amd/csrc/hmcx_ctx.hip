@@ -15,7 +15,7 @@ int set_error(hmcx_ctx* ctx, int code, const std::string& msg) {
 bool Workspace::retry() {
   if (off <= ctx->ws_cap) return false;
   if (ctx->ws) {
-    if (hipStreamSynchronize(ctx->stream) != hipSuccess) { failed = true; return false; }
+    if (hipDeviceSynchronize() != hipSuccess) { failed = true; return false; }
     (void)hipFree(ctx->ws);
     ctx->ws = nullptr;
     ctx->ws_cap = 0;
@@ -64,35 +64,61 @@ int upload(hmcx_ctx* ctx, void* dst, const void* src, size_t bytes) {
 }
 
 GraphScope::GraphScope(hmcx_ctx* c) : ctx(c) {
-  if (ctx->graph_mode && hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal) == hipSuccess)
-    capturing = true;
+  if (!ctx->graph_mode) return;
+  // fork: own_stream waits for everything already queued on the caller's stream
+  user_stream = ctx->stream;
+  if (hipEventRecord(ctx->ev_in, user_stream) != hipSuccess) return;
+  if (hipStreamWaitEvent(ctx->own_stream, ctx->ev_in, 0) != hipSuccess) return;
+  if (hipStreamBeginCapture(ctx->own_stream, hipStreamCaptureModeThreadLocal) != hipSuccess) return;
+  ctx->stream = ctx->own_stream;
+  capturing = true;
+}
+
+static void sweep_graveyard(hmcx_ctx* ctx) {
+  auto& g = ctx->graveyard;
+  for (size_t i = 0; i < g.size();) {
+    if (hipEventQuery(g[i].second) == hipSuccess) {
+      (void)hipGraphExecDestroy(g[i].first);
+      (void)hipEventDestroy(g[i].second);
+      g[i] = g.back();
+      g.pop_back();
+    } else {
+      ++i;
+    }
+  }
 }
 
 int GraphScope::finish() {
   if (!capturing) return HMCX_OK;
   capturing = false;
+  ctx->stream = user_stream;
   hipGraph_t graph = nullptr;
-  HMCX_HIP(ctx, hipStreamEndCapture(ctx->stream, &graph));
+  HMCX_HIP(ctx, hipStreamEndCapture(ctx->own_stream, &graph));
   hipGraphExec_t exec = nullptr;
   hipError_t e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
-  if (e != hipSuccess) {
-    (void)hipGraphDestroy(graph);
-    return set_error(ctx, HMCX_EHIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(e));
-  }
-  e = hipGraphLaunch(exec, ctx->stream);
-  // The executable graph is destroyed only after it has run.
-  (void)hipStreamSynchronize(ctx->stream);
-  (void)hipGraphExecDestroy(exec);
   (void)hipGraphDestroy(graph);
-  if (e != hipSuccess) return set_error(ctx, HMCX_EHIP, std::string("hipGraphLaunch: ") + hipGetErrorString(e));
+  if (e != hipSuccess) return set_error(ctx, HMCX_EHIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(e));
+  e = hipGraphLaunch(exec, ctx->own_stream);
+  if (e != hipSuccess) {
+    (void)hipGraphExecDestroy(exec);
+    return set_error(ctx, HMCX_EHIP, std::string("hipGraphLaunch: ") + hipGetErrorString(e));
+  }
+  // join: the caller's stream waits for the graph; the exec is released once it has run
+  hipEvent_t done = nullptr;
+  HMCX_HIP(ctx, hipEventCreateWithFlags(&done, hipEventDisableTiming));
+  HMCX_HIP(ctx, hipEventRecord(done, ctx->own_stream));
+  HMCX_HIP(ctx, hipStreamWaitEvent(user_stream, done, 0));
+  ctx->graveyard.emplace_back(exec, done);
+  sweep_graveyard(ctx);
   return HMCX_OK;
 }
 
 GraphScope::~GraphScope() {
   if (capturing) {
     hipGraph_t g = nullptr;
-    (void)hipStreamEndCapture(ctx->stream, &g);
+    (void)hipStreamEndCapture(ctx->own_stream, &g);
     if (g) (void)hipGraphDestroy(g);
+    ctx->stream = user_stream;
   }
 }
 
@@ -223,11 +249,17 @@ int hmcx_create(int device, hmcx_ctx** out) {
   if (!c) return HMCX_ENOMEM;
   c->device = device;
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreateWithFlags(&c->stage_ev, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&c->stage_ev, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming) != hipSuccess) {
     delete c;
     return HMCX_EHIP;
   }
   c->stream = c->own_stream;
+  int ncu = 0, lds = 0;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
+    c->num_cus = ncu;
+  if (hipDeviceGetAttribute(&lds, hipDeviceAttributeSharedMemPerBlockOptin, device) == hipSuccess && lds > 0)
+    c->lds_max = (size_t)lds;
   *out = c;
   return HMCX_OK;
 }
@@ -239,6 +271,11 @@ int hmcx_destroy(hmcx_ctx* ctx) {
   if (ctx->ws) (void)hipFree(ctx->ws);
   if (ctx->stage) (void)hipHostFree(ctx->stage);
   if (ctx->stage_ev) (void)hipEventDestroy(ctx->stage_ev);
+  if (ctx->ev_in) (void)hipEventDestroy(ctx->ev_in);
+  for (auto& g : ctx->graveyard) {
+    (void)hipGraphExecDestroy(g.first);
+    (void)hipEventDestroy(g.second);
+  }
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
   delete ctx;
   return HMCX_OK;
@@ -248,13 +285,20 @@ const char* hmcx_last_error(const hmcx_ctx* ctx) { return ctx ? ctx->err.c_str()
 
 int hmcx_set_stream(hmcx_ctx* ctx, void* stream) {
   HMCX_GUARD_CTX(ctx);
-  ctx->stream = stream ? (hipStream_t)stream : ctx->own_stream;
+  ctx->stream = (hipStream_t)stream;   // NULL = the legacy default stream (torch's default)
   return HMCX_OK;
 }
 
 int hmcx_synchronize(hmcx_ctx* ctx) {
   HMCX_GUARD_CTX(ctx);
   HMCX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return HMCX_OK;
+}
+
+int hmcx_set_sghmc_path(hmcx_ctx* ctx, int path) {
+  HMCX_GUARD_CTX(ctx);
+  if (path < 0 || path > 2) return set_error(ctx, HMCX_EINVAL, "path must be 0 (auto), 1 (kernels), 2 (persistent)");
+  ctx->sghmc_path = path;
   return HMCX_OK;
 }
 

@@ -13,6 +13,9 @@ struct hmcx_ctx {
   hipStream_t stream = nullptr;
   std::string err;
   int graph_mode = 0;
+  int sghmc_path = 0;          // 0 auto (persistent when eligible), 1 kernel-per-phase, 2 persistent only
+  int num_cus = 256;
+  size_t lds_max = 160 * 1024;
   // device workspace (grows; freed only after a stream sync)
   char* ws = nullptr;
   size_t ws_cap = 0;
@@ -22,6 +25,9 @@ struct hmcx_ctx {
   size_t stage_off = 0;
   hipEvent_t stage_ev = nullptr;
   bool stage_pending = false;
+  // hipGraph mode: capture happens on own_stream (the legacy default stream cannot be captured)
+  hipEvent_t ev_in = nullptr, ev_out = nullptr;
+  std::vector<std::pair<hipGraphExec_t, hipEvent_t>> graveyard;   // executed graphs awaiting release
 };
 
 namespace hmcx {
@@ -77,34 +83,45 @@ template <typename T> struct FwdArgs {
 
 template <typename T> struct GradArgs {
   const T* X; const T* diff; const T* colsum_part;
-  int B, D, K, C, N, CB, nRB, P;
+  int B, D, K, C, N, CB, nRB, nDB, P;
   int mode;
   T alpha, eps, one_minus_eps, noise_scale, m_half_eps;
   int iter;
   const int32_t* n_iter;
   const T* Wsrc; const T* bsrc;
   T* W; T* b; T* pW; T* pb; T* gW; T* gb;
+  double* kin_part;   // SGHMC: [nDB][C] Σ pW² of the block at the chain's last iteration
+  double* kinb;       // SGHMC: [C] Σ pb² at the chain's last iteration
   int noise_mode; const double* noise; const int64_t* noff;
   uint64_t seed; uint32_t chain0, step, slot;
 };
 
+// SGHMC step start: commit the previous step's accepted proposal, draw momentum, first drift.
 template <typename T> struct InitArgs {
-  int D, K, C, N;
+  int D, K, C, N, nDB;
   T eps;
   const int32_t* n_iter;
+  const int32_t* prev_acc;   // [C] accept flags of the previous step of this call, or null
   int noise_mode; const double* noise; const int64_t* noff;
   uint64_t seed; uint32_t chain0, step;
-  const T* W; const T* b;
-  T* Wwork; T* bwork; T* pW; T* pb; T* p0W; T* p0b;
+  T* W; T* b;
+  T* Wwork; T* bwork; T* pW; T* pb;
+  double* kin0_part;         // [nDB][C]
+  double* kin0b;             // [C]
+};
+
+template <typename T> struct CommitArgs {
+  int D, K, C, N;
+  const int32_t* acc;
+  const T* Wwork; const T* bwork; T* W; T* b;
 };
 
 template <typename T> struct AcceptArgs {
-  int D, K, C, N, nRB;
+  int C, nRB, nDB;
   const int32_t* n_iter; const double* u;
   double neg_inv_n, log_prior;
-  const T* p0W; const T* p0b; const T* pW; const T* pb;
+  const double* kin0_part; const double* kin0b; const double* kin1_part; const double* kin1b;
   const double* ll0_part; const double* ll1_part;
-  const T* Wwork; const T* bwork; T* W; T* b;
   double* out_A; int32_t* out_acc; double* out_ll; double* out_E;
 };
 
@@ -116,6 +133,7 @@ void begin_call(hmcx_ctx* ctx);
 struct GraphScope {
   hmcx_ctx* ctx;
   bool capturing = false;
+  hipStream_t user_stream = nullptr;
   explicit GraphScope(hmcx_ctx* c);
   int finish();
   ~GraphScope();

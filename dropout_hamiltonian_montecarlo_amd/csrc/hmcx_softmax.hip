@@ -7,29 +7,38 @@
 //   sgld.step             /root/reference/hamiltonian/inference/cpu/sgld.py:31-46   (A2)
 //
 // One SGHMC leapfrog iteration (sghmc.py:28-34, vars in order weights, bias) is two kernels:
-//   k_fwd  (rows x chain-tile):  Z = X·W (MFMA), then per (row, chain): z = clip(Z+b),
-//          softmax, diff = y − ŷ  (for the weights sub-step), and the bias sub-step
-//          b' = b + ε·pb, z' = clip(Z+b'), Σ_rows(y − ŷ') partials and log-likelihood
-//          partials at (W, b') — the bias sub-step reuses X·W (W is unchanged by it).
-//   k_grad (features x chain-tile):  Xᵀ·diff (MFMA), fused epilogue
-//          g = −(Xᵀdiff − αW);  p = (1−ε)p + εg + 2ε·ξ;  W += ε·p (next drift);
-//          tile-column 0 also finishes the bias sub-step from the row partials.
+//   k_fwd  (16-row x chain tile):  Z = X·W on v_mfma_*_16x16x4 (d split over the block's
+//          waves, 4 k-chunks of loads in flight per wave), then, element-parallel from LDS:
+//          z = clip(Z+b), softmax, diff = y − ŷ (weights sub-step), and the bias sub-step
+//          b' = b + ε·pb, z' = clip(Z+b'): Σ_rows(y − ŷ') and log-likelihood partials at (W,b')
+//          — the bias sub-step reuses X·W (W is unchanged by it).
+//   k_grad (16-feature x chain tile):  Xᵀ·diff on MFMA (minibatch split over waves), fused
+//          epilogue g = −(Xᵀdiff − αW);  p = (1−ε)p + εg + 2ε·ξ;  W += ε·p (next drift);
+//          the tile-column-0 blocks finish the bias sub-step from the row partials.
+// Per step: k_sghmc_init (commit previous accept, momentum, first drift, kinetic partials),
+// k_fwd(LL) at q0, n_iter × (k_fwd, k_grad), k_sghmc_accept (energies, MH decision).
+// Rules followed for latency: no serial loop over global loads anywhere (all reductions are
+// parallel loads + fixed-order LDS trees, so results are deterministic run to run).
 // Elementwise arithmetic follows the reference's NumPy op order with FP contraction off
-// (-ffp-contract=off), so float64 runs differ from NumPy only through GEMM summation order.
+// (-ffp-contract=off), so float64 runs differ from NumPy only through summation order.
 #include "hmcx_common.h"
 #include "hmcx_internal.h"
+#include "hmcx_persist.h"
 
 namespace hmcx {
 
 // ------------------------------------------------------------------ forward (logits) kernel
-template <typename T, int NBLK, bool VEC>
-__global__ __launch_bounds__(256) void k_fwd(FwdArgs<T> a) {
+template <typename T, int NBLK, bool VEC, int NW>
+__global__ __launch_bounds__(NW * 64) void k_fwd(FwdArgs<T> a) {
   using M = mfma16<T>;
-  constexpr int NT = NBLK * 16;
-  __shared__ T red[4][16][NT];
-  __shared__ T zt[16][NT + 1];
-  __shared__ T dt[16][NT + 1];
-  __shared__ double llt[16][NT];
+  constexpr int NT = NBLK * 16, NTH = NW * 64, LD = NT + 1;
+  constexpr int YPT = (16 * NT + NTH - 1) / NTH;   // Y values prefetched per thread
+  __shared__ T red[NW][16][NT];
+  __shared__ T zA[16][LD], eA[16][LD], zB[16][LD], eB[16][LD], yt[16][LD];
+  __shared__ T bt[NT], bpt[NT];
+  __shared__ T mA[16][NT], sA[16][NT], mB[16][NT], sB[16][NT];
+  __shared__ double lrow[16][NT];
+  __shared__ int act[NT];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 15, g = lane >> 4;
@@ -38,140 +47,180 @@ __global__ __launch_bounds__(256) void k_fwd(FwdArgs<T> a) {
   const int ncb = min(a.CB, a.C - c0);
   const int n0 = c0 * a.K;
   const int ncols = ncb * a.K;
+  const int K = a.K;
+  const int mode = a.mode;
+  const bool sghmc = mode == FWD_SGHMC;
+  const int nrow = min(16, a.B - m0);
 
+  // ---- prefetch epilogue operands into registers (their latency overlaps the GEMM)
+  T breg = T(0), bpreg = T(0);
+  int actreg = 1;
+  if (tid < ncols) {
+    breg = a.b[n0 + tid];
+    if (sghmc) bpreg = breg + a.eps * a.pb[n0 + tid];                  // b' = b + ε·pb (sghmc.py:32)
+  }
+  if (sghmc && tid < ncb) actreg = a.iter < a.n_iter[c0 + tid];
+  T yreg[YPT];
+#pragma unroll
+  for (int q = 0; q < YPT; ++q) {
+    const int e = tid + q * NTH;
+    const int i = e / NT, j = e - (e / NT) * NT;
+    yreg[q] = (mode != FWD_PRED && e < 16 * NT && i < nrow && j < ncols) ? a.Y[(size_t)(m0 + i) * K + j % K] : T(0);
+  }
+
+  // ---- Z = X·W : wave w owns d in [w·Dw, (w+1)·Dw), 4 chunks of 16 loaded before their MFMAs
   typename M::acc_t acc0[NBLK], acc1[NBLK];
 #pragma unroll
   for (int nb = 0; nb < NBLK; ++nb) { acc0[nb] = M::zero(); acc1[nb] = M::zero(); }
-
-  const int Dq = ((a.D + 63) / 64) * 16;
-  const int kbeg = wave * Dq, kend = min(a.D, kbeg + Dq);
-  const int row = m0 + r;
-  const bool rok = row < a.B;
-  const T* xrow = a.X + (size_t)(rok ? row : 0) * a.D;
-
-  for (int kc = kbeg; kc < kend; kc += 16) {
-    const int kb = kc + 4 * g;
-    T av[4];
-    if (VEC && kc + 16 <= kend) {
-      if (rok) {
+  const int Dw = ((a.D + NW * 16 - 1) / (NW * 16)) * 16;
+  const int kbeg = wave * Dw, kend = min(a.D, kbeg + Dw);
+  const bool rok = r < nrow;
+  const T* xrow = a.X + (size_t)(m0 + (rok ? r : 0)) * a.D;
+  for (int kc = kbeg; kc < kend; kc += 64) {
+    T av[4][4], bv[4][NBLK][4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int kb = kc + 16 * u + 4 * g;
+      if (VEC && kb + 3 < kend && rok) {
         if constexpr (sizeof(T) == 8) {
           const double2* p2 = reinterpret_cast<const double2*>(xrow + kb);
-          double2 u = p2[0], v = p2[1];
-          av[0] = u.x; av[1] = u.y; av[2] = v.x; av[3] = v.y;
+          const double2 x0 = p2[0], x1 = p2[1];
+          av[u][0] = x0.x; av[u][1] = x0.y; av[u][2] = x1.x; av[u][3] = x1.y;
         } else {
-          float4 u = *reinterpret_cast<const float4*>(xrow + kb);
-          av[0] = u.x; av[1] = u.y; av[2] = u.z; av[3] = u.w;
+          const float4 x0 = *reinterpret_cast<const float4*>(xrow + kb);
+          av[u][0] = x0.x; av[u][1] = x0.y; av[u][2] = x0.z; av[u][3] = x0.w;
         }
       } else {
 #pragma unroll
-        for (int s = 0; s < 4; ++s) av[s] = T(0);
+        for (int s = 0; s < 4; ++s) av[u][s] = (rok && kb + s < kend) ? xrow[kb + s] : T(0);
       }
-    } else {
 #pragma unroll
-      for (int s = 0; s < 4; ++s) av[s] = (rok && kb + s < kend) ? xrow[kb + s] : T(0);
+      for (int nb = 0; nb < NBLK; ++nb) {
+        const int col = nb * 16 + r;
+        const bool cok = col < ncols;
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+          bv[u][nb][s] = (cok && kb + s < kend) ? a.W[(size_t)(kb + s) * a.N + n0 + col] : T(0);
+      }
     }
 #pragma unroll
-    for (int nb = 0; nb < NBLK; ++nb) {
-      const int col = nb * 16 + r;
-      const bool cok = col < ncols;
-      T bv[4];
+    for (int u = 0; u < 4; ++u)
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const int kk = kb + s;
-        bv[s] = (cok && kk < kend) ? a.W[(size_t)kk * a.N + n0 + col] : T(0);
+      for (int nb = 0; nb < NBLK; ++nb) {
+        acc0[nb] = M::fma(av[u][0], bv[u][nb][0], acc0[nb]);
+        acc1[nb] = M::fma(av[u][1], bv[u][nb][1], acc1[nb]);
+        acc0[nb] = M::fma(av[u][2], bv[u][nb][2], acc0[nb]);
+        acc1[nb] = M::fma(av[u][3], bv[u][nb][3], acc1[nb]);
       }
-      acc0[nb] = M::fma(av[0], bv[0], acc0[nb]);
-      acc1[nb] = M::fma(av[1], bv[1], acc1[nb]);
-      acc0[nb] = M::fma(av[2], bv[2], acc0[nb]);
-      acc1[nb] = M::fma(av[3], bv[3], acc1[nb]);
-    }
   }
 #pragma unroll
   for (int nb = 0; nb < NBLK; ++nb)
 #pragma unroll
     for (int q = 0; q < 4; ++q) red[wave][M::row(lane, q)][nb * 16 + r] = acc0[nb][q] + acc1[nb][q];
-  __syncthreads();
-  for (int e = tid; e < 16 * NT; e += 256) {
-    const int i = e / NT, j = e % NT;
-    zt[i][j] = ((red[0][i][j] + red[1][i][j]) + red[2][i][j]) + red[3][i][j];
+  if (tid < NT) { bt[tid] = breg; bpt[tid] = bpreg; }
+  if (tid < NT) act[tid] = actreg;
+#pragma unroll
+  for (int q = 0; q < YPT; ++q) {
+    const int e = tid + q * NTH;
+    if (e < 16 * NT) yt[e / NT][e - (e / NT) * NT] = yreg[q];
   }
   __syncthreads();
 
-  // ---- epilogue: one thread per (row, chain)
+  // ---- pass 1 (element): XW (fixed wave order), z = clip(XW + b), z' = clip(XW + b')
   const T hi = a.clip_hi, lo = a.clip_lo;
-  for (int p = tid; p < 16 * ncb; p += 256) {
-    const int i = p & 15, cc = p >> 4;
-    const int rw = m0 + i;
-    const int cb = cc * a.K;
-    const int c = c0 + cc;
-    if (rw >= a.B) continue;
-    const bool active = (a.mode != FWD_SGHMC) || (a.iter < a.n_iter[c]);
-    const T* y = a.Y + (size_t)rw * a.K;
-    const T* bb = a.b + n0 + cb;
-    if (a.mode == FWD_GRAD || a.mode == FWD_SGHMC || a.mode == FWD_PRED) {
-      // softmax.py:39-43 at (W, b)
-      T m = np_max(np_min(zt[i][cb] + bb[0], hi), lo);
-      for (int k = 1; k < a.K; ++k) m = max_nan(m, np_max(np_min(zt[i][cb + k] + bb[k], hi), lo));
-      T s = T(0);
-      for (int k = 0; k < a.K; ++k) s += exp(np_max(np_min(zt[i][cb + k] + bb[k], hi), lo) - m);
-      for (int k = 0; k < a.K; ++k) {
-        const T yh = exp(np_max(np_min(zt[i][cb + k] + bb[k], hi), lo) - m) / s;
-        if (a.mode == FWD_PRED) {
-          a.prob[(size_t)rw * a.N + n0 + cb + k] = yh;
-        } else {
-          const T d = y[k] - yh;                                  // softmax.py:52
-          if (active) a.diff[(size_t)rw * a.N + n0 + cb + k] = d;
-          if (a.mode == FWD_GRAD) dt[i][cb + k] = d;
-        }
-      }
-    }
-    if (a.mode == FWD_SGHMC) {
-      // bias sub-step (sghmc.py:32-33 for var 'bias'): b' = b + ε·pb, grad at (W, b')
-      const T* pb = a.pb + n0 + cb;
-      T m = np_max(np_min(zt[i][cb] + (bb[0] + a.eps * pb[0]), hi), lo);
-      for (int k = 1; k < a.K; ++k)
-        m = max_nan(m, np_max(np_min(zt[i][cb + k] + (bb[k] + a.eps * pb[k]), hi), lo));
-      T s = T(0);
-      for (int k = 0; k < a.K; ++k) s += exp(np_max(np_min(zt[i][cb + k] + (bb[k] + a.eps * pb[k]), hi), lo) - m);
-      const T lse = log(s) + m;
-      double ll = 0.0;
-      for (int k = 0; k < a.K; ++k) {
-        const T z = np_max(np_min(zt[i][cb + k] + (bb[k] + a.eps * pb[k]), hi), lo);
-        dt[i][cb + k] = y[k] - exp(z - m) / s;
-        ll += (double)(y[k] * (z - lse));                         // softmax.py:17-20
-      }
-      llt[i][cc] = ll;
-    } else if (a.mode == FWD_LL) {
-      T m = np_max(np_min(zt[i][cb] + bb[0], hi), lo);
-      for (int k = 1; k < a.K; ++k) m = max_nan(m, np_max(np_min(zt[i][cb + k] + bb[k], hi), lo));
-      T s = T(0);
-      for (int k = 0; k < a.K; ++k) s += exp(np_max(np_min(zt[i][cb + k] + bb[k], hi), lo) - m);
-      const T lse = log(s) + m;
-      double ll = 0.0;
-      for (int k = 0; k < a.K; ++k) {
-        const T z = np_max(np_min(zt[i][cb + k] + bb[k], hi), lo);
-        ll += (double)(y[k] * (z - lse));
-      }
-      llt[i][cc] = ll;
+  for (int e = tid; e < 16 * NT; e += NTH) {
+    const int i = e / NT, j = e - (e / NT) * NT;
+    T xw = red[0][i][j];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) xw += red[w][i][j];
+    zA[i][j] = clipz(xw + bt[j], hi, lo);                                  // softmax.py:39-41
+    if (sghmc) zB[i][j] = clipz(xw + bpt[j], hi, lo);
+  }
+  __syncthreads();
+  // ---- pass 2 (row, chain): row max (np.max semantics: NaN propagates)
+  for (int p = tid; p < 16 * ncb; p += NTH) {
+    const int i = p & 15, cb = (p >> 4) * K;
+    T m = zA[i][cb];
+    for (int k = 1; k < K; ++k) m = max_nan(m, zA[i][cb + k]);
+    mA[i][p >> 4] = m;
+    if (sghmc) {
+      T mb = zB[i][cb];
+      for (int k = 1; k < K; ++k) mb = max_nan(mb, zB[i][cb + k]);
+      mB[i][p >> 4] = mb;
     }
   }
   __syncthreads();
-  if (a.mode == FWD_GRAD || a.mode == FWD_SGHMC) {
-    for (int j = tid; j < ncols; j += 256) {
-      const int c = c0 + j / a.K;
-      if (a.mode == FWD_SGHMC && a.iter >= a.n_iter[c]) continue;
+  // ---- pass 3 (element): exponentials
+  for (int e = tid; e < 16 * NT; e += NTH) {
+    const int i = e / NT, j = e - (e / NT) * NT;
+    if (j >= ncols) continue;
+    const int cc = j / K;
+    eA[i][j] = exp(zA[i][j] - mA[i][cc]);                                 // softmax.py:34
+    if (sghmc) eB[i][j] = exp(zB[i][j] - mB[i][cc]);
+  }
+  __syncthreads();
+  // ---- pass 4 (row, chain): normalisers
+  for (int p = tid; p < 16 * ncb; p += NTH) {
+    const int i = p & 15, cc = p >> 4, cb = cc * K;
+    T s = T(0);
+    for (int k = 0; k < K; ++k) s += eA[i][cb + k];
+    sA[i][cc] = s;
+    if (sghmc) {
+      T sb = T(0);
+      for (int k = 0; k < K; ++k) sb += eB[i][cb + k];
+      sB[i][cc] = sb;
+    }
+  }
+  __syncthreads();
+  // ---- pass 5 (element): ŷ, diff, colsum terms, log-likelihood terms (written in place)
+  for (int e = tid; e < 16 * NT; e += NTH) {
+    const int i = e / NT, j = e - (e / NT) * NT;
+    if (j >= ncols || i >= nrow) continue;
+    const int cc = j / K;
+    const size_t gidx = (size_t)(m0 + i) * a.N + n0 + j;
+    const T yh = eA[i][j] / sA[i][cc];                                    // softmax.py:35-36
+    if (mode == FWD_PRED) { a.prob[gidx] = yh; continue; }
+    const T y = yt[i][j];
+    if (mode == FWD_GRAD || sghmc) {
+      const T d = y - yh;                                                 // softmax.py:52
+      if (act[cc]) a.diff[gidx] = d;
+      if (mode == FWD_GRAD) eA[i][j] = d;
+    }
+    if (sghmc) {
+      const T lse = log(sB[i][cc]) + mB[i][cc];                           // logsumexp (softmax.py:18)
+      const T yb = eB[i][j] / sB[i][cc];
+      zA[i][j] = y - yb;                                                  // bias sub-step colsum term
+      eB[i][j] = y * (zB[i][j] - lse);                                    // softmax.py:19-20
+    } else if (mode == FWD_LL) {
+      const T lse = log(sA[i][cc]) + mA[i][cc];
+      eA[i][j] = y * (zA[i][j] - lse);
+    }
+  }
+  __syncthreads();
+  // ---- pass 6: column sums of diff (→ gb partial) and row log-likelihoods
+  if (mode == FWD_GRAD || sghmc) {
+    const T(*src)[LD] = sghmc ? zA : eA;
+    for (int j = tid; j < ncols; j += NTH) {
+      if (!act[j / K]) continue;
       T s = T(0);
-      for (int i = 0; i < 16 && m0 + i < a.B; ++i) s += dt[i][j];
+      for (int i = 0; i < nrow; ++i) s += src[i][j];
       a.colsum_part[(size_t)blockIdx.x * a.N + n0 + j] = s;
     }
   }
-  if (a.mode == FWD_SGHMC || a.mode == FWD_LL) {
-    for (int cc = tid; cc < ncb; cc += 256) {
-      const int c = c0 + cc;
-      if (a.mode == FWD_SGHMC && a.iter >= a.n_iter[c]) continue;
+  if (sghmc || mode == FWD_LL) {
+    const T(*src)[LD] = sghmc ? eB : eA;
+    for (int p = tid; p < nrow * ncb; p += NTH) {
+      const int i = p % nrow, cc = p / nrow, cb = cc * K;
       double s = 0.0;
-      for (int i = 0; i < 16 && m0 + i < a.B; ++i) s += llt[i][cc];
-      a.ll_part[(size_t)blockIdx.x * a.C + c] = s;
+      for (int k = 0; k < K; ++k) s += (double)src[i][cb + k];
+      lrow[i][cc] = s;
+    }
+    __syncthreads();
+    for (int cc = tid; cc < ncb; cc += NTH) {
+      if (!act[cc]) continue;
+      double s = 0.0;
+      for (int i = 0; i < nrow; ++i) s += lrow[i][cc];
+      a.ll_part[(size_t)blockIdx.x * a.C + c0 + cc] = s;
     }
   }
 }
@@ -180,15 +229,18 @@ __global__ __launch_bounds__(256) void k_fwd(FwdArgs<T> a) {
 template <typename T>
 __device__ inline double noise_at(const GradArgs<T>& a, int c, uint32_t e) {
   if (a.noise_mode == HMCX_NOISE_BUFFER) return a.noise[a.noff[c] + (int64_t)a.slot * a.P + e];
-  return philox_normal(a.seed, a.chain0 + c, a.step, a.slot, e);
+  return (double)philox_normal(a.seed, a.chain0 + c, a.step, a.slot, e);
 }
 
 // ------------------------------------------------------------------ gradient (Xᵀ·diff) kernel
-template <typename T, int NBLK>
-__global__ __launch_bounds__(256) void k_grad(GradArgs<T> a) {
+template <typename T, int NBLK, int NW>
+__global__ __launch_bounds__(NW * 64) void k_grad(GradArgs<T> a) {
   using M = mfma16<T>;
-  constexpr int NT = NBLK * 16;
-  __shared__ T red[4][16][NT];
+  constexpr int NT = NBLK * 16, NTH = NW * 64;
+  constexpr int EPT = (16 * NT + NTH - 1) / NTH;    // epilogue elements per thread
+  __shared__ T red[NW][16][NT];
+  __shared__ T csr[NTH];
+  __shared__ double ksh[NTH];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 15, g = lane >> 4;
@@ -197,37 +249,65 @@ __global__ __launch_bounds__(256) void k_grad(GradArgs<T> a) {
   const int ncb = min(a.CB, a.C - c0);
   const int n0 = c0 * a.K;
   const int ncols = ncb * a.K;
+  const int K = a.K;
+  const int mode = a.mode;
 
+  // ---- prefetch the epilogue's per-element operands and noise (overlaps the GEMM)
+  T wreg[EPT], preg[EPT], zreg[EPT];
+  int ok[EPT];
+#pragma unroll
+  for (int q = 0; q < EPT; ++q) {
+    const int e = tid + q * NTH;
+    const int i = e / NT, j = e - (e / NT) * NT;
+    const int d = d0 + i;
+    ok[q] = e < 16 * NT && d < a.D && j < ncols;
+    if (ok[q] && mode == GRAD_SGHMC) ok[q] = a.iter < a.n_iter[c0 + j / K];
+    wreg[q] = preg[q] = zreg[q] = T(0);
+    if (ok[q]) {
+      const size_t idx = (size_t)d * a.N + n0 + j;
+      const int cc = j / K, k = j - cc * K;
+      if (mode == GRAD_OUT) {
+        wreg[q] = a.Wsrc[idx];
+      } else {
+        wreg[q] = a.W[idx];
+        if (mode == GRAD_SGHMC) preg[q] = a.pW[idx];
+        zreg[q] = (T)noise_at(a, c0 + cc, (uint32_t)(d * K + k));
+      }
+    }
+  }
+
+  // ---- Xᵀ·diff : wave w owns minibatch rows [w·Bw, (w+1)·Bw)
   typename M::acc_t acc0[NBLK], acc1[NBLK];
 #pragma unroll
   for (int nb = 0; nb < NBLK; ++nb) { acc0[nb] = M::zero(); acc1[nb] = M::zero(); }
-
-  const int Bq = ((a.B + 63) / 64) * 16;
-  const int kbeg = wave * Bq, kend = min(a.B, kbeg + Bq);
+  const int Bw = ((a.B + NW * 16 - 1) / (NW * 16)) * 16;
+  const int kbeg = wave * Bw, kend = min(a.B, kbeg + Bw);
   const bool dok = d0 + r < a.D;
-  for (int kc = kbeg; kc < kend; kc += 16) {
-    const int kb = kc + 4 * g;
-    T av[4];
+  for (int kc = kbeg; kc < kend; kc += 64) {
+    T av[4][4], bv[4][NBLK][4];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int kk = kb + s;
-      av[s] = (dok && kk < kend) ? a.X[(size_t)kk * a.D + d0 + r] : T(0);
-    }
+    for (int u = 0; u < 4; ++u) {
+      const int kb = kc + 16 * u + 4 * g;
 #pragma unroll
-    for (int nb = 0; nb < NBLK; ++nb) {
-      const int col = nb * 16 + r;
-      const bool cok = col < ncols;
-      T bv[4];
+      for (int s = 0; s < 4; ++s) av[u][s] = (dok && kb + s < kend) ? a.X[(size_t)(kb + s) * a.D + d0 + r] : T(0);
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const int kk = kb + s;
-        bv[s] = (cok && kk < kend) ? a.diff[(size_t)kk * a.N + n0 + col] : T(0);
+      for (int nb = 0; nb < NBLK; ++nb) {
+        const int col = nb * 16 + r;
+        const bool cok = col < ncols;
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+          bv[u][nb][s] = (cok && kb + s < kend) ? a.diff[(size_t)(kb + s) * a.N + n0 + col] : T(0);
       }
-      acc0[nb] = M::fma(av[0], bv[0], acc0[nb]);
-      acc1[nb] = M::fma(av[1], bv[1], acc1[nb]);
-      acc0[nb] = M::fma(av[2], bv[2], acc0[nb]);
-      acc1[nb] = M::fma(av[3], bv[3], acc1[nb]);
     }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int nb = 0; nb < NBLK; ++nb) {
+        acc0[nb] = M::fma(av[u][0], bv[u][nb][0], acc0[nb]);
+        acc1[nb] = M::fma(av[u][1], bv[u][nb][1], acc1[nb]);
+        acc0[nb] = M::fma(av[u][2], bv[u][nb][2], acc0[nb]);
+        acc1[nb] = M::fma(av[u][3], bv[u][nb][3], acc1[nb]);
+      }
   }
 #pragma unroll
   for (int nb = 0; nb < NBLK; ++nb)
@@ -235,99 +315,196 @@ __global__ __launch_bounds__(256) void k_grad(GradArgs<T> a) {
     for (int q = 0; q < 4; ++q) red[wave][M::row(lane, q)][nb * 16 + r] = acc0[nb][q] + acc1[nb][q];
   __syncthreads();
 
-  const int DK = a.D * a.K;
-  for (int e = tid; e < 16 * NT; e += 256) {
-    const int i = e / NT, j = e % NT;
-    const int d = d0 + i;
-    if (d >= a.D || j >= ncols) continue;
-    const T dot = ((red[0][i][j] + red[1][i][j]) + red[2][i][j]) + red[3][i][j];
-    const int cc = j / a.K, k = j - cc * a.K, c = c0 + cc;
-    const size_t idx = (size_t)d * a.N + n0 + j;
-    if (a.mode == GRAD_OUT) {
-      a.gW[idx] = -(dot - a.alpha * a.Wsrc[idx]);                 // softmax.py:57-58
-    } else if (a.mode == GRAD_SGHMC) {
-      if (a.iter >= a.n_iter[c]) continue;
-      const T w = a.W[idx];
-      const T gr = -(dot - a.alpha * w);
-      T p = a.pW[idx];
-      const T z = (T)noise_at(a, c, (uint32_t)(d * a.K + k));
-      p = (a.one_minus_eps * p + a.eps * gr) + a.noise_scale * z;  // sghmc.py:31,34
+  // ---- epilogue (element): gradient, momentum, drift (sghmc.py:31-34 / sgld.py:34-38)
+  T pnew[EPT];
+#pragma unroll
+  for (int q = 0; q < EPT; ++q) {
+    pnew[q] = T(0);
+    if (!ok[q]) continue;
+    const int e = tid + q * NTH;
+    const int i = e / NT, j = e - (e / NT) * NT;
+    const size_t idx = (size_t)(d0 + i) * a.N + n0 + j;
+    T dot = red[0][i][j];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) dot += red[w][i][j];
+    const T gr = -(dot - a.alpha * wreg[q]);                              // softmax.py:57-58
+    if (mode == GRAD_OUT) {
+      a.gW[idx] = gr;
+    } else if (mode == GRAD_SGHMC) {
+      const T p = (a.one_minus_eps * preg[q] + a.eps * gr) + a.noise_scale * zreg[q];
       a.pW[idx] = p;
-      if (a.iter < a.n_iter[c] - 1) a.W[idx] = w + a.eps * p;     // next iteration's drift :32
-    } else {  // GRAD_SGLD (sgld.py:34-38)
-      const T w = a.W[idx];
-      const T gr = -(dot - a.alpha * w);
-      const T z = (T)noise_at(a, c, (uint32_t)(d * a.K + k));
-      T p = a.noise_scale * z;
+      pnew[q] = p;
+      if (a.iter < a.n_iter[c0 + j / K] - 1) a.W[idx] = wreg[q] + a.eps * p;   // next drift
+    } else {
+      T p = a.noise_scale * zreg[q];
       p = p + a.m_half_eps * gr;
-      a.W[idx] = w + p;
+      a.W[idx] = wreg[q] + p;
+    }
+  }
+  if (mode == GRAD_SGHMC) {
+    // Σ pW² of this block, per chain whose trajectory ends at this iteration (E_new, hmc.py:74-79)
+    for (int cc = 0; cc < ncb; ++cc) {
+      if (a.iter != a.n_iter[c0 + cc] - 1) continue;
+      double v = 0.0;
+#pragma unroll
+      for (int q = 0; q < EPT; ++q) {
+        const int e = tid + q * NTH;
+        const int j = e - (e / NT) * NT;
+        if (ok[q] && j / K == cc) v += (double)pnew[q] * (double)pnew[q];
+      }
+      ksh[tid] = v;
+      __syncthreads();
+      for (int s = NTH / 2; s > 0; s >>= 1) {
+        if (tid < s) ksh[tid] += ksh[tid + s];
+        __syncthreads();
+      }
+      if (tid == 0) a.kin_part[(size_t)blockIdx.x * a.C + c0 + cc] = ksh[0];
+      __syncthreads();
     }
   }
 
   if (blockIdx.x == 0) {  // bias: Σ_rows(y−ŷ) from the k_fwd row partials (softmax.py:55,59-60)
-    for (int j = tid; j < ncols; j += 256) {
-      const int cc = j / a.K, k = j - cc * a.K, c = c0 + cc;
-      const int col = n0 + j;
-      if (a.mode == GRAD_SGHMC && a.iter >= a.n_iter[c]) continue;
-      T cs = T(0);
-      for (int rb = 0; rb < a.nRB; ++rb) cs += a.colsum_part[(size_t)rb * a.N + col];
-      if (a.mode == GRAD_OUT) {
-        a.gb[col] = -(cs - a.alpha * a.bsrc[col]);
-      } else if (a.mode == GRAD_SGHMC) {
-        const T bb = a.b[col];
-        T p = a.pb[col];
-        const T bp = bb + a.eps * p;
-        const T gr = -(cs - a.alpha * bp);
-        const T z = (T)noise_at(a, c, (uint32_t)(DK + k));
-        p = (a.one_minus_eps * p + a.eps * gr) + a.noise_scale * z;
-        a.pb[col] = p;
-        a.b[col] = bp;
-      } else {
-        const T bb = a.b[col];
-        const T gr = -(cs - a.alpha * bb);
-        const T z = (T)noise_at(a, c, (uint32_t)(DK + k));
-        T p = a.noise_scale * z;
-        p = p + a.m_half_eps * gr;
-        a.b[col] = bb + p;
+    constexpr int G = NTH / NT;
+    const int j = tid % NT, grp = tid / NT;
+    T s = T(0);
+    if (j < ncols && grp < G) {
+      const T* src = a.colsum_part + n0 + j;
+      int rb = grp;
+      for (; rb + 3 * G < a.nRB; rb += 4 * G) {
+        const T v0 = src[(size_t)rb * a.N], v1 = src[(size_t)(rb + G) * a.N];
+        const T v2 = src[(size_t)(rb + 2 * G) * a.N], v3 = src[(size_t)(rb + 3 * G) * a.N];
+        s += ((v0 + v1) + v2) + v3;
+      }
+      for (; rb < a.nRB; rb += G) s += src[(size_t)rb * a.N];
+    }
+    csr[tid] = s;
+    __syncthreads();
+    T pb_new = T(0);
+    if (tid < ncols) {
+      const int cc = tid / K, k = tid - cc * K, c = c0 + cc, col = n0 + tid;
+      const bool active = mode != GRAD_SGHMC || a.iter < a.n_iter[c];
+      if (active) {
+        T cs = csr[tid];
+        for (int q = 1; q < G; ++q) cs += csr[q * NT + tid];
+        const int DK = a.D * K;
+        if (mode == GRAD_OUT) {
+          a.gb[col] = -(cs - a.alpha * a.bsrc[col]);
+        } else if (mode == GRAD_SGHMC) {
+          const T bb = a.b[col];
+          T p = a.pb[col];
+          const T bp = bb + a.eps * p;
+          const T gr = -(cs - a.alpha * bp);
+          const T z = (T)noise_at(a, c, (uint32_t)(DK + k));
+          p = (a.one_minus_eps * p + a.eps * gr) + a.noise_scale * z;
+          a.pb[col] = p;
+          a.b[col] = bp;
+          pb_new = p;
+        } else {
+          const T bb = a.b[col];
+          const T gr = -(cs - a.alpha * bb);
+          const T z = (T)noise_at(a, c, (uint32_t)(DK + k));
+          T p = a.noise_scale * z;
+          p = p + a.m_half_eps * gr;
+          a.b[col] = bb + p;
+        }
+      }
+    }
+    if (mode == GRAD_SGHMC) {
+      __syncthreads();
+      csr[tid] = pb_new;      // reuse as staging for Σ pb² of finished chains
+      __syncthreads();
+      if (tid < ncb && a.iter == a.n_iter[c0 + tid] - 1) {
+        double v = 0.0;
+        for (int k = 0; k < K; ++k) {
+          const double p = (double)csr[tid * K + k];
+          v += p * p;
+        }
+        a.kinb[c0 + tid] = v;
       }
     }
   }
 }
 
-// ------------------------------------------------------------------ SGHMC step init / accept
+// ------------------------------------------------------------------ SGHMC step init / commit / accept
+// grid (nDB, C): block x handles features [16x, 16x+16) of chain y; block 0 also the bias.
 template <typename T>
 __global__ __launch_bounds__(256) void k_sghmc_init(InitArgs<T> a) {
-  const int P = a.D * a.K + a.K;
-  const int DK = a.D * a.K;
-  const int total = a.C * P;
-  for (int idx = blockIdx.x * 256 + threadIdx.x; idx < total; idx += gridDim.x * 256) {
-    const int c = idx / P, e = idx - c * P;
+  __shared__ double ksh[256];
+  const int c = blockIdx.y, tid = threadIdx.x;
+  const int K = a.K;
+  const int d0 = blockIdx.x * 16;
+  const bool take = a.prev_acc && a.prev_acc[c];
+  const bool drift = a.n_iter[c] >= 1;
+  double kin = 0.0;
+  for (int e = tid; e < 16 * K; e += 256) {
+    const int i = e / K, k = e - (e / K) * K, d = d0 + i;
+    if (d >= a.D) continue;
+    const size_t w = (size_t)d * a.N + c * K + k;
     double z;
-    if (a.noise_mode == HMCX_NOISE_BUFFER) z = a.noise[a.noff[c] + e];
-    else z = philox_normal(a.seed, a.chain0 + c, a.step, 0u, (uint32_t)e);
-    const T p = (T)z;                                             // hmc.py:86 N(0,1)
-    if (e < DK) {
-      const int d = e / a.K, k = e - d * a.K;
-      const size_t w = (size_t)d * a.N + c * a.K + k;
-      a.p0W[w] = p;
-      a.pW[w] = p;
-      const T q = a.W[w];
-      a.Wwork[w] = (a.n_iter[c] >= 1) ? q + a.eps * p : q;        // sghmc.py:32 (iteration 0)
-    } else {
-      const int col = c * a.K + (e - DK);
-      a.p0b[col] = p;
+    if (a.noise_mode == HMCX_NOISE_BUFFER) z = a.noise[a.noff[c] + d * K + k];
+    else z = (double)philox_normal(a.seed, a.chain0 + c, a.step, 0u, (uint32_t)(d * K + k));
+    const T p = (T)z;                                                     // hmc.py:86 N(0,1)
+    T q = a.W[w];
+    if (take) { q = a.Wwork[w]; a.W[w] = q; }                             // commit (sghmc.py:37)
+    a.pW[w] = p;
+    a.Wwork[w] = drift ? q + a.eps * p : q;                               // sghmc.py:32 (iteration 0)
+    kin += (double)p * (double)p;
+  }
+  ksh[tid] = kin;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (tid < s) ksh[tid] += ksh[tid + s];
+    __syncthreads();
+  }
+  if (tid == 0) a.kin0_part[(size_t)blockIdx.x * a.C + c] = ksh[0];
+  if (blockIdx.x == 0) {
+    __syncthreads();
+    double kb = 0.0;
+    if (tid < K) {
+      const int col = c * K + tid;
+      double z;
+      if (a.noise_mode == HMCX_NOISE_BUFFER) z = a.noise[a.noff[c] + a.D * K + tid];
+      else z = (double)philox_normal(a.seed, a.chain0 + c, a.step, 0u, (uint32_t)(a.D * K + tid));
+      const T p = (T)z;
+      T q = a.b[col];
+      if (take) { q = a.bwork[col]; a.b[col] = q; }
       a.pb[col] = p;
-      a.bwork[col] = a.b[col];
+      a.bwork[col] = q;
+      kb = (double)p * (double)p;
     }
+    ksh[tid] = kb;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+      if (tid < s) ksh[tid] += ksh[tid + s];
+      __syncthreads();
+    }
+    if (tid == 0) a.kin0b[c] = ksh[0];
   }
 }
 
-__device__ inline double block_sum256(double v, double* sh) {
+template <typename T>
+__global__ __launch_bounds__(256) void k_sghmc_commit(CommitArgs<T> a) {
+  const int c = blockIdx.y, tid = threadIdx.x;
+  if (!a.acc[c]) return;
+  const int K = a.K, d0 = blockIdx.x * 16;
+  for (int e = tid; e < 16 * K; e += 256) {
+    const int i = e / K, k = e - (e / K) * K, d = d0 + i;
+    if (d >= a.D) continue;
+    const size_t w = (size_t)d * a.N + c * K + k;
+    a.W[w] = a.Wwork[w];
+  }
+  if (blockIdx.x == 0 && tid < K) a.b[c * K + tid] = a.bwork[c * K + tid];
+}
+
+// Deterministic parallel sum of a[i*stride] for i < n over a 64-thread block.
+__device__ inline double block_sum64(const double* a, int n, int stride, double* sh) {
   const int t = threadIdx.x;
-  sh[t] = v;
+  double s = 0.0;
+  for (int i = t; i < n; i += 64) s += a[(size_t)i * stride];
+  sh[t] = s;
   __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
-    if (t < s) sh[t] = sh[t] + sh[t + s];
+  for (int w = 32; w > 0; w >>= 1) {
+    if (t < w) sh[t] += sh[t + w];
     __syncthreads();
   }
   const double r = sh[0];
@@ -336,33 +513,20 @@ __device__ inline double block_sum256(double v, double* sh) {
 }
 
 template <typename T>
-__global__ __launch_bounds__(256) void k_sghmc_accept(AcceptArgs<T> a) {
-  __shared__ double sh[256];
-  const int c = blockIdx.x, t = threadIdx.x;
-  const int DK = a.D * a.K;
+__global__ __launch_bounds__(64) void k_sghmc_accept(AcceptArgs<T> a) {
+  __shared__ double sh[64];
+  const int c = blockIdx.x;
   const int n = a.n_iter[c];
-  double s0 = 0.0, s1 = 0.0;
-  for (int e = t; e < DK; e += 256) {
-    const int d = e / a.K, k = e - d * a.K;
-    const size_t w = (size_t)d * a.N + c * a.K + k;
-    const double x0 = (double)a.p0W[w], x1 = (double)a.pW[w];
-    s0 += x0 * x0;
-    s1 += x1 * x1;
+  // hmc.py:67-79: E = nlp + ½Σp² (vars in order weights, bias); A = min(1, exp(E_cur − E_new))
+  const double ll0 = block_sum64(a.ll0_part + c, a.nRB, a.C, sh);
+  const double S0W = block_sum64(a.kin0_part + c, a.nDB, a.C, sh);
+  double ll1 = 0.0, S1W = 0.0;
+  if (n > 0) {
+    ll1 = block_sum64(a.ll1_part + c, a.nRB, a.C, sh);
+    S1W = block_sum64(a.kin1_part + c, a.nDB, a.C, sh);
   }
-  const double S0W = block_sum256(s0, sh), S1W = block_sum256(s1, sh);
-  s0 = 0.0; s1 = 0.0;
-  for (int k = t; k < a.K; k += 256) {
-    const double x0 = (double)a.p0b[c * a.K + k], x1 = (double)a.pb[c * a.K + k];
-    s0 += x0 * x0;
-    s1 += x1 * x1;
-  }
-  const double S0b = block_sum256(s0, sh), S1b = block_sum256(s1, sh);
-  __shared__ int acc_sh;
-  if (t == 0) {
-    // hmc.py:67-79: E = nlp + ½Σp² (vars in order weights, bias); A = min(1, exp(E_cur − E_new))
-    double ll0 = 0.0;
-    for (int rb = 0; rb < a.nRB; ++rb) ll0 += a.ll0_part[(size_t)rb * a.C + c];
-    const double K0 = (0.0 + 0.5 * S0W) + 0.5 * S0b;
+  if (threadIdx.x == 0) {
+    const double K0 = (0.0 + 0.5 * S0W) + 0.5 * a.kin0b[c];
     const double Ecur = a.neg_inv_n * (ll0 + a.log_prior) + K0;
     double A, Enew, llq;
     int acc;
@@ -370,9 +534,7 @@ __global__ __launch_bounds__(256) void k_sghmc_accept(AcceptArgs<T> a) {
       A = 1.0; Enew = Ecur; llq = ll0;
       acc = a.u[c] < A;
     } else {
-      double ll1 = 0.0;
-      for (int rb = 0; rb < a.nRB; ++rb) ll1 += a.ll1_part[(size_t)rb * a.C + c];
-      const double K1 = (0.0 + 0.5 * S1W) + 0.5 * S1b;
+      const double K1 = (0.0 + 0.5 * S1W) + 0.5 * a.kin1b[c];
       Enew = a.neg_inv_n * (ll1 + a.log_prior) + K1;
       const double x = exp(Ecur - Enew);
       A = (x < 1.0) ? x : 1.0;                                    // Python min(1, x): NaN -> 1
@@ -380,43 +542,38 @@ __global__ __launch_bounds__(256) void k_sghmc_accept(AcceptArgs<T> a) {
       llq = acc ? ll1 : ll0;
     }
     a.out_A[c] = A;
-    a.out_acc[c] = acc;
+    // n == 0: q_new is q (sghmc.py:22), nothing to commit; k_fix_acc reports the flag at the end
+    a.out_acc[c] = acc && n > 0;
     a.out_ll[c] = llq;
     if (a.out_E) { a.out_E[2 * c] = Ecur; a.out_E[2 * c + 1] = Enew; }
-    acc_sh = acc && (n > 0);
-  }
-  __syncthreads();
-  if (acc_sh) {                                                  // sghmc.py:36-38
-    for (int e = t; e < DK; e += 256) {
-      const int d = e / a.K, k = e - d * a.K;
-      const size_t w = (size_t)d * a.N + c * a.K + k;
-      a.W[w] = a.Wwork[w];
-    }
-    for (int k = t; k < a.K; k += 256) a.b[c * a.K + k] = a.bwork[c * a.K + k];
   }
 }
 
-__global__ void k_reduce_ll(const double* ll_part, int nRB, int C, double* out) {
+__global__ void k_fix_acc(const int32_t* n_iter, const double* u, int32_t* acc, int n) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s = 0.0;
-  for (int rb = 0; rb < nRB; ++rb) s += ll_part[(size_t)rb * C + c];
-  out[c] = s;
+  if (c < n && n_iter[c] <= 0) acc[c] = u[c] < 1.0;
+}
+
+__global__ void k_reduce_ll(const double* ll_part, int nRB, int C, double* out) {
+  __shared__ double sh[64];
+  const int c = blockIdx.x;
+  const double s = block_sum64(ll_part + c, nRB, C, sh);
+  if (threadIdx.x == 0) out[c] = s;
 }
 
 // ------------------------------------------------------------------ host-side launchers
 template <typename T>
 static hipError_t launch_fwd(const FwdArgs<T>& a, const Tiling& t, hipStream_t st) {
-  dim3 grid(t.nRB, t.nCT), block(256);
+  dim3 grid(t.nRB, t.nCT);
   const bool vec = (a.D % 4) == 0;
-#define HMCX_FWD(NB)                                                                   \
-  if (vec) hipLaunchKernelGGL((k_fwd<T, NB, true>), grid, block, 0, st, a);            \
-  else hipLaunchKernelGGL((k_fwd<T, NB, false>), grid, block, 0, st, a);
+#define HMCX_FWD(NB, NW)                                                                          \
+  if (vec) hipLaunchKernelGGL((k_fwd<T, NB, true, NW>), grid, dim3(NW * 64), 0, st, a);           \
+  else hipLaunchKernelGGL((k_fwd<T, NB, false, NW>), grid, dim3(NW * 64), 0, st, a);
   switch (t.NBLK) {
-    case 1: HMCX_FWD(1) break;
-    case 2: HMCX_FWD(2) break;
-    case 3: HMCX_FWD(3) break;
-    default: HMCX_FWD(4) break;
+    case 1: HMCX_FWD(1, 8) break;
+    case 2: HMCX_FWD(2, 8) break;
+    case 3: HMCX_FWD(3, 4) break;
+    default: HMCX_FWD(4, 4) break;
   }
 #undef HMCX_FWD
   return hipGetLastError();
@@ -424,12 +581,12 @@ static hipError_t launch_fwd(const FwdArgs<T>& a, const Tiling& t, hipStream_t s
 
 template <typename T>
 static hipError_t launch_grad(const GradArgs<T>& a, const Tiling& t, hipStream_t st) {
-  dim3 grid(t.nDB, t.nCT), block(256);
+  dim3 grid(t.nDB, t.nCT);
   switch (t.NBLK) {
-    case 1: hipLaunchKernelGGL((k_grad<T, 1>), grid, block, 0, st, a); break;
-    case 2: hipLaunchKernelGGL((k_grad<T, 2>), grid, block, 0, st, a); break;
-    case 3: hipLaunchKernelGGL((k_grad<T, 3>), grid, block, 0, st, a); break;
-    default: hipLaunchKernelGGL((k_grad<T, 4>), grid, block, 0, st, a); break;
+    case 1: hipLaunchKernelGGL((k_grad<T, 1, 8>), grid, dim3(512), 0, st, a); break;
+    case 2: hipLaunchKernelGGL((k_grad<T, 2, 8>), grid, dim3(512), 0, st, a); break;
+    case 3: hipLaunchKernelGGL((k_grad<T, 3, 4>), grid, dim3(256), 0, st, a); break;
+    default: hipLaunchKernelGGL((k_grad<T, 4, 4>), grid, dim3(256), 0, st, a); break;
   }
   return hipGetLastError();
 }
@@ -448,13 +605,23 @@ Tiling make_tiling(int B, int D, int K, int C) {
 
 template <typename T>
 static FwdArgs<T> fwd_args(const void* X, const void* Y, const void* W, const void* b, int B, int D, int K,
-                           int C, const Tiling& t, int mode, double clip_hi, double clip_lo) {
+                           int C, const Tiling& t, int mode) {
   FwdArgs<T> a{};
   a.X = (const T*)X; a.Y = (const T*)Y; a.W = (const T*)W; a.b = (const T*)b;
   a.B = B; a.D = D; a.K = K; a.C = C; a.N = C * K; a.CB = t.CB;
   a.mode = mode;
-  a.clip_hi = (T)clip_hi; a.clip_lo = (T)clip_lo;
+  a.clip_hi = (T)CLIP_HI; a.clip_lo = (T)CLIP_LO;
   return a;
+}
+
+template <typename T>
+static GradArgs<T> grad_args(const T* X, const T* diff, const T* csp, int B, int D, int K, int C, const Tiling& t,
+                             int mode, double alpha) {
+  GradArgs<T> g{};
+  g.X = X; g.diff = diff; g.colsum_part = csp;
+  g.B = B; g.D = D; g.K = K; g.C = C; g.N = C * K; g.CB = t.CB; g.nRB = t.nRB; g.nDB = t.nDB; g.P = D * K + K;
+  g.mode = mode; g.alpha = (T)alpha;
+  return g;
 }
 
 // ------------------------------------------------------------------ entry points (typed)
@@ -471,13 +638,10 @@ int softmax_grad_t(hmcx_ctx* ctx, const void* X, const void* Y, int B, int D, in
     csp = ws.take<T>((size_t)t.nRB * N);
   } while (ws.retry());
   if (ws.failed) return HMCX_ENOMEM;
-  FwdArgs<T> f = fwd_args<T>(X, Y, W, b, B, D, K, C, t, FWD_GRAD, CLIP_HI, CLIP_LO);
+  FwdArgs<T> f = fwd_args<T>(X, Y, W, b, B, D, K, C, t, FWD_GRAD);
   f.diff = diff; f.colsum_part = csp;
   HMCX_HIP(ctx, launch_fwd<T>(f, t, ctx->stream));
-  GradArgs<T> g{};
-  g.X = (const T*)X; g.diff = diff; g.colsum_part = csp;
-  g.B = B; g.D = D; g.K = K; g.C = C; g.N = N; g.CB = t.CB; g.nRB = t.nRB; g.P = D * K + K;
-  g.mode = GRAD_OUT; g.alpha = (T)alpha;
+  GradArgs<T> g = grad_args<T>((const T*)X, diff, csp, B, D, K, C, t, GRAD_OUT, alpha);
   g.Wsrc = (const T*)W; g.bsrc = (const T*)b; g.gW = (T*)gW; g.gb = (T*)gb;
   HMCX_HIP(ctx, launch_grad<T>(g, t, ctx->stream));
   return HMCX_OK;
@@ -494,10 +658,10 @@ int softmax_loglik_t(hmcx_ctx* ctx, const void* X, const void* Y, int B, int D, 
     llp = ws.take<double>((size_t)t.nRB * C);
   } while (ws.retry());
   if (ws.failed) return HMCX_ENOMEM;
-  FwdArgs<T> f = fwd_args<T>(X, Y, W, b, B, D, K, C, t, FWD_LL, CLIP_HI, CLIP_LO);
+  FwdArgs<T> f = fwd_args<T>(X, Y, W, b, B, D, K, C, t, FWD_LL);
   f.ll_part = llp;
   HMCX_HIP(ctx, launch_fwd<T>(f, t, ctx->stream));
-  hipLaunchKernelGGL(k_reduce_ll, dim3((C + 63) / 64), dim3(64), 0, ctx->stream, llp, t.nRB, C, ll);
+  hipLaunchKernelGGL(k_reduce_ll, dim3(C), dim3(64), 0, ctx->stream, llp, t.nRB, C, ll);
   HMCX_HIP(ctx, hipGetLastError());
   return HMCX_OK;
 }
@@ -506,7 +670,7 @@ template <typename T>
 int softmax_predict_t(hmcx_ctx* ctx, const void* X, int B, int D, int K, int C, const void* W, const void* b,
                       void* prob) {
   const Tiling t = make_tiling(B, D, K, C);
-  FwdArgs<T> f = fwd_args<T>(X, nullptr, W, b, B, D, K, C, t, FWD_PRED, CLIP_HI, CLIP_LO);
+  FwdArgs<T> f = fwd_args<T>(X, nullptr, W, b, B, D, K, C, t, FWD_PRED);
   f.prob = (T*)prob;
   HMCX_HIP(ctx, launch_fwd<T>(f, t, ctx->stream));
   return HMCX_OK;
@@ -514,12 +678,19 @@ int softmax_predict_t(hmcx_ctx* ctx, const void* X, int B, int D, int K, int C, 
 
 template <typename T>
 int sghmc_run_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
-  const int B = s->B, D = s->D, K = s->K, C = s->C, N = C * K, P = D * K + K;
+  const int B = s->B, D = s->D, K = s->K, C = s->C, N = C * K;
+  if (C == 1 && ctx->sghmc_path != 1) {   // single chain: persistent kernel (hmcx_persist.hip)
+    const PersistPlan pl = plan_persist(B, D, K, sizeof(T), ctx->num_cus, ctx->lds_max);
+    if (pl.ok) return sghmc_persist_t<T>(ctx, s, pl);
+    if (ctx->sghmc_path == 2) return set_error(ctx, HMCX_EUNSUPPORTED, "persistent SGHMC: shape not supported");
+  } else if (ctx->sghmc_path == 2) {
+    return set_error(ctx, HMCX_EUNSUPPORTED, "persistent SGHMC needs C == 1");
+  }
   const Tiling t = make_tiling(B, D, K, C);
   const size_t nsc = (size_t)s->n_steps * C;
   Workspace ws(ctx);
-  T *Wwork, *bwork, *pW, *pb, *p0W, *p0b, *diff, *csp;
-  double *ll0, *ll1, *d_u;
+  T *Wwork, *bwork, *pW, *pb, *diff, *csp;
+  double *ll0, *ll1, *k0p, *k0b, *k1p, *k1b, *d_u;
   int32_t* d_niter;
   int64_t* d_noff;
   do {
@@ -528,19 +699,20 @@ int sghmc_run_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
     bwork = ws.take<T>(N);
     pW = ws.take<T>((size_t)D * N);
     pb = ws.take<T>(N);
-    p0W = ws.take<T>((size_t)D * N);
-    p0b = ws.take<T>(N);
     diff = ws.take<T>((size_t)B * N);
     csp = ws.take<T>((size_t)t.nRB * N);
     ll0 = ws.take<double>((size_t)t.nRB * C);
     ll1 = ws.take<double>((size_t)t.nRB * C);
+    k0p = ws.take<double>((size_t)t.nDB * C);
+    k1p = ws.take<double>((size_t)t.nDB * C);
+    k0b = ws.take<double>(C);
+    k1b = ws.take<double>(C);
     d_niter = ws.take<int32_t>(nsc);
     d_u = ws.take<double>(nsc);
     d_noff = ws.take<int64_t>(nsc);
   } while (ws.retry());
   if (ws.failed) return HMCX_ENOMEM;
   begin_call(ctx);
-  // per-call schedule -> device
   int rc = upload(ctx, d_niter, s->n_iter, nsc * sizeof(int32_t));
   if (rc) return rc;
   if ((rc = upload(ctx, d_u, s->u_accept, nsc * sizeof(double)))) return rc;
@@ -549,9 +721,8 @@ int sghmc_run_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
 
   const T* X = (const T*)s->X;
   const T* Y = (const T*)s->Y;
-  const int init_grid = (int)std::min<long>(1024, ((long)C * P + 255) / 256);
-  hipStream_t st = ctx->stream;
   GraphScope gs(ctx);
+  hipStream_t st = ctx->stream;
   for (int st_i = 0; st_i < s->n_steps; ++st_i) {
     const T* Xs = X + (size_t)s->row0[st_i] * D;
     const T* Ys = Y + (size_t)s->row0[st_i] * K;
@@ -563,29 +734,29 @@ int sghmc_run_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
     const uint32_t step_id = s->step_base + (uint32_t)st_i;
 
     InitArgs<T> ia{};
-    ia.D = D; ia.K = K; ia.C = C; ia.N = N;
+    ia.D = D; ia.K = K; ia.C = C; ia.N = N; ia.nDB = t.nDB;
     ia.eps = (T)eps; ia.n_iter = niter;
+    ia.prev_acc = st_i > 0 ? s->out_accepted + (size_t)(st_i - 1) * C : nullptr;
     ia.noise_mode = s->noise_mode; ia.noise = s->noise; ia.noff = noff;
     ia.seed = s->seed; ia.chain0 = s->chain0; ia.step = step_id;
-    ia.W = (const T*)s->W; ia.b = (const T*)s->b;
-    ia.Wwork = Wwork; ia.bwork = bwork; ia.pW = pW; ia.pb = pb; ia.p0W = p0W; ia.p0b = p0b;
-    hipLaunchKernelGGL((k_sghmc_init<T>), dim3(init_grid), dim3(256), 0, st, ia);
+    ia.W = (T*)s->W; ia.b = (T*)s->b;
+    ia.Wwork = Wwork; ia.bwork = bwork; ia.pW = pW; ia.pb = pb;
+    ia.kin0_part = k0p; ia.kin0b = k0b;
+    hipLaunchKernelGGL((k_sghmc_init<T>), dim3(t.nDB, C), dim3(256), 0, st, ia);
     HMCX_HIP(ctx, hipGetLastError());
 
-    FwdArgs<T> f0 = fwd_args<T>(Xs, Ys, s->W, s->b, B, D, K, C, t, FWD_LL, CLIP_HI, CLIP_LO);
+    FwdArgs<T> f0 = fwd_args<T>(Xs, Ys, s->W, s->b, B, D, K, C, t, FWD_LL);
     f0.ll_part = ll0;
     HMCX_HIP(ctx, launch_fwd<T>(f0, t, st));
 
-    FwdArgs<T> f = fwd_args<T>(Xs, Ys, Wwork, bwork, B, D, K, C, t, FWD_SGHMC, CLIP_HI, CLIP_LO);
+    FwdArgs<T> f = fwd_args<T>(Xs, Ys, Wwork, bwork, B, D, K, C, t, FWD_SGHMC);
     f.pb = pb; f.eps = (T)eps; f.n_iter = niter;
     f.diff = diff; f.colsum_part = csp; f.ll_part = ll1;
-    GradArgs<T> g{};
-    g.X = Xs; g.diff = diff; g.colsum_part = csp;
-    g.B = B; g.D = D; g.K = K; g.C = C; g.N = N; g.CB = t.CB; g.nRB = t.nRB; g.P = P;
-    g.mode = GRAD_SGHMC;
-    g.alpha = (T)s->alpha; g.eps = (T)eps; g.one_minus_eps = (T)(1.0 - eps); g.noise_scale = (T)(2.0 * eps);
+    GradArgs<T> g = grad_args<T>(Xs, diff, csp, B, D, K, C, t, GRAD_SGHMC, s->alpha);
+    g.eps = (T)eps; g.one_minus_eps = (T)(1.0 - eps); g.noise_scale = (T)(2.0 * eps);
     g.n_iter = niter;
     g.W = Wwork; g.b = bwork; g.pW = pW; g.pb = pb;
+    g.kin_part = k1p; g.kinb = k1b;
     g.noise_mode = s->noise_mode; g.noise = s->noise; g.noff = noff;
     g.seed = s->seed; g.chain0 = s->chain0; g.step = step_id;
     for (int it = 0; it < maxit; ++it) {
@@ -596,25 +767,34 @@ int sghmc_run_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
       HMCX_HIP(ctx, launch_grad<T>(g, t, st));
     }
     AcceptArgs<T> aa{};
-    aa.D = D; aa.K = K; aa.C = C; aa.N = N; aa.nRB = t.nRB;
+    aa.C = C; aa.nRB = t.nRB; aa.nDB = t.nDB;
     aa.n_iter = niter; aa.u = d_u + (size_t)st_i * C;
     aa.neg_inv_n = -1.0 / (double)B; aa.log_prior = s->log_prior;
-    aa.p0W = p0W; aa.p0b = p0b; aa.pW = pW; aa.pb = pb;
+    aa.kin0_part = k0p; aa.kin0b = k0b; aa.kin1_part = k1p; aa.kin1b = k1b;
     aa.ll0_part = ll0; aa.ll1_part = ll1;
-    aa.Wwork = Wwork; aa.bwork = bwork; aa.W = (T*)s->W; aa.b = (T*)s->b;
     aa.out_A = s->out_A + (size_t)st_i * C;
     aa.out_acc = s->out_accepted + (size_t)st_i * C;
     aa.out_ll = s->out_ll + (size_t)st_i * C;
     aa.out_E = s->out_E ? s->out_E + (size_t)st_i * C * 2 : nullptr;
-    hipLaunchKernelGGL((k_sghmc_accept<T>), dim3(C), dim3(256), 0, st, aa);
+    hipLaunchKernelGGL((k_sghmc_accept<T>), dim3(C), dim3(64), 0, st, aa);
     HMCX_HIP(ctx, hipGetLastError());
   }
+  // commit the last step's proposal, then report n_iter == 0 steps as accepted (A = 1 > u)
+  CommitArgs<T> ca{};
+  ca.D = D; ca.K = K; ca.C = C; ca.N = N;
+  ca.acc = s->out_accepted + (size_t)(s->n_steps - 1) * C;
+  ca.Wwork = Wwork; ca.bwork = bwork; ca.W = (T*)s->W; ca.b = (T*)s->b;
+  hipLaunchKernelGGL((k_sghmc_commit<T>), dim3(t.nDB, C), dim3(256), 0, st, ca);
+  HMCX_HIP(ctx, hipGetLastError());
+  hipLaunchKernelGGL(k_fix_acc, dim3((unsigned)((nsc + 255) / 256)), dim3(256), 0, st, d_niter, d_u,
+                     s->out_accepted, (int)nsc);
+  HMCX_HIP(ctx, hipGetLastError());
   return gs.finish();
 }
 
 template <typename T>
 int sgld_run_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
-  const int B = s->B, D = s->D, K = s->K, C = s->C, N = C * K, P = D * K + K;
+  const int B = s->B, D = s->D, K = s->K, C = s->C, N = C * K;
   const Tiling t = make_tiling(B, D, K, C);
   const size_t nsc = (size_t)s->n_steps * C;
   Workspace ws(ctx);
@@ -635,20 +815,17 @@ int sgld_run_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
     return rc;
   const T* X = (const T*)s->X;
   const T* Y = (const T*)s->Y;
-  hipStream_t st = ctx->stream;
   GraphScope gs(ctx);
+  hipStream_t st = ctx->stream;
   for (int st_i = 0; st_i < s->n_steps; ++st_i) {
     const T* Xs = X + (size_t)s->row0[st_i] * D;
     const T* Ys = Y + (size_t)s->row0[st_i] * K;
     const double eps = s->eps[st_i];
-    FwdArgs<T> f = fwd_args<T>(Xs, Ys, s->W, s->b, B, D, K, C, t, FWD_GRAD, CLIP_HI, CLIP_LO);
+    FwdArgs<T> f = fwd_args<T>(Xs, Ys, s->W, s->b, B, D, K, C, t, FWD_GRAD);
     f.diff = diff; f.colsum_part = csp;
     HMCX_HIP(ctx, launch_fwd<T>(f, t, st));
-    GradArgs<T> g{};
-    g.X = Xs; g.diff = diff; g.colsum_part = csp;
-    g.B = B; g.D = D; g.K = K; g.C = C; g.N = N; g.CB = t.CB; g.nRB = t.nRB; g.P = P;
-    g.mode = GRAD_SGLD;
-    g.alpha = (T)s->alpha; g.eps = (T)eps;
+    GradArgs<T> g = grad_args<T>(Xs, diff, csp, B, D, K, C, t, GRAD_SGLD, s->alpha);
+    g.eps = (T)eps;
     g.noise_scale = (T)(2.0 * eps);                               // sgld.py:43
     g.m_half_eps = (T)(-0.5 * eps);                               // sgld.py:37
     g.W = (T*)s->W; g.b = (T*)s->b;
@@ -656,11 +833,10 @@ int sgld_run_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
     g.seed = s->seed; g.chain0 = s->chain0; g.step = s->step_base + (uint32_t)st_i; g.slot = 0;
     HMCX_HIP(ctx, launch_grad<T>(g, t, st));
     if (s->want_ll && s->want_ll[st_i] && s->out_ll) {
-      FwdArgs<T> fl = fwd_args<T>(Xs, Ys, s->W, s->b, B, D, K, C, t, FWD_LL, CLIP_HI, CLIP_LO);
+      FwdArgs<T> fl = fwd_args<T>(Xs, Ys, s->W, s->b, B, D, K, C, t, FWD_LL);
       fl.ll_part = llp;
       HMCX_HIP(ctx, launch_fwd<T>(fl, t, st));
-      hipLaunchKernelGGL(k_reduce_ll, dim3((C + 63) / 64), dim3(64), 0, st, llp, t.nRB, C,
-                         s->out_ll + (size_t)st_i * C);
+      hipLaunchKernelGGL(k_reduce_ll, dim3(C), dim3(64), 0, st, llp, t.nRB, C, s->out_ll + (size_t)st_i * C);
       HMCX_HIP(ctx, hipGetLastError());
     }
   }

@@ -43,11 +43,15 @@ int hmcx_version(void);
 int hmcx_create(int device, hmcx_ctx** out);
 int hmcx_destroy(hmcx_ctx* ctx);
 const char* hmcx_last_error(const hmcx_ctx* ctx);
-/* Use an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream); NULL restores the own stream. */
+/* Run on an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream); NULL = the legacy
+ * default stream.  A new context runs on its own non-blocking stream until this is called. */
 int hmcx_set_stream(hmcx_ctx* ctx, void* hip_stream);
 int hmcx_synchronize(hmcx_ctx* ctx);
 /* Capture each hmcx_*_run call into a hipGraph and replay it (1) or launch eagerly (0). */
 int hmcx_set_graph_mode(hmcx_ctx* ctx, int enabled);
+/* SGHMC implementation: 0 = auto (persistent single-launch kernel when C == 1 and the shape
+ * fits, else kernel-per-phase), 1 = kernel-per-phase, 2 = persistent only (error otherwise). */
+int hmcx_set_sghmc_path(hmcx_ctx* ctx, int path);
 
 /* Philox4x32-10 uniforms in [0,1), bit-identical to the device generator (host function). */
 void hmcx_philox_uniforms(uint64_t seed, uint32_t chain, uint32_t step, uint32_t slot,

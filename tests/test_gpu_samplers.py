@@ -37,11 +37,13 @@ def _run_oracle(c):
     return post, logp, s.trace, s.out.getvalue()
 
 
-def _run_gpu(c, dtype=torch.float64, noise="numpy", seed=0):
+def _run_gpu(c, dtype=torch.float64, noise="numpy", seed=0, path=0):
     softmax, sghmc, sgld = _gpu_classes()
     X, Y = gi.dataset(c["data_seed"], c["N"], c["D"], c["K"])
     cls = sghmc if c["kind"] == "sghmc" else sgld
-    s = cls(softmax({"alpha": c["alpha"]}, dtype=dtype, device="cuda:0"),
+    m = softmax({"alpha": c["alpha"]}, dtype=dtype, device="cuda:0")
+    m.ctx.set_sghmc_path(path)
+    s = cls(m,
             {"weights": np.zeros((c["D"], c["K"])), "bias": np.zeros(c["K"])},
             path_length=c["path_length"], step_size=c["step_size"], verbose=True, noise=noise, seed=seed)
     s.trace = []
@@ -52,11 +54,15 @@ def _run_gpu(c, dtype=torch.float64, noise="numpy", seed=0):
     return post, logp, s.trace, s.out.getvalue()
 
 
-@pytest.mark.parametrize("name", sorted(gi.TRAJ_CONFIGS))
-def test_trajectory_f64_vs_oracle_and_golden(name, golden_dir):
+_PATHS = [(n, p) for n in sorted(gi.TRAJ_CONFIGS) for p in ((1, 2) if gi.TRAJ_CONFIGS[n]["kind"] == "sghmc" else (0,))]
+
+
+@pytest.mark.parametrize("name,path", _PATHS)
+def test_trajectory_f64_vs_oracle_and_golden(name, path, golden_dir):
+    """path 1 = kernel-per-phase, 2 = persistent single-launch kernel (both must agree with NumPy)."""
     c = gi.TRAJ_CONFIGS[name]
     post_r, logp_r, tr_r, log_r = _run_oracle(c)
-    post_g, logp_g, tr_g, log_g = _run_gpu(c)
+    post_g, logp_g, tr_g, log_g = _run_gpu(c, path=path)
     # integer bookkeeping: bit-exact
     if c["kind"] == "sghmc":
         assert [t["L"] for t in tr_g] == [t["L"] for t in tr_r]
@@ -84,11 +90,12 @@ def test_trajectory_f64_vs_oracle_and_golden(name, golden_dir):
         np.testing.assert_allclose(post_g["weights"], d["post_weights"], rtol=1e-9, atol=1e-12)
 
 
-@pytest.mark.parametrize("name", ["sghmc_small", "sgld_small", "sghmc_hot"])
-def test_trajectory_f32(name):
+@pytest.mark.parametrize("name,path", [("sghmc_small", 1), ("sghmc_small", 2), ("sgld_small", 0),
+                                       ("sghmc_hot", 1), ("sghmc_hot", 2), ("sghmc_mnist", 2)])
+def test_trajectory_f32(name, path):
     c = gi.TRAJ_CONFIGS[name]
     post_r, logp_r, tr_r, _ = _run_oracle(c)
-    post_g, logp_g, tr_g, _ = _run_gpu(c, dtype=torch.float32)
+    post_g, logp_g, tr_g, _ = _run_gpu(c, dtype=torch.float32, path=path)
     if c["kind"] == "sghmc":
         assert [t["L"] for t in tr_g] == [t["L"] for t in tr_r]
     scale = np.abs(post_r["weights"]).max() + 1e-3
@@ -96,15 +103,25 @@ def test_trajectory_f32(name):
     np.testing.assert_allclose(logp_g, logp_r, rtol=1e-4)
 
 
-def test_philox_mode_runs_and_is_deterministic():
-    c = dict(gi.TRAJ_CONFIGS["sghmc_small"])
-    p1, l1, t1, _ = _run_gpu(c, noise="philox", seed=11)
-    p2, l2, t2, _ = _run_gpu(c, noise="philox", seed=11)
-    p3, l3, t3, _ = _run_gpu(c, noise="philox", seed=12)
+@pytest.mark.parametrize("path", [1, 2])
+def test_philox_mode_runs_and_is_deterministic(path):
+    c = dict(gi.TRAJ_CONFIGS["sghmc_mnist"])
+    p1, l1, t1, _ = _run_gpu(c, noise="philox", seed=11, path=path)
+    p2, l2, t2, _ = _run_gpu(c, noise="philox", seed=11, path=path)
+    p3, l3, t3, _ = _run_gpu(c, noise="philox", seed=12, path=path)
     np.testing.assert_array_equal(p1["weights"], p2["weights"])
     assert [t["L"] for t in t1] == [t["L"] for t in t2]
     assert not np.array_equal(p1["weights"], p3["weights"])
     assert np.all(np.isfinite(l1))
+
+
+def test_philox_paths_agree():
+    """Both SGHMC implementations consume the same Philox streams: same trajectory (f64)."""
+    c = dict(gi.TRAJ_CONFIGS["sghmc_mnist"])
+    p1, l1, t1, _ = _run_gpu(c, noise="philox", seed=5, path=1)
+    p2, l2, t2, _ = _run_gpu(c, noise="philox", seed=5, path=2)
+    assert [t["accepted"] for t in t1] == [t["accepted"] for t in t2]
+    np.testing.assert_allclose(p1["weights"], p2["weights"], rtol=1e-9, atol=1e-12)
 
 
 def test_philox_noise_statistics():
@@ -162,13 +179,16 @@ def test_hmc_generic_softmax_vs_golden(golden_dir):
     np.testing.assert_allclose(loss, d["loss"], rtol=1e-10)
 
 
-def test_full_size_mnist_shape_properties():
+@pytest.mark.parametrize("path", [1, 2])
+def test_full_size_mnist_shape_properties(path):
     """BASELINE config 2 size (N=60000 would be slow for the oracle; use N=5000, B=500, D=784):
     every step accepted or rejected consistently with its own A and u; logp finite; the state
     after sampling equals the last posterior sample."""
     softmax, sghmc, _ = _gpu_classes()
     X, Y = gi.dataset(0, 5000, 784, 10)
-    s = sghmc(softmax({"alpha": 0.01}), {"weights": np.zeros((784, 10)), "bias": np.zeros(10)},
+    m = softmax({"alpha": 0.01})
+    m.ctx.set_sghmc_path(path)
+    s = sghmc(m, {"weights": np.zeros((784, 10)), "bias": np.zeros(10)},
               path_length=1e-2, step_size=1e-3, noise="philox", seed=1)
     s.out = io.StringIO()
     s.trace = []
