@@ -1,0 +1,203 @@
+#!/usr/bin/env python3
+"""Headline benchmark: leapfrog-steps/sec × param-dim, MNIST-shaped softmax SGHMC (BASELINE.json).
+
+One "step" = one SGHMC step over one minibatch (reference cpu/sghmc.py:19-39, A1 completion):
+momentum draw, L−1 leapfrog iterations (each = weights sub-step + bias sub-step, i.e. one
+softmax-gradient evaluation X·W → softmax → Xᵀ·diff), energies and the MH accept — all inside
+libhmcx.  The reported unit counts leapfrog iterations (sghmc.py:28), summed over chains, times
+the parameter dimension P = 784·10 + 10 = 7850.
+
+Workload (BASELINE config 2 at N=1, config 4 at N=8): synthetic MNIST-shaped data
+(X = rand(60000, 784), one-hot labels over 10 classes), batch 500, α = 0.01, ε = 1e-3,
+λ = 1e-2 (E[L] ≈ 10.5), zero start, one chain per GPU, float64 (the reference's dtype),
+device Philox noise.  Ranks run independent chains (no communication while sampling); after the
+timed region one all-gather (RCCL) moves the per-chain log-likelihood traces to rank 0 for R̂/ESS.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+"""
+import argparse
+import io
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+D, K, B, N_DATA = 784, 10, 500, 60000
+P = D * K + K
+ALPHA, EPS, LAMBDA = 0.01, 1e-3, 1e-2
+FLOP_PER_LEAPFROG = 4.0 * B * D * K          # X·W and Xᵀ·diff: 15.68 MFLOP
+MFMA_PEAK_TFLOPS = {"f64": 78.6, "f32": 157.3}   # dense MFMA, MI355X spec (f32: MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=240, help="timed SGHMC steps per chain")
+    ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--dtype", choices=["f64", "f32"], default="f64")
+    ap.add_argument("--path", choices=["auto", "kernels", "persistent"], default="auto")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline time budget (0 = skip)")
+    return ap.parse_args()
+
+
+def synthetic_data(seed=0):
+    X = np.random.RandomState(seed).rand(N_DATA, D)
+    lab = np.random.RandomState(seed + 1).randint(0, K, N_DATA)
+    Y = np.zeros((N_DATA, K))
+    Y[np.arange(N_DATA), lab] = 1.0
+    return X, Y
+
+
+def cpu_baseline(X, Y, budget_s):
+    """The oracle (NumPy float64 restatement of the reference SGHMC, bit-exact to it) on host
+    cores: bounded sample of the same workload, leapfrogs counted the same way."""
+    from oracle import models as om, samplers as osm
+    try:
+        import threadpoolctl
+        threads = max(i.get("num_threads", 1) for i in threadpoolctl.threadpool_info()) or 1
+    except Exception:
+        threads = len(os.sched_getaffinity(0))
+    nb = 10
+    Xs, Ys = X[:nb * B], Y[:nb * B]
+    lf, t_total, steps = 0.0, 0.0, 0
+    rep = 0
+    while t_total < budget_s:
+        s = osm.sghmc(om.softmax({"alpha": ALPHA}), {"weights": np.zeros((D, K)), "bias": np.zeros(K)},
+                      path_length=LAMBDA, step_size=EPS, verbose=False)
+        s.out = io.StringIO()
+        s.trace = []
+        np.random.seed(rep)
+        t0 = time.perf_counter()
+        s.sample(epochs=1, burnin=0, batch_size=B, rng=np.random.RandomState(rep), X_train=Xs, y_train=Ys)
+        t_total += time.perf_counter() - t0
+        lf += sum(max(0.0, t["L"] - 1) for t in s.trace)
+        steps += len(s.trace)
+        rep += 1
+    return {"value": lf / t_total * P, "unit": "leapfrog-steps/s x param-dim", "cores": int(threads),
+            "kind": "port",
+            "sample": "oracle/samplers.py SGHMC (NumPy f64, bit-exact to the reference) incl. its per-10-minibatch "
+                      "log-likelihood logging: %d steps / %.0f leapfrogs on minibatches of B=500 (D=784, K=10), "
+                      "eps=1e-3, lambda=1e-2, %.1f s, %d BLAS threads" % (steps, lf, t_total, threads),
+            "lf_per_s": lf / t_total}
+
+
+def main():
+    args = parse()
+    import torch
+    from dropout_hamiltonian_montecarlo_amd import parallel
+    rank, world, local = parallel.init()
+    if world != args.gpus and rank == 0:
+        print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, world), file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    from dropout_hamiltonian_montecarlo_amd.hamiltonian.models.gpu.softmax import softmax
+    from dropout_hamiltonian_montecarlo_amd.hamiltonian.inference.gpu.sghmc import sghmc
+
+    dtype = torch.float64 if args.dtype == "f64" else torch.float32
+    X, Y = synthetic_data(0)
+    model = softmax({"alpha": ALPHA}, dtype=dtype, device=dev)
+    model.ctx.set_sghmc_path({"auto": 0, "kernels": 1, "persistent": 2}[args.path])
+    s = sghmc(model, {"weights": np.zeros((D, K)), "bias": np.zeros(K)}, path_length=LAMBDA, step_size=EPS,
+              noise="philox", seed=20251015, chain=rank)
+    s.out = io.StringIO()
+    data = s._upload_data(X, Y)                      # dataset resident in HBM before timing
+    state = s._init_state()
+    nb = N_DATA // B
+
+    def run(n_steps, step0):
+        rows = [((step0 + i) % nb) * B for i in range(n_steps)]
+        return s._run(state, data, rows, [EPS] * n_steps, None, B)
+
+    CHUNK = nb                                       # one call per epoch (120 steps)
+    # warm-up (untimed)
+    s.trace = []
+    done = 0
+    while done < args.warmup:
+        n = min(CHUNK, args.warmup - done)
+        run(n, done)
+        done += n
+    torch.cuda.synchronize()
+
+    # timed region: exactly args.steps steps per chain
+    s.trace = []
+    lls = []
+    n_calls = 0
+    model.ctx.set_timing(True)        # HIP events around each run's kernels, on the launch stream
+    parallel.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    done = 0
+    while done < args.steps:
+        n = min(CHUNK, args.steps - done)
+        res = run(n, args.warmup + done)
+        lls.append(res.ll)
+        done += n
+        n_calls += 1
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    parallel.barrier()
+    elapsed = t1 - t0
+    kern_ms, kern_n = model.ctx.get_timing()
+    model.ctx.set_timing(False)
+
+    lf_local = float(sum(max(0.0, t["L"] - 1) for t in s.trace))
+    t_max = parallel.allreduce_max(elapsed, device=dev)
+    lf_total = parallel.allreduce_sum(lf_local, device=dev)
+    value = lf_total / t_max * P
+
+    # cross-chain diagnostics: one RCCL all-gather of the per-chain ll traces (untimed)
+    trace = np.concatenate(lls)[None, :, None]       # [1 chain, T, 1]
+    allt = parallel.gather_traces(trace, device=dev)
+    diag = parallel.chain_diagnostics(allt) if allt.shape[1] >= 4 else {"rhat": np.nan, "ess": np.nan}
+
+    if rank != 0:
+        return
+    path = "persistent" if (args.path != "kernels") else "kernels"
+    assert kern_n == n_calls, (kern_n, n_calls)
+    launch_ms = kern_ms / kern_n
+    flop_per_launch = FLOP_PER_LEAPFROG * lf_local / n_calls
+    achieved = flop_per_launch / (launch_ms * 1e-3) / 1e12
+    peak = MFMA_PEAK_TFLOPS[args.dtype]
+    out = {
+        "metric": "leapfrog-steps/sec × param-dim, MNIST softmax SGHMC, 1/2/4/8 chains↔GPUs",
+        "value": value,
+        "unit": "leapfrog-steps/s x param-dim",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": t_max * 1e3 / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.dtype,
+        "data": "synthetic (MNIST-shaped X=rand(60000,784), one-hot y, K=10)",
+        "config": {"workload": "MNIST softmax regression SGHMC, 1 chain per GPU (BASELINE configs 2/4)",
+                   "global_batch": B * world, "batch_per_chain": B, "D": D, "K": K, "param_dim": P,
+                   "chains": world, "step_size": EPS, "path_length": LAMBDA, "parallelism": "independent chains x%d" % world,
+                   "impl": path},
+        "leapfrogs_per_s": lf_total / t_max,
+        "leapfrogs": lf_total,
+        "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+                     "frac": achieved / peak, "traffic": None,
+                     "kernel": ("k_sghmc_persist<%s> (one launch per %d-step call)" % (
+                         "double" if args.dtype == "f64" else "float", CHUNK)) if path == "persistent"
+                     else "kernel-per-phase sequence of one %d-step call" % CHUNK,
+                     "launch_ms": launch_ms, "flop_per_launch": flop_per_launch},
+        "diagnostics": {"rhat_ll": float(np.ravel(diag["rhat"])[0]), "ess_ll": float(np.ravel(diag["ess"])[0]),
+                        "gather": "torch.distributed all_gather (%s)" % ("nccl/RCCL" if world > 1 else "local")},
+        "cpu_baseline": None,
+    }
+    if world == 1 and args.cpu_seconds > 0:
+        cb = cpu_baseline(X, Y, args.cpu_seconds)
+        out["cpu_baseline"] = cb
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

@@ -46,7 +46,8 @@ class MvnArgs(ctypes.Structure):
 
 # Every symbol include/hmcx.h declares (checked by tests/test_capi.py).
 EXPORTS = ("hmcx_version", "hmcx_create", "hmcx_destroy", "hmcx_last_error", "hmcx_set_stream",
-           "hmcx_synchronize", "hmcx_set_graph_mode", "hmcx_set_sghmc_path", "hmcx_philox_uniforms", "hmcx_philox_normals",
+           "hmcx_synchronize", "hmcx_set_graph_mode", "hmcx_set_sghmc_path", "hmcx_set_timing", "hmcx_get_timing",
+           "hmcx_philox_uniforms", "hmcx_philox_normals",
            "hmcx_softmax_grad", "hmcx_softmax_loglik", "hmcx_softmax_predict", "hmcx_sghmc_run",
            "hmcx_sgld_run", "hmcx_hmc_mvn_run")
 
@@ -77,6 +78,8 @@ def load_library():
         lib.hmcx_synchronize.argtypes = [c_void_p]
         lib.hmcx_set_graph_mode.argtypes = [c_void_p, c_int]
         lib.hmcx_set_sghmc_path.argtypes = [c_void_p, c_int]
+        lib.hmcx_set_timing.argtypes = [c_void_p, c_int]
+        lib.hmcx_get_timing.argtypes = [c_void_p, c_dblp, ctypes.POINTER(ctypes.c_longlong)]
         lib.hmcx_philox_uniforms.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                              ctypes.c_uint32, c_dblp]
         lib.hmcx_philox_uniforms.restype = None
@@ -124,6 +127,16 @@ class Context:
     def set_sghmc_path(self, path):
         """0 auto, 1 kernel-per-phase, 2 persistent (see include/hmcx.h)."""
         self.check(self.lib.hmcx_set_sghmc_path(self.h, int(path)), "hmcx_set_sghmc_path")
+
+    def set_timing(self, on):
+        """Bracket every sampler run's kernels with HIP events on the launch stream (resets totals)."""
+        self.check(self.lib.hmcx_set_timing(self.h, 1 if on else 0), "hmcx_set_timing")
+
+    def get_timing(self):
+        """(summed kernel milliseconds, number of timed runs) since set_timing(True)."""
+        ms, n = c_double(), ctypes.c_longlong()
+        self.check(self.lib.hmcx_get_timing(self.h, ctypes.byref(ms), ctypes.byref(n)), "hmcx_get_timing")
+        return ms.value, n.value
 
     def set_graph_mode(self, on):
         self.check(self.lib.hmcx_set_graph_mode(self.h, 1 if on else 0), "hmcx_set_graph_mode")

@@ -31,6 +31,32 @@ bool Workspace::retry() {
   return true;
 }
 
+int timing_collect(hmcx_ctx* ctx) {
+  if (!ctx->t_pending) return HMCX_OK;
+  ctx->t_pending = false;
+  HMCX_HIP(ctx, hipEventSynchronize(ctx->tev1));
+  float ms = 0.f;
+  HMCX_HIP(ctx, hipEventElapsedTime(&ms, ctx->tev0, ctx->tev1));
+  ctx->t_ms += ms;
+  ctx->t_n += 1;
+  return HMCX_OK;
+}
+
+int timing_begin(hmcx_ctx* ctx, hipStream_t st) {
+  if (!ctx->timing) return HMCX_OK;
+  int rc = timing_collect(ctx);
+  if (rc) return rc;
+  HMCX_HIP(ctx, hipEventRecord(ctx->tev0, st));
+  return HMCX_OK;
+}
+
+int timing_end(hmcx_ctx* ctx, hipStream_t st) {
+  if (!ctx->timing) return HMCX_OK;
+  HMCX_HIP(ctx, hipEventRecord(ctx->tev1, st));
+  ctx->t_pending = true;
+  return HMCX_OK;
+}
+
 void begin_call(hmcx_ctx* ctx) {
   if (ctx->stage_pending) {
     (void)hipEventSynchronize(ctx->stage_ev);
@@ -250,7 +276,8 @@ int hmcx_create(int device, hmcx_ctx** out) {
   c->device = device;
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->stage_ev, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreate(&c->tev0) != hipSuccess || hipEventCreate(&c->tev1) != hipSuccess) {
     delete c;
     return HMCX_EHIP;
   }
@@ -272,6 +299,8 @@ int hmcx_destroy(hmcx_ctx* ctx) {
   if (ctx->stage) (void)hipHostFree(ctx->stage);
   if (ctx->stage_ev) (void)hipEventDestroy(ctx->stage_ev);
   if (ctx->ev_in) (void)hipEventDestroy(ctx->ev_in);
+  if (ctx->tev0) (void)hipEventDestroy(ctx->tev0);
+  if (ctx->tev1) (void)hipEventDestroy(ctx->tev1);
   for (auto& g : ctx->graveyard) {
     (void)hipGraphExecDestroy(g.first);
     (void)hipEventDestroy(g.second);
@@ -305,6 +334,26 @@ int hmcx_set_sghmc_path(hmcx_ctx* ctx, int path) {
 int hmcx_set_graph_mode(hmcx_ctx* ctx, int enabled) {
   HMCX_GUARD_CTX(ctx);
   ctx->graph_mode = enabled ? 1 : 0;
+  return HMCX_OK;
+}
+
+int hmcx_set_timing(hmcx_ctx* ctx, int enabled) {
+  HMCX_GUARD_CTX(ctx);
+  if (ctx->t_pending) (void)hipEventSynchronize(ctx->tev1);
+  ctx->timing = enabled ? 1 : 0;
+  ctx->t_pending = false;
+  ctx->t_ms = 0.0;
+  ctx->t_n = 0;
+  return HMCX_OK;
+}
+
+int hmcx_get_timing(hmcx_ctx* ctx, double* kernel_ms, long long* launches) {
+  HMCX_GUARD_CTX(ctx);
+  if (!kernel_ms || !launches) return set_error(ctx, HMCX_EINVAL, "hmcx_get_timing: null output");
+  int rc = timing_collect(ctx);
+  if (rc) return rc;
+  *kernel_ms = ctx->t_ms;
+  *launches = ctx->t_n;
   return HMCX_OK;
 }
 

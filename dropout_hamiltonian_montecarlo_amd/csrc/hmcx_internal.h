@@ -28,6 +28,12 @@ struct hmcx_ctx {
   // hipGraph mode: capture happens on own_stream (the legacy default stream cannot be captured)
   hipEvent_t ev_in = nullptr, ev_out = nullptr;
   std::vector<std::pair<hipGraphExec_t, hipEvent_t>> graveyard;   // executed graphs awaiting release
+  // device timing of sampler launches (hmcx_set_timing): events bracket the kernels of each run
+  int timing = 0;
+  hipEvent_t tev0 = nullptr, tev1 = nullptr;
+  bool t_pending = false;
+  double t_ms = 0.0;
+  long long t_n = 0;
 };
 
 namespace hmcx {
@@ -37,6 +43,12 @@ constexpr double CLIP_HI = 0x1.205966f2b4f12p+5;    //  36.04365338911715
 constexpr double CLIP_LO = -0x1.6232bdd7abcd2p+9;   // -708.3964185322641
 
 int set_error(hmcx_ctx* ctx, int code, const std::string& msg);
+
+// Kernel timing: timing_begin/timing_end record events on `st` around a run's kernels;
+// timing_collect folds a finished interval into (t_ms, t_n).  No-ops while timing is off.
+int timing_begin(hmcx_ctx* ctx, hipStream_t st);
+int timing_end(hmcx_ctx* ctx, hipStream_t st);
+int timing_collect(hmcx_ctx* ctx);
 
 #define HMCX_HIP(ctx, expr)                                                                  \
   do {                                                                                       \

@@ -679,12 +679,15 @@ int sghmc_persist_t(hmcx_ctx* ctx, const hmcx_sampler_args* s, const PersistPlan
   HMCX_HIP(ctx, hipFuncSetAttribute((const void*)k_sghmc_persist<T>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)pl.lds));
   void* kargs[] = {&a};
+  if ((rc = timing_begin(ctx, ctx->stream))) return rc;
   HMCX_HIP(ctx, hipLaunchCooperativeKernel((const void*)k_sghmc_persist<T>, dim3(G), dim3(PTH), kargs,
                                            (unsigned)pl.lds, ctx->stream));
+  if ((rc = timing_end(ctx, ctx->stream))) return rc;
   // the abort flag is checked synchronously: a timed-out barrier must not pass silently
   int flag = 0;
   HMCX_HIP(ctx, hipMemcpyAsync(&flag, a.abort_flag, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
   HMCX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if ((rc = timing_collect(ctx))) return rc;
   if (dprof) {
     unsigned long long h[16];
     HMCX_HIP(ctx, hipMemcpy(h, dprof, sizeof(h), hipMemcpyDeviceToHost));

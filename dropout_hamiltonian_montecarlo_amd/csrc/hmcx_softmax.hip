@@ -721,6 +721,7 @@ int sghmc_run_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
 
   const T* X = (const T*)s->X;
   const T* Y = (const T*)s->Y;
+  if ((rc = timing_begin(ctx, ctx->stream))) return rc;
   GraphScope gs(ctx);
   hipStream_t st = ctx->stream;
   for (int st_i = 0; st_i < s->n_steps; ++st_i) {
@@ -789,7 +790,8 @@ int sghmc_run_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
   hipLaunchKernelGGL(k_fix_acc, dim3((unsigned)((nsc + 255) / 256)), dim3(256), 0, st, d_niter, d_u,
                      s->out_accepted, (int)nsc);
   HMCX_HIP(ctx, hipGetLastError());
-  return gs.finish();
+  if ((rc = gs.finish())) return rc;
+  return timing_end(ctx, ctx->stream);
 }
 
 template <typename T>
@@ -815,6 +817,7 @@ int sgld_run_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
     return rc;
   const T* X = (const T*)s->X;
   const T* Y = (const T*)s->Y;
+  if ((rc = timing_begin(ctx, ctx->stream))) return rc;
   GraphScope gs(ctx);
   hipStream_t st = ctx->stream;
   for (int st_i = 0; st_i < s->n_steps; ++st_i) {
@@ -840,7 +843,8 @@ int sgld_run_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
       HMCX_HIP(ctx, hipGetLastError());
     }
   }
-  return gs.finish();
+  if ((rc = gs.finish())) return rc;
+  return timing_end(ctx, ctx->stream);
 }
 
 template int softmax_grad_t<float>(hmcx_ctx*, const void*, const void*, int, int, int, int, const void*,

@@ -52,6 +52,12 @@ int hmcx_set_graph_mode(hmcx_ctx* ctx, int enabled);
 /* SGHMC implementation: 0 = auto (persistent single-launch kernel when C == 1 and the shape
  * fits, else kernel-per-phase), 1 = kernel-per-phase, 2 = persistent only (error otherwise). */
 int hmcx_set_sghmc_path(hmcx_ctx* ctx, int path);
+/* Device timing of sampler runs: when enabled, HIP events on the launch stream bracket the
+ * kernels of every hmcx_sghmc_run / hmcx_sgld_run call (for the persistent SGHMC path: exactly
+ * its one kernel launch).  Enabling (or disabling) resets the totals; hmcx_get_timing waits
+ * for the last bracketed run and returns the summed kernel time and the number of runs. */
+int hmcx_set_timing(hmcx_ctx* ctx, int enabled);
+int hmcx_get_timing(hmcx_ctx* ctx, double* kernel_ms, long long* launches);
 
 /* Philox4x32-10 uniforms in [0,1), bit-identical to the device generator (host function). */
 void hmcx_philox_uniforms(uint64_t seed, uint32_t chain, uint32_t step, uint32_t slot,

@@ -73,7 +73,55 @@ __global__ __launch_bounds__(512) void k_ops(double* buf, unsigned* ctr, unsigne
   if (t == 0) { out[7] = t1 - t0; out[8] = rt1 - rt0; out[9] = (y == 0.0); }
 }
 
+typedef double d4v __attribute__((ext_vector_type(4)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void k_mfma64(double* out, int reps) {
+  d4v c0 = {0, 0, 0, 0}, c1 = c0, c2 = c0, c3 = c0;
+  double a = 1e-3 * threadIdx.x, b = 2e-3;
+  for (int r = 0; r < reps; ++r) {
+    c0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c1, 0, 0, 0);
+    c2 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c2, 0, 0, 0);
+    c3 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c3, 0, 0, 0);
+  }
+  out[blockIdx.x * 256 + threadIdx.x] = c0[0] + c1[1] + c2[2] + c3[3];
+}
+__global__ __launch_bounds__(256) void k_mfma32(double* out, int reps) {
+  f4v c0 = {0, 0, 0, 0}, c1 = c0, c2 = c0, c3 = c0;
+  float a = 1e-3f * threadIdx.x, b = 2e-3f;
+  for (int r = 0; r < reps; ++r) {
+    c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c1, 0, 0, 0);
+    c2 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c2, 0, 0, 0);
+    c3 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c3, 0, 0, 0);
+  }
+  out[blockIdx.x * 256 + threadIdx.x] = c0[0] + c1[1] + c2[2] + c3[3];
+}
+
 int main() {
+  {
+    double* o;
+    CK(hipMalloc(&o, 256 * 1024 * 8));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    const int reps = 20000, blocks = 1024;
+    for (int pass = 0; pass < 2; ++pass) {
+      float ms64 = 0, ms32 = 0;
+      CK(hipEventRecord(e0, 0));
+      hipLaunchKernelGGL(k_mfma64, dim3(blocks), dim3(256), 0, 0, o, reps);
+      CK(hipEventRecord(e1, 0));
+      CK(hipEventSynchronize(e1));
+      CK(hipEventElapsedTime(&ms64, e0, e1));
+      CK(hipEventRecord(e0, 0));
+      hipLaunchKernelGGL(k_mfma32, dim3(blocks), dim3(256), 0, 0, o, reps);
+      CK(hipEventRecord(e1, 0));
+      CK(hipEventSynchronize(e1));
+      CK(hipEventElapsedTime(&ms32, e0, e1));
+      const double flop = (double)blocks * 4 /*waves*/ * reps * 4 /*mfma*/ * 2048.0;
+      if (pass) printf("MFMA f64 16x16x4: %.1f TFLOP/s | f32 16x16x4: %.1f TFLOP/s\n", flop / ms64 / 1e9, flop / ms32 / 1e9);
+    }
+  }
   double* buf;
   unsigned* ctr;
   unsigned long long* out;
