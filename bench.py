@@ -38,8 +38,8 @@ MFMA_PEAK_TFLOPS = {"f64": 78.6, "f32": 157.3}   # dense MFMA, MI355X spec (f32:
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=240, help="timed SGHMC steps per chain")
-    ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--steps", type=int, default=600, help="timed SGHMC steps per chain")
+    ap.add_argument("--warmup", type=int, default=120)
     ap.add_argument("--dtype", choices=["f64", "f32"], default="f64")
     ap.add_argument("--path", choices=["auto", "kernels", "persistent"], default="auto")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline time budget (0 = skip)")

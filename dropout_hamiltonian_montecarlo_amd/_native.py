@@ -5,6 +5,7 @@ HIP device is visible, every entry point raises — there is no CPU fallback.
 torch is imported first so that the process has exactly one HIP runtime (torch's
 libamdhip64.so.7 satisfies libhmcx.so's NEEDED entry by soname).
 """
+import atexit
 import ctypes
 import os
 import threading
@@ -165,6 +166,18 @@ def context(device=None):
             _ctxs[idx] = ctx
     ctx.bind_stream()
     return ctx
+
+
+@atexit.register
+def _release_contexts():
+    """Destroy contexts while the HIP runtime (and any profiler tool) is still alive."""
+    with _lock:
+        ctxs = list(_ctxs.values())
+        _ctxs.clear()
+    for c in ctxs:
+        if getattr(c, "h", None) and c.h.value:
+            c.lib.hmcx_destroy(c.h)
+            c.h = c_void_p()
 
 
 def ptr(t):

@@ -1,0 +1,837 @@
+// hmcx_persist2.hip — single-chain SGHMC for the softmax model as ONE persistent launch per call,
+// built around tagged-granule hand-offs (no counters, no fences, no grid barrier per leapfrog).
+//
+// Mathematics and op order: cpu/sghmc.py:19-39 with the A1 completion, cpu/softmax.py:38-79, as in
+// the kernel-per-phase path (hmcx_softmax.hip).  Layout (BASELINE config 2: B=500, D=784, K=10):
+//
+//  * G = Gr x Gf workgroups (256 threads, one per CU, co-resident).  Workgroup (r, f) keeps the
+//    minibatch tile X[R_r, F_f] in LDS for a whole step (rows R_r = Br rows, features F_f = Bf).
+//  * Inside the row team r, workgroup f OWNS the row slice rho(r,f) (Ro rows); inside the feature
+//    team f, workgroup r OWNS the feature slice phi(r,f) (Fo features x K weights and momenta).
+//  * One leapfrog iteration = four team-local hand-off rounds, each a reduce-scatter or an
+//    all-gather of a few KB:
+//      A-RS  partial logits X[R_r,F_f]·W[F_f]          → owner of rho sums the Gf partials,
+//            runs both softmaxes of its rows (at b and at b' = b + ε·pb), builds diff rows;
+//      A-AG  diff rows + colsum/ll partials            → every member has diff[R_r];
+//      B-RS  partial gradient X[R_r,F_f]ᵀ·diff         → owner of phi sums the Gr partials and
+//            updates its weights/momenta (friction noise from Philox); the bias sub-step is
+//            replicated from the all-row colsum that travels with the partials;
+//      B-AG  drifted weights of phi                    → every member has W[F_f] for the next X·W.
+//    Per step one more all-gather (kinetic and log-likelihood partials) decides the MH accept in
+//    every workgroup identically.
+//  * The two GEMMs run on MFMA (v_mfma_f64_16x16x4 / f32_16x16x4) with operands from the LDS tile;
+//    the class dimension (KC = 10 compiled in, 16 generic) pads to the 16-wide tile.  A VALU
+//    variant with the classes in registers measured 1.7x slower (LDS-latency bound).
+//  * Transport: every value travels as one 16-byte granule {lo32, epoch, hi32, epoch} written by
+//    ONE `buffer_store_dwordx4 … sc1` and read by `buffer_load_dwordx4 … sc1`; a consumer re-reads
+//    a granule until both epoch words match (cdna_hip_programming.md §6 G16, recipe R2: the data
+//    is the flag).  Epochs count rounds within the call; the arena is zeroed before each launch.
+//    Measured on MI355X (tools/microbench_handoff.hip): one team round of 8 x 80-130 granules
+//    ≈ 1.4-1.6 µs, against 3-3.4 µs for payload + counter barrier.
+// All reductions run in a fixed order, so the replicated state is bit-identical in every
+// workgroup and runs are deterministic.
+#include "hmcx_common.h"
+#include "hmcx_internal.h"
+#include "hmcx_persist.h"
+#include <cstdio>
+#include <cstdlib>
+
+namespace hmcx {
+
+constexpr int QTH = 256;                 // threads per workgroup (4 waves)
+constexpr int QNW = QTH / 64;
+constexpr int QNPM = 16;                 // largest team (producers per gather)
+constexpr unsigned long long QTIMEOUT = 400000000ull;   // s_memrealtime ticks (100 MHz): 4 s
+
+typedef unsigned int gran_t __attribute__((ext_vector_type(4)));
+
+struct Q2Args {
+  int B, D, K, P, n_steps;
+  int Gr, Gf, Br, Bf, BfP, BFP, Ro, Fo;
+  double alpha, neg_inv_n, log_prior;
+  const void* X; const void* Y;
+  const double* eps; const double* u; const int64_t* row0; const int32_t* n_iter;
+  int noise_mode; const double* noise; const int64_t* noff;
+  uint64_t seed; uint32_t chain0, step_base;
+  void* W; void* b;
+  char* arena;                              // granule arena (zeroed per call)
+  int oXA, oXD, oXB, oXW, oXS;              // region offsets in granules
+  int arena_bytes;
+  int* abort_flag;                          // inside the arena
+  double* out_A; int32_t* out_acc; double* out_ll; double* out_E;
+  unsigned long long* prof;                 // HMCX_PERSIST_PROF=1: per-segment s_memtime totals (workgroup 0)
+};
+
+// Segment profiler (workgroup 0, thread 0): s_memtime deltas accumulate in LDS (a global
+// read-modify-write per stamp would add a memory round trip to the critical path); flushed once.
+struct P2Prof {
+  unsigned long long* out;
+  unsigned long long* acc;   // LDS [16]
+  unsigned long long last;
+  int cur;
+  __device__ inline void stamp(int next) {
+    if (!out) return;
+    const unsigned long long t = __builtin_amdgcn_s_memtime();
+    if (last) acc[cur] += t - last;
+    last = t;
+    cur = next;
+  }
+  __device__ inline void flush() {
+    if (!out) return;
+    for (int i = 0; i < 16; ++i) out[i] = acc[i];
+  }
+};
+
+// ---------------------------------------------------------------- granule transport
+__device__ inline __amdgpu_buffer_rsrc_t arena_rsrc(char* base, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(base, 0, bytes, 0x00020000);
+}
+__device__ inline void put(__amdgpu_buffer_rsrc_t rs, int g, double v, unsigned ep) {
+  const unsigned long long x = __builtin_bit_cast(unsigned long long, v);
+  gran_t w = {(unsigned)x, ep, (unsigned)(x >> 32), ep};
+  __builtin_amdgcn_raw_buffer_store_b128(w, rs, g * 16, 0, 16 /* sc1 */);
+}
+__device__ inline double decode(gran_t w) {
+  return __builtin_bit_cast(double, (unsigned long long)w.x | ((unsigned long long)w.z << 32));
+}
+
+// Polls one granule per producer p < np (p != pskip) at base0 + p·pstride + off until both epoch
+// words match.  Loads go out unpredicated in one batch of 8·NB (absent producers clamped to a
+// valid address and ignored); a pass re-reads the batch while any granule is missing.
+// SUM: *sum = v_0 + v_1 + … in producer order; else v_p → dst[p·dstride].  false on timeout/abort.
+template <int NB, bool SUM, typename V>
+__device__ inline bool poll_nb(__amdgpu_buffer_rsrc_t rs, int base0, int pstride, int np, int pskip, int off,
+                               bool valid, unsigned ep, double* sum, int* abort_flag, V* dst, int dstride) {
+  constexpr int N = 8 * NB;
+  unsigned pend = 0;
+  int o[N];
+#pragma unroll
+  for (int u = 0; u < N; ++u) {
+    const bool want = valid && u < np && u != pskip;
+    pend |= want ? 1u << u : 0u;
+    o[u] = (base0 + (want ? u * pstride + off : 0)) * 16;
+  }
+  double val[N];
+#pragma unroll
+  for (int u = 0; u < N; ++u) val[u] = 0.0;
+  unsigned long long t0 = 0;
+  for (int spins = 0; pend; ++spins) {
+    gran_t v[N];
+#pragma unroll
+    for (int u = 0; u < N; ++u) v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, o[u], 0, 16 /* sc1 */);
+#pragma unroll
+    for (int u = 0; u < N; ++u)
+      if (((pend >> u) & 1u) && v[u].y == ep && v[u].w == ep) {
+        val[u] = decode(v[u]);
+        pend &= ~(1u << u);
+      }
+    if (!pend) break;
+    if (spins == 0) t0 = __builtin_amdgcn_s_memrealtime();
+    if ((spins & 63) == 63 &&
+        (__builtin_amdgcn_s_memrealtime() - t0 > QTIMEOUT ||
+         __hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+      __hip_atomic_store(abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  if (!valid) return true;
+  if (SUM) {
+    double acc = val[0];
+#pragma unroll
+    for (int u = 1; u < N; ++u)
+      if (u < np && u != pskip) acc += val[u];
+    *sum = acc;
+  } else {
+#pragma unroll
+    for (int u = 0; u < N; ++u)
+      if (u < np && u != pskip) dst[u * dstride] = (V)val[u];
+  }
+  return true;
+}
+template <bool SUM, typename V = double>
+__device__ inline bool poll(__amdgpu_buffer_rsrc_t rs, int base0, int pstride, int np, int pskip, int off, bool valid,
+                            unsigned ep, double* /*unused*/, int /*unused*/, double* sum, int* abort_flag,
+                            V* dst = nullptr, int dstride = 0) {
+  return np <= 8 ? poll_nb<1, SUM, V>(rs, base0, pstride, np, pskip, off, valid, ep, sum, abort_flag, dst, dstride)
+                 : poll_nb<2, SUM, V>(rs, base0, pstride, np, pskip, off, valid, ep, sum, abort_flag, dst, dstride);
+}
+
+// Workgroup-uniform verdict after a gather (also the barrier that publishes dst).
+__device__ inline bool all_ok(bool ok, int* sh_fail) {
+  if (!ok) *sh_fail = 1;
+  __syncthreads();
+  return *sh_fail == 0;
+}
+
+// Deterministic workgroup sum (fixed butterfly + fixed wave order).
+__device__ inline double wsum(double v, double* sh) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  double r = sh[0];
+#pragma unroll
+  for (int w = 1; w < QNW; ++w) r += sh[w];
+  __syncthreads();
+  return r;
+}
+
+// All-reduce over a 16-lane row with DPP (xor 1, xor 2, half-row mirror, row mirror): every lane
+// of the row ends with the same bits (each step combines a symmetric pair).
+template <int CTRL> __device__ inline double dpp64(double v) {
+  const unsigned long long x = __builtin_bit_cast(unsigned long long, v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)(unsigned)x, CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(unsigned)(x >> 32), CTRL, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, (unsigned long long)(unsigned)lo | ((unsigned long long)(unsigned)hi << 32));
+}
+template <int CTRL> __device__ inline float dpp64(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+constexpr int DPP_XOR1 = 0xB1, DPP_XOR2 = 0x4E, DPP_HMIRROR = 0x141, DPP_MIRROR = 0x140;
+template <typename T> __device__ inline T g16_max2(T v) {
+  v = max_nan(v, dpp64<DPP_XOR1>(v));
+  v = max_nan(v, dpp64<DPP_XOR2>(v));
+  v = max_nan(v, dpp64<DPP_HMIRROR>(v));
+  v = max_nan(v, dpp64<DPP_MIRROR>(v));
+  return v;
+}
+template <typename T> __device__ inline T g16_sum2(T v) {
+  v = v + dpp64<DPP_XOR1>(v);
+  v = v + dpp64<DPP_XOR2>(v);
+  v = v + dpp64<DPP_HMIRROR>(v);
+  v = v + dpp64<DPP_MIRROR>(v);
+  return v;
+}
+
+// Integer quotient e / d for small non-negative e (e·d < 2^22) via a float reciprocal.
+__device__ inline int qdiv(int e, float inv) { return (int)(((float)e + 0.5f) * inv); }
+
+// Noise value of flat element e for slot `slot` of step s: Philox block z4 (already generated for
+// block e >> 2) or the host-drawn buffer (cpu/sghmc.py:21,31 draw order).
+template <typename T>
+__device__ inline T noise_at(const Q2Args& a, int s, uint32_t slot, uint32_t e, const float* z4) {
+  if (a.noise_mode == HMCX_NOISE_BUFFER) return (T)a.noise[a.noff[s] + (int64_t)slot * a.P + e];
+  return (T)z4[e & 3];
+}
+__device__ inline void philox4_if(const Q2Args& a, int s, uint32_t slot, uint32_t g, float z[4]) {
+  if (a.noise_mode != HMCX_NOISE_BUFFER) philox_normal4(a.seed, a.chain0, a.step_base + (uint32_t)s, slot, g, z);
+}
+
+// Minibatch tile X[row0:+nrow, feat0:+nfeat] → LDS [Br][BFP], zero padded to BfP columns;
+// 16-byte loads, 8 in flight per thread when rows are 16-byte aligned.
+template <typename T>
+__device__ inline void load_tile(T* Xs, const T* Xg, int Br, int BfP, int BFP, int nrow, int nfeat, int row0,
+                                 int feat0, int D) {
+  constexpr int V = 16 / sizeof(T);
+  typedef T vec_t __attribute__((ext_vector_type(V)));
+  const int PR = BfP / V;                        // vectors per tile row
+  const float inv = 1.0f / (float)PR;
+  const int total = Br * PR;
+  const bool vec_ok = (D % V) == 0 && (feat0 % V) == 0 &&
+                      ((reinterpret_cast<uintptr_t>(Xg) & 15) == 0);
+  for (int base = threadIdx.x; base < total; base += 8 * QTH) {
+    vec_t v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = base + u * QTH;
+      const int i = qdiv(e, inv), j = (e - i * PR) * V;
+      const T* src = Xg + (size_t)(row0 + i) * D + feat0 + j;
+      if (e < total && i < nrow && j + V <= nfeat && vec_ok) {
+        v[u] = *reinterpret_cast<const vec_t*>(src);
+      } else {
+#pragma unroll
+        for (int q = 0; q < V; ++q) v[u][q] = (e < total && i < nrow && j + q < nfeat) ? src[q] : T(0);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = base + u * QTH;
+      if (e < total) {
+        const int i = qdiv(e, inv), j = (e - i * PR) * V;
+#pragma unroll
+        for (int q = 0; q < V; ++q) Xs[i * BFP + j + q] = v[u][q];
+      }
+    }
+  }
+}
+
+// C[16 x 16] += A[16 x 4·nk] · B[4·nk x 16] on one wave (v_mfma_*_16x16x4): A(i, kk) = a[i·as_i +
+// kk·as_k], B(kk, j) = b[kk·bs_k + j]; operands of 8 k-steps are loaded before their MFMAs, two
+// accumulators alternate.  Returns the D fragment (rows M::row(lane, q), column lane & 15).
+template <typename T>
+__device__ inline typename mfma16<T>::acc_t mfma_tile(const T* a, int as_i, int as_k, const T* b, int bs_k, int nk) {
+  using M = mfma16<T>;
+  const int lane = threadIdx.x & 63, lr = lane & 15, lg = lane >> 4;
+  const T* pa = a + lr * as_i + lg * as_k;
+  const T* pb = b + lg * bs_k + lr;
+  typename M::acc_t c0 = M::zero(), c1 = M::zero();
+  int kk = 0;
+  for (; kk + 8 <= nk; kk += 8) {
+    T av[8], bv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      av[u] = pa[(kk + u) * 4 * as_k];
+      bv[u] = pb[(kk + u) * 4 * bs_k];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u += 2) {
+      c0 = M::fma(av[u], bv[u], c0);
+      c1 = M::fma(av[u + 1], bv[u + 1], c1);
+    }
+  }
+  for (; kk < nk; ++kk) c0 = M::fma(pa[kk * 4 * as_k], pb[kk * 4 * bs_k], c0);
+  return c0 + c1;
+}
+
+template <typename T, int KC>
+__global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
+  using M = mfma16<T>;
+  extern __shared__ __align__(16) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15;
+  const int Gr = a.Gr, Gf = a.Gf, G = Gr * Gf;
+  const int bid = blockIdx.x;
+  const int r = bid / Gf, f = bid - (bid / Gf) * Gf;
+  const int Br = a.Br, Bf = a.Bf, BfP = a.BfP, BFP = a.BFP, Ro = a.Ro, Fo = a.Fo;
+  const int K = a.K, D = a.D, B = a.B;
+  const int row0 = r * Br, feat0 = f * Bf;
+  const int nrow = max(0, min(Br, B - row0));
+  const int nfeat = max(0, min(Bf, D - feat0));
+  const int ro0 = f * Ro, nro = max(0, min(Ro, nrow - ro0));            // my softmax rows
+  const int fo0 = r * Fo, nfo = max(0, min(Fo, nfeat - fo0));           // my owned features
+  const T hi = (T)CLIP_HI, lo = (T)CLIP_LO;
+  const T alpha = (T)a.alpha;
+  const __amdgpu_buffer_rsrc_t rs = arena_rsrc(a.arena, a.arena_bytes);
+  // MFMA work split: phase A m-tiles = Br/16 rows (k over BfP features), phase B m-tiles = BfP/16
+  // features (k over Br rows); split-K parts when the tiles are fewer than the waves
+  const int MTA = Br / 16, WPA = max(1, QNW / MTA);
+  const int MTB = BfP / 16, WPB = max(1, QNW / MTB);
+  const int HA = KC + 1;                              // payload header: colsum[KC], ll
+  const int NXA = HA + Ro * KC;                       // A-AG payload per producer
+  const int NXB = HA + Bf * KC;                       // B-RS payload per producer
+
+  // ---- LDS carve-up (mirrored by p2_lds)
+  T* Xs = reinterpret_cast<T*>(smem);                 // [Br][BFP]
+  T* Wf = Xs + (size_t)Br * BFP;                      // [BfP][16] weights of F_f
+  T* Wf0 = Wf + BfP * 16;                             // [BfP][16] step-start copy
+  T* Ds = Wf0 + BfP * 16;                             // [Gf·Ro][16] diff of the row tile
+  T* Zp = Ds + Gf * Ro * 16;                          // split-K partials: [WPA][Br][16] | [WPB][BfP][16]
+  const int ZPN = max(WPA * Br, WPB * BfP) * 16;
+  T* Zo = Zp + ZPN;                                   // [Ro][16] logits of my rows
+  T* Yo = Zo + Ro * 16;                               // [Ro][16] labels of my rows
+  T* Dme = Yo + Ro * 16;                              // [Ro][16] diff of my rows
+  T* Csr = Dme + Ro * 16;                             // [Ro][16] y − ŷ' of my rows
+  T* bsh = Csr + Ro * 16;                             // [16] b
+  T* pbsh = bsh + 16;                                 // [16] pb
+  T* b0sh = pbsh + 16;                                // [16] b at step start
+  T* bpsh = b0sh + 16;                                // [16] b'
+  size_t off = ((size_t)(reinterpret_cast<char*>(bpsh + 16) - smem) + 15) & ~(size_t)15;
+  double* rowll = reinterpret_cast<double*>(smem + off);  // [Ro] ll of my rows
+  double* hdr = rowll + Ro;                               // [16] all-row colsum, ll
+  double* dsh = hdr + 16;                                 // [16] reductions
+  int* ish = reinterpret_cast<int*>(dsh + 16);            // [4] flags
+  unsigned long long* profacc = reinterpret_cast<unsigned long long*>(ish + 4);   // [16]
+
+  // owned weight of this thread: feature fo0 + od, class ok (thread t = od·KC + ok)
+  const int od = tid / KC, okc = tid - (tid / KC) * KC;
+  const bool own = od < nfo && okc < K;
+  const int e_own = (feat0 + fo0 + od) * K + okc;     // flat index (W is [D][K])
+  const int wl = (fo0 + od) * 16 + okc;               // index in Wf
+  T pw = T(0), wv = T(0), w0 = T(0), zn = T(0);
+
+  if (tid == 0) ish[0] = 0;
+  if (tid < 16) profacc[tid] = 0ull;
+  for (int e = tid; e < BfP * 16; e += QTH) {
+    const int i = e >> 4, k = e & 15;
+    Wf[e] = (i < nfeat && k < K) ? reinterpret_cast<const T*>(a.W)[(size_t)(feat0 + i) * K + k] : T(0);
+  }
+  for (int e = tid; e < Gf * Ro * 16; e += QTH) Ds[e] = T(0);
+  for (int e = tid; e < Ro * 16; e += QTH) { Dme[e] = T(0); Csr[e] = T(0); }
+  if (tid < 16) bsh[tid] = tid < K ? reinterpret_cast<const T*>(a.b)[tid] : T(0);
+  __syncthreads();
+  if (own) wv = Wf[wl];
+
+  P2Prof prof{(bid == 0 && tid == 0) ? a.prof : nullptr, profacc, 0ull, 0};
+  unsigned ep = 0;                                    // round epoch (same sequence in every workgroup)
+  unsigned uA = 0, uD = 0, uB = 0, uW = 0, uS = 0;    // per-region use counters (buffer parity)
+
+  // ---- phase A: partial logits X[R_r,F_f]·W[F_f] → XA(par, r, f) [nrow][KC], then A-RS consume:
+  //      Zo[ii][k] = Σ_f' partials of my rows (f' order)
+  auto roundA = [&]() -> bool {
+    ++ep;
+    const int reg = a.oXA + (((int)(uA & 1) * Gr + r) * Gf + f) * Br * KC;
+    const int nkp = (BfP / 4) / WPA;
+    for (int item = wave; item < MTA * WPA; item += QNW) {
+      const int mt = item % MTA, part = item / MTA;
+      const typename M::acc_t c = mfma_tile<T>(Xs + mt * 16 * BFP + part * nkp * 4, BFP, 1,
+                                               Wf + part * nkp * 4 * 16, 16, nkp);
+      if (WPA == 1) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int row = mt * 16 + M::row(lane, q);
+          if (row < nrow && lr < KC) put(rs, reg + row * KC + lr, (double)c[q], ep);
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) Zp[(part * Br + mt * 16 + M::row(lane, q)) * 16 + lr] = c[q];
+      }
+    }
+    if (WPA > 1) {
+      __syncthreads();
+      for (int e = tid; e < nrow * KC; e += QTH) {
+        const int i = e / KC, k = e - (e / KC) * KC;
+        T v = Zp[i * 16 + k];
+        for (int p = 1; p < WPA; ++p) v += Zp[(p * Br + i) * 16 + k];
+        put(rs, reg + e, (double)v, ep);
+      }
+    }
+    return true;
+  };
+  auto consumeA = [&]() -> bool {
+    const int base0 = a.oXA + ((int)(uA & 1) * Gr + r) * Gf * Br * KC;
+    ++uA;
+    double z = 0.0;
+    const bool ok = poll<true>(rs, base0, Br * KC, Gf, -1, ro0 * KC + tid, tid < nro * KC, ep, nullptr, 0, &z,
+                               a.abort_flag);
+    if (tid < nro * KC) Zo[(tid / KC) * 16 + (tid % KC)] = (T)z;
+    return all_ok(ok, ish);
+  };
+
+  for (int s = 0; s < a.n_steps; ++s) {
+    const double epsd = a.eps[s];
+    const T eps = (T)epsd, ome = (T)(1.0 - epsd), nsc = (T)(2.0 * epsd);
+    const int n = a.n_iter[s];
+    const T* Xg = reinterpret_cast<const T*>(a.X) + (size_t)a.row0[s] * D;
+    const T* Yg = reinterpret_cast<const T*>(a.Y) + (size_t)a.row0[s] * K;
+    prof.stamp(0);
+
+    // ---- step start: tile, labels of my rows, momentum (hmc.py:82-87), step-start copies
+    load_tile<T>(Xs, Xg, Br, BfP, BFP, nrow, nfeat, row0, feat0, D);
+    for (int e = tid; e < Ro * 16; e += QTH) {
+      const int ii = e >> 4, k = e & 15;
+      Yo[e] = (ii < nro && k < K) ? Yg[(size_t)(row0 + ro0 + ii) * K + k] : T(0);
+    }
+    for (int e = tid; e < BfP * 16; e += QTH) Wf0[e] = Wf[e];
+    {
+      float z4[4];
+      if (own) philox4_if(a, s, 0u, (uint32_t)(e_own >> 2), z4);
+      pw = own ? noise_at<T>(a, s, 0u, (uint32_t)e_own, z4) : T(0);
+      w0 = wv;
+    }
+    if (tid < 16) {
+      float z4[4];
+      const uint32_t e = (uint32_t)(D * K + tid);
+      if (tid < K) philox4_if(a, s, 0u, e >> 2, z4);
+      pbsh[tid] = tid < K ? noise_at<T>(a, s, 0u, e, z4) : T(0);
+      b0sh[tid] = bsh[tid];
+    }
+    const double kin0 = wsum((double)pw * (double)pw, dsh);
+    double kb0 = 0.0;
+    for (int k = 0; k < K; ++k) kb0 += (double)pbsh[k] * (double)pbsh[k];
+
+    // ---- it = -1: log-likelihood of my rows at the step-start state (E_current)
+    double ll0 = 0.0, ll_last = 0.0;
+    prof.stamp(11);
+    roundA();
+    if (!consumeA()) return;
+    {
+      const int k = lane & 15, grp = tid >> 4;
+      const bool kv = k < K;
+      for (int ii = grp; ii < nro; ii += QTH / 16) {
+        const T z = kv ? clipz(Zo[ii * 16 + k] + b0sh[k], hi, lo) : (T)-__builtin_inf();
+        const T m = g16_max2(z);
+        const T e = kv ? exp(z - m) : T(0);
+        const T sm = g16_sum2(e);
+        const T lse = log(sm) + m;                                          // softmax.py:18
+        const double t = kv ? (double)(Yo[ii * 16 + k] * (z - lse)) : 0.0;  // softmax.py:19-20
+        const double rsum = g16_sum2(t);
+        if (k == 0) rowll[ii] = rsum;
+      }
+      __syncthreads();
+      if (tid == 0) {
+        double v = 0.0;
+        for (int ii = 0; ii < nro; ++ii) v += rowll[ii];
+        dsh[4] = v;
+      }
+      __syncthreads();
+      ll0 = dsh[4];
+    }
+
+    double kin1 = 0.0;
+    for (int it = 0; it < n; ++it) {
+      const bool last = it == n - 1;
+      if (it == 0) {
+        // drift of the whole F_f slice by p0 (every member computes it identically; sghmc.py:32)
+        const int ge0 = (feat0 * K) >> 2, ge1 = ((feat0 + nfeat) * K + 3) >> 2;
+        for (int g = ge0 + tid; g < ge1; g += QTH) {
+          float z4[4];
+          philox4_if(a, s, 0u, (uint32_t)g, z4);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int e = 4 * g + q;
+            if (e < feat0 * K || e >= (feat0 + nfeat) * K) continue;
+            const int i = e / K - feat0, k = e - (e / K) * K;
+            Wf[i * 16 + k] = Wf[i * 16 + k] + eps * noise_at<T>(a, s, 0u, (uint32_t)e, z4);
+          }
+        }
+        if (own) wv = wv + eps * pw;
+        __syncthreads();
+      }
+      if (tid < 16) bpsh[tid] = bsh[tid] + eps * pbsh[tid];                // b' (bias sub-step)
+
+      // ===== A-RS: partial logits → owners of the row slices
+      prof.stamp(1);
+      roundA();
+      prof.stamp(2);
+      // friction noise of this iteration (sghmc.py:31), generated while the partials travel
+      T zb = T(0);
+      {
+        float z4[4];
+        if (own) philox4_if(a, s, (uint32_t)(it + 1), (uint32_t)(e_own >> 2), z4);
+        zn = own ? noise_at<T>(a, s, (uint32_t)(it + 1), (uint32_t)e_own, z4) : T(0);
+        if (tid < K) {
+          const uint32_t e = (uint32_t)(D * K + tid);
+          philox4_if(a, s, (uint32_t)(it + 1), e >> 2, z4);
+          zb = noise_at<T>(a, s, (uint32_t)(it + 1), e, z4);
+        }
+      }
+      prof.stamp(3);
+      if (!consumeA()) return;
+      prof.stamp(4);
+
+      // ===== softmaxes of my rows: diff at b (weights sub-step), y − ŷ' at b' (bias sub-step)
+      {
+        const int k = lane & 15, grp = tid >> 4;
+        const bool kv = k < K;
+        for (int item = grp; item < 2 * nro; item += QTH / 16) {
+          const bool v1 = item >= nro;
+          const int ii = v1 ? item - nro : item;
+          const T bias = kv ? (v1 ? bpsh[k] : bsh[k]) : T(0);
+          const T y = Yo[ii * 16 + k];
+          const T z = kv ? clipz(Zo[ii * 16 + k] + bias, hi, lo) : (T)-__builtin_inf();   // softmax.py:39-41
+          const T m = g16_max2(z);
+          const T e = kv ? exp(z - m) : T(0);                                                // softmax.py:34
+          const T sm = g16_sum2(e);
+          const T dd = kv ? y - e / sm : T(0);                                                // softmax.py:52
+          if (!v1) {
+            Dme[ii * 16 + k] = dd;
+          } else {
+            Csr[ii * 16 + k] = dd;
+            if (last) {
+              const T lse = log(sm) + m;
+              const double t = kv ? (double)(y * (z - lse)) : 0.0;
+              const double rsum = g16_sum2(t);
+              if (k == 0) rowll[ii] = rsum;
+            }
+          }
+        }
+        __syncthreads();
+      }
+      // ===== A-AG: [colsum part (KC), ll part, diff rows (Ro·KC)] → every row-team member
+      prof.stamp(5);
+      double hv = 0.0;                                  // t < KC: team colsum; t == KC: team ll
+      {
+        ++ep;
+        const int reg = a.oXD + (((int)(uD & 1) * Gr + r) * Gf + f) * NXA;
+        if (tid < NXA) {
+          double v;
+          if (tid < KC) {
+            T c = T(0);
+            for (int ii = 0; ii < nro; ++ii) c += Csr[ii * 16 + tid];
+            v = (double)c;
+          } else if (tid == KC) {
+            v = 0.0;
+            if (last) for (int ii = 0; ii < nro; ++ii) v += rowll[ii];
+          } else {
+            const int m = tid - HA;
+            v = (double)Dme[(m / KC) * 16 + (m % KC)];
+          }
+          put(rs, reg + tid, v, ep);
+        }
+        const int base0 = a.oXD + ((int)(uD & 1) * Gr + r) * Gf * NXA;
+        ++uD;
+        bool ok;
+        if (tid < HA) {
+          ok = poll<true>(rs, base0, NXA, Gf, -1, tid, true, ep, nullptr, 0, &hv, a.abort_flag);
+        } else {
+          const int m = tid - HA;
+          ok = poll<false>(rs, base0, NXA, Gf, -1, tid, tid < NXA, ep, nullptr, 0, nullptr, a.abort_flag,
+                           Ds + (m / KC) * 16 + (m % KC), Ro * 16);
+        }
+        if (!all_ok(ok, ish)) return;
+      }
+
+      // ===== B-RS: partial gradient X[R_r,F_f]ᵀ·diff → owners of the feature slices
+      prof.stamp(6);
+      {
+        ++ep;
+        const int reg = a.oXB + (((int)(uB & 1) * Gf + f) * Gr + r) * NXB;
+        if (tid < HA) put(rs, reg + tid, hv, ep);
+        const int nkp = (Br / 4) / WPB;
+        for (int item = wave; item < MTB * WPB; item += QNW) {
+          const int mt = item % MTB, part = item / MTB;
+          const typename M::acc_t c = mfma_tile<T>(Xs + part * nkp * 4 * BFP + mt * 16, 1, BFP,
+                                                   Ds + part * nkp * 4 * 16, 16, nkp);
+          if (WPB == 1) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const int d = mt * 16 + M::row(lane, q);
+              if (d < nfeat && lr < KC) put(rs, reg + HA + d * KC + lr, (double)c[q], ep);
+            }
+          } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) Zp[(part * BfP + mt * 16 + M::row(lane, q)) * 16 + lr] = c[q];
+          }
+        }
+        if (WPB > 1) {
+          __syncthreads();
+          for (int e = tid; e < nfeat * KC; e += QTH) {
+            const int i = e / KC, k = e - (e / KC) * KC;
+            T v = Zp[i * 16 + k];
+            for (int q = 1; q < WPB; ++q) v += Zp[(q * BfP + i) * 16 + k];
+            put(rs, reg + HA + e, (double)v, ep);
+          }
+        }
+        const int base0 = a.oXB + ((int)(uB & 1) * Gf + f) * Gr * NXB;
+        ++uB;
+        prof.stamp(7);
+        // threads [0, nfo·KC): owned gradient element; threads [nfo·KC, nfo·KC + HA): header
+        const int ng = nfo * KC;
+        double sum = 0.0;
+        const bool isg = tid < ng, ish_ = tid >= ng && tid < ng + HA;
+        const int offB = isg ? HA + fo0 * KC + tid : tid - ng;
+        const bool ok = poll<true>(rs, base0, NXB, Gr, -1, offB, isg || ish_, ep, nullptr, 0, &sum, a.abort_flag);
+        if (ish_) hdr[tid - ng] = sum;
+        if (!all_ok(ok, ish)) return;
+        prof.stamp(8);
+        // owned weight: gradient (softmax.py:57-58), momentum (sghmc.py:31,34), drift (:32)
+        if (own) {
+          const T gr = -((T)sum - alpha * wv);
+          const T p = (ome * pw + eps * gr) + nsc * zn;
+          pw = p;
+          if (!last) wv = wv + eps * p;
+          else kin1 = (double)p * (double)p;
+        }
+        if (tid < K) {                                                      // bias sub-step, replicated
+          const T gr = -((T)hdr[tid] - alpha * bpsh[tid]);
+          pbsh[tid] = (ome * pbsh[tid] + eps * gr) + nsc * zb;
+          bsh[tid] = bpsh[tid];
+        }
+        if (last) ll_last = hdr[KC];                                        // ll(q_new) on this batch
+      }
+      if (last) break;
+      // ===== B-AG: drifted owned weights → every member of the feature team
+      prof.stamp(9);
+      {
+        ++ep;
+        const int per = Fo * KC;
+        const int reg = a.oXW + (((int)(uW & 1) * Gf + f) * Gr + r) * per;
+        if (tid < nfo * KC) put(rs, reg + tid, own ? (double)wv : 0.0, ep);
+        if (own) Wf[wl] = wv;
+        const int base0 = a.oXW + ((int)(uW & 1) * Gf + f) * Gr * per;
+        ++uW;
+        const int dloc = tid / KC, kk = tid - (tid / KC) * KC;
+        const int npd = tid < per ? min(Gr, (nfeat - dloc + Fo - 1) / Fo) : 0;   // producers owning feature dloc
+        const bool ok = poll<false>(rs, base0, per, npd, r, tid, tid < per, ep, nullptr, 0, nullptr, a.abort_flag,
+                                    Wf + dloc * 16 + kk, Fo * 16);
+        if (!all_ok(ok, ish)) return;
+      }
+    }
+
+    // ===== accept (hmc.py:67-71): all-gather of the kinetic / log-likelihood partials
+    prof.stamp(10);
+    const double kin1w = wsum(kin1, dsh);
+    double kb1 = 0.0;
+    for (int k = 0; k < K; ++k) kb1 += (double)pbsh[k] * (double)pbsh[k];
+    ++ep;
+    {
+      const int reg = a.oXS + ((int)(uS & 1) * G + bid) * 4;
+      if (tid == 0) put(rs, reg + 0, kin0, ep);
+      if (tid == 1) put(rs, reg + 1, kin1w, ep);
+      if (tid == 2) put(rs, reg + 2, ll0, ep);
+    }
+    const int sbase = a.oXS + (int)(uS & 1) * G * 4;
+    ++uS;
+    double v3[3] = {0.0, 0.0, 0.0};
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      ok = ok && poll<true>(rs, sbase + j, 4, 1, -1, tid * 4, tid < G, ep, nullptr, 0, &v3[j], a.abort_flag);
+    if (!all_ok(ok, ish)) return;
+    const double S0 = wsum(v3[0], dsh), S1 = wsum(v3[1], dsh), L0 = wsum(v3[2], dsh);
+    const double K0 = (0.0 + 0.5 * S0) + 0.5 * kb0;
+    const double Ecur = a.neg_inv_n * (L0 + a.log_prior) + K0;
+    double A, Enew, llq;
+    int acc;
+    if (n <= 0) {
+      A = 1.0; Enew = Ecur; llq = L0;
+      acc = a.u[s] < A;
+    } else {
+      const double K1 = (0.0 + 0.5 * S1) + 0.5 * kb1;
+      Enew = a.neg_inv_n * (ll_last + a.log_prior) + K1;
+      const double x = exp(Ecur - Enew);
+      A = (x < 1.0) ? x : 1.0;                                             // Python min(1, x)
+      acc = a.u[s] < A;
+      llq = acc ? ll_last : L0;
+    }
+    if (!acc || n <= 0) {                                                  // keep q (sghmc.py:36-38)
+      for (int e = tid; e < BfP * 16; e += QTH) Wf[e] = Wf0[e];
+      wv = w0;
+      if (tid < 16) bsh[tid] = b0sh[tid];
+    }
+    if (bid == 0 && tid == 0) {
+      a.out_A[s] = A;
+      a.out_acc[s] = acc;
+      a.out_ll[s] = llq;
+      if (a.out_E) { a.out_E[2 * s] = Ecur; a.out_E[2 * s + 1] = Enew; }
+    }
+    __syncthreads();
+  }
+  prof.stamp(0);
+  prof.flush();
+  // ---- committed state: owners write their weights, workgroup 0 the bias
+  if (own) reinterpret_cast<T*>(a.W)[e_own] = wv;
+  if (bid == 0 && tid < K) reinterpret_cast<T*>(a.b)[tid] = bsh[tid];
+}
+
+// ---------------------------------------------------------------- plan + launch
+static int kc_of(int K) { return K == 10 ? 10 : 16; }
+
+static size_t p2_lds(const PersistPlan2& p, int K, size_t ts) {
+  const int WPA = std::max(1, QNW / (p.Br / 16)), WPB = std::max(1, QNW / (p.BfP / 16));
+  const int ZPN = std::max(WPA * p.Br, WPB * p.BfP) * 16;
+  size_t t = ts * ((size_t)p.Br * p.BFP + 2 * (size_t)p.BfP * 16 + (size_t)p.Gf * p.Ro * 16 + ZPN +
+                   4 * (size_t)p.Ro * 16 + 64);
+  t = (t + 15) & ~(size_t)15;
+  t += 8 * ((size_t)p.Ro + 32) + 16 + 16 * 8;
+  (void)K;
+  return t;
+}
+
+PersistPlan2 plan_p2(int B, int D, int K, size_t ts, int num_cus, size_t lds_max) {
+  PersistPlan2 best{};
+  best.ok = false;
+  if (K > 16 || K < 1 || B < 1 || D < 1) return best;
+  const int KC = kc_of(K);
+  int fGr = 0, fGf = 0;
+  if (const char* env = getenv("HMCX_P2_GRID")) sscanf(env, "%dx%d", &fGr, &fGf);
+  const int cand[] = {1, 2, 4, 8, 16};
+  for (int Gr : cand)
+    for (int Gf : cand) {
+      if (fGr && (Gr != fGr || Gf != fGf)) continue;
+      const int G = Gr * Gf;
+      if (G > num_cus || G > 128) continue;
+      PersistPlan2 p{};
+      p.Gr = Gr; p.Gf = Gf;
+      const int rows = (B + Gr - 1) / Gr;
+      p.Br = 16;
+      while (p.Br < rows) p.Br <<= 1;                                         // power of two (GEMM split)
+      if (p.Br > QTH) continue;
+      p.Bf = (D + Gf - 1) / Gf;
+      p.BfP = (p.Bf + 15) / 16 * 16;
+      p.BFP = p.BfP + (ts == 8 ? 2 : 1);
+      p.Ro = (p.Br + Gf - 1) / Gf;
+      p.Fo = (p.Bf + Gr - 1) / Gr;
+      if ((long)(Gr - 1) * rows >= B || (long)(Gf - 1) * p.Bf >= D) continue;  // no empty teams
+      // thread ↔ element mappings of the rounds (one granule per producer per thread)
+      if (KC + 1 + p.Ro * KC > QTH || p.Fo * KC + KC + 1 > QTH || G > QTH) continue;
+      p.lds = p2_lds(p, K, ts);
+      if (p.lds > lds_max) continue;
+      // cost model (cycles): VALU GEMM work per thread + granule loads per thread of the four
+      // rounds + a fixed price per round that grows with the team size
+      const double gemm = 16.0 * ((double)p.Br * p.BfP / QTH);
+      const double loads = ((double)p.Ro * KC + (KC + 1 + p.Ro * KC) + (KC + 1 + p.Fo * KC) + p.Fo * KC);
+      const double cost = 8.0 * gemm + 2.0 * loads * (Gr + Gf) / 2 + 250.0 * (Gr + Gf);
+      p.cost = cost;
+      p.ok = true;
+      if (!best.ok || cost < best.cost) best = p;
+    }
+  return best;
+}
+
+template <typename T>
+int sghmc_p2_t(hmcx_ctx* ctx, const hmcx_sampler_args* s, const PersistPlan2& pl) {
+  const int G = pl.Gr * pl.Gf, K = s->K, KC = kc_of(K);
+  const size_t n = (size_t)s->n_steps;
+  // granule arena: XA, XD, XB, XW, XS (double-buffered), then the abort word
+  const long nXA = 2L * G * pl.Br * KC, nXD = 2L * G * (KC + 1 + pl.Ro * KC), nXB = 2L * G * (KC + 1 + pl.Bf * KC),
+             nXW = 2L * G * pl.Fo * KC, nXS = 2L * G * 4;
+  const long ngran = nXA + nXD + nXB + nXW + nXS + 1;
+  if (ngran * 16 > 0x7fffffffL) return set_error(ctx, HMCX_EUNSUPPORTED, "persistent SGHMC: arena too large");
+  Workspace ws(ctx);
+  char* arena;
+  double *d_eps, *d_u;
+  int64_t *d_row0, *d_noff;
+  int32_t* d_n;
+  do {
+    ws.reset();
+    arena = reinterpret_cast<char*>(ws.take<double>((size_t)ngran * 2));
+    d_eps = ws.take<double>(n);
+    d_u = ws.take<double>(n);
+    d_row0 = ws.take<int64_t>(n);
+    d_noff = ws.take<int64_t>(n);
+    d_n = ws.take<int32_t>(n);
+  } while (ws.retry());
+  if (ws.failed) return HMCX_ENOMEM;
+  begin_call(ctx);
+  int rc;
+  if ((rc = upload(ctx, d_eps, s->eps, n * sizeof(double)))) return rc;
+  if ((rc = upload(ctx, d_u, s->u_accept, n * sizeof(double)))) return rc;
+  if ((rc = upload(ctx, d_row0, s->row0, n * sizeof(int64_t)))) return rc;
+  if ((rc = upload(ctx, d_n, s->n_iter, n * sizeof(int32_t)))) return rc;
+  if (s->noise_mode == HMCX_NOISE_BUFFER && (rc = upload(ctx, d_noff, s->noise_off, n * sizeof(int64_t)))) return rc;
+  HMCX_HIP(ctx, hipMemsetAsync(arena, 0, (size_t)ngran * 16, ctx->stream));
+
+  Q2Args a{};
+  a.B = s->B; a.D = s->D; a.K = K; a.P = s->D * K + K; a.n_steps = s->n_steps;
+  a.Gr = pl.Gr; a.Gf = pl.Gf; a.Br = pl.Br; a.Bf = pl.Bf; a.BfP = pl.BfP; a.BFP = pl.BFP; a.Ro = pl.Ro; a.Fo = pl.Fo;
+  a.alpha = s->alpha; a.neg_inv_n = -1.0 / (double)s->B; a.log_prior = s->log_prior;
+  a.X = s->X; a.Y = s->Y;
+  a.eps = d_eps; a.u = d_u; a.row0 = d_row0; a.n_iter = d_n;
+  a.noise_mode = s->noise_mode; a.noise = s->noise; a.noff = d_noff;
+  a.seed = s->seed; a.chain0 = s->chain0; a.step_base = s->step_base;
+  a.W = s->W; a.b = s->b;
+  a.arena = arena;
+  a.oXA = 0; a.oXD = (int)nXA; a.oXB = (int)(nXA + nXD); a.oXW = (int)(nXA + nXD + nXB);
+  a.oXS = (int)(nXA + nXD + nXB + nXW);
+  a.arena_bytes = (int)(ngran * 16);
+  a.abort_flag = reinterpret_cast<int*>(arena + (ngran - 1) * 16);
+  a.out_A = s->out_A; a.out_acc = s->out_accepted; a.out_ll = s->out_ll; a.out_E = s->out_E;
+  static const bool prof_on = getenv("HMCX_PERSIST_PROF") && getenv("HMCX_PERSIST_PROF")[0] == '1';
+  unsigned long long* dprof = nullptr;
+  if (prof_on) {
+    HMCX_HIP(ctx, hipMalloc((void**)&dprof, 16 * sizeof(unsigned long long)));
+    HMCX_HIP(ctx, hipMemsetAsync(dprof, 0, 16 * sizeof(unsigned long long), ctx->stream));
+  }
+  a.prof = dprof;
+  const void* kfn = KC == 10 ? (const void*)k_sghmc_p2<T, 10> : (const void*)k_sghmc_p2<T, 16>;
+  HMCX_HIP(ctx, hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.lds));
+  void* kargs[] = {&a};
+  if ((rc = timing_begin(ctx, ctx->stream))) return rc;
+  HMCX_HIP(ctx, hipLaunchCooperativeKernel(kfn, dim3(G), dim3(QTH), kargs, (unsigned)pl.lds, ctx->stream));
+  if ((rc = timing_end(ctx, ctx->stream))) return rc;
+  int flag = 0;
+  HMCX_HIP(ctx, hipMemcpyAsync(&flag, a.abort_flag, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  HMCX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if ((rc = timing_collect(ctx))) return rc;
+  if (dprof) {
+    unsigned long long h[16];
+    HMCX_HIP(ctx, hipMemcpy(h, dprof, sizeof(h), hipMemcpyDeviceToHost));
+    (void)hipFree(dprof);
+    unsigned long long tot = 0;
+    for (int i = 0; i < 12; ++i) tot += h[i];
+    static const char* names[12] = {"step-start", "A-gemm+publish", "noise", "A-RS wait", "softmax", "A-AG",
+                                    "B-gemm+publish", "B-RS wait", "update", "B-AG", "accept", "it=-1"};
+    fprintf(stderr, "[hmcx p2 prof] G=%dx%d Br=%d Bf=%d Ro=%d Fo=%d total %llu ticks:", pl.Gr, pl.Gf, pl.Br, pl.Bf,
+            pl.Ro, pl.Fo, tot);
+    for (int i = 0; i < 12; ++i) fprintf(stderr, " %s %.1f%%", names[i], tot ? 100.0 * h[i] / tot : 0.0);
+    fprintf(stderr, "\n");
+  }
+  if (flag) return set_error(ctx, HMCX_EHIP, "persistent SGHMC: hand-off timed out (workgroups not co-resident?)");
+  return HMCX_OK;
+}
+
+template int sghmc_p2_t<float>(hmcx_ctx*, const hmcx_sampler_args*, const PersistPlan2&);
+template int sghmc_p2_t<double>(hmcx_ctx*, const hmcx_sampler_args*, const PersistPlan2&);
+
+}  // namespace hmcx

@@ -679,8 +679,13 @@ int softmax_predict_t(hmcx_ctx* ctx, const void* X, int B, int D, int K, int C, 
 template <typename T>
 int sghmc_run_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
   const int B = s->B, D = s->D, K = s->K, C = s->C, N = C * K;
-  if (C == 1 && ctx->sghmc_path != 1) {   // single chain: persistent kernel (hmcx_persist.hip)
-    const PersistPlan pl = plan_persist(B, D, K, sizeof(T), ctx->num_cus, ctx->lds_max);
+  if (C == 1 && ctx->sghmc_path != 1) {   // single chain: persistent kernel
+    static const bool v1 = getenv("HMCX_PERSIST_V1") && getenv("HMCX_PERSIST_V1")[0] == '1';
+    if (!v1) {                            // hmcx_persist2.hip (tagged-granule teams)
+      const PersistPlan2 p2 = plan_p2(B, D, K, sizeof(T), ctx->num_cus, ctx->lds_max);
+      if (p2.ok) return sghmc_p2_t<T>(ctx, s, p2);
+    }
+    const PersistPlan pl = plan_persist(B, D, K, sizeof(T), ctx->num_cus, ctx->lds_max);   // hmcx_persist.hip
     if (pl.ok) return sghmc_persist_t<T>(ctx, s, pl);
     if (ctx->sghmc_path == 2) return set_error(ctx, HMCX_EUNSUPPORTED, "persistent SGHMC: shape not supported");
   } else if (ctx->sghmc_path == 2) {
