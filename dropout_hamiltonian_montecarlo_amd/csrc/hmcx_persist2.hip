@@ -720,7 +720,7 @@ PersistPlan2 plan_p2(int B, int D, int K, size_t ts, int num_cus, size_t lds_max
     for (int Gf : cand) {
       if (fGr && (Gr != fGr || Gf != fGf)) continue;
       const int G = Gr * Gf;
-      if (G > num_cus || G > 128) continue;
+      if (G > num_cus) continue;
       PersistPlan2 p{};
       p.Gr = Gr; p.Gf = Gf;
       const int rows = (B + Gr - 1) / Gr;
@@ -737,11 +737,12 @@ PersistPlan2 plan_p2(int B, int D, int K, size_t ts, int num_cus, size_t lds_max
       if (KC + 1 + p.Ro * KC > QTH || p.Fo * KC + KC + 1 > QTH || G > QTH) continue;
       p.lds = p2_lds(p, K, ts);
       if (p.lds > lds_max) continue;
-      // cost model (cycles): VALU GEMM work per thread + granule loads per thread of the four
-      // rounds + a fixed price per round that grows with the team size
-      const double gemm = 16.0 * ((double)p.Br * p.BfP / QTH);
-      const double loads = ((double)p.Ro * KC + (KC + 1 + p.Ro * KC) + (KC + 1 + p.Fo * KC) + p.Fo * KC);
-      const double cost = 8.0 * gemm + 2.0 * loads * (Gr + Gf) / 2 + 250.0 * (Gr + Gf);
+      // cost model (calibrated on MI355X at B=500, D=784, K=10: 8x16 15.6, 16x8 16.3, 8x8 16.7,
+      // 16x16 16.8, 4x16 27 µs per leapfrog): f64 MFMAs per wave of the two GEMMs, plus a price per
+      // member of the row teams (A rounds, softmax skew) and of the feature teams
+      const int WPA = std::max(1, QNW / (p.Br / 16)), WPB = std::max(1, QNW / (p.BfP / 16));
+      const double mfma = (double)(p.Br / 16) * (p.BfP / 4) / QNW + (double)(p.BfP / 16) * (p.Br / 4) / QNW;
+      const double cost = 300.0 * mfma + 700.0 * Gr + 400.0 * Gf + 0.0 * (WPA + WPB);
       p.cost = cost;
       p.ok = true;
       if (!best.ok || cost < best.cost) best = p;
