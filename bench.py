@@ -54,15 +54,33 @@ def synthetic_data(seed=0):
     return X, Y
 
 
-def cpu_baseline(X, Y, budget_s):
-    """The oracle (NumPy float64 restatement of the reference SGHMC, bit-exact to it) on host
-    cores: bounded sample of the same workload, leapfrogs counted the same way."""
-    from oracle import models as om, samplers as osm
+def cpu_model():
     try:
-        import threadpoolctl
-        threads = max(i.get("num_threads", 1) for i in threadpoolctl.threadpool_info()) or 1
-    except Exception:
-        threads = len(os.sched_getaffinity(0))
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(X, Y, budget_s, threads=None):
+    """The oracle (NumPy float64 restatement of the reference SGHMC, bit-exact to it) on host
+    cores: bounded sample of the same workload, leapfrogs counted the same way.  threads=None:
+    OpenBLAS default (all cores of the affinity mask); threads=1: one BLAS thread."""
+    import threadpoolctl
+    if threads is None:
+        return _cpu_baseline(X, Y, budget_s)
+    with threadpoolctl.threadpool_limits(limits=threads, user_api="blas"):
+        return _cpu_baseline(X, Y, budget_s)
+
+
+def _cpu_baseline(X, Y, budget_s):
+    from oracle import models as om, samplers as osm
+    import threadpoolctl
+    blas = [i for i in threadpoolctl.threadpool_info() if i.get("user_api") == "blas"]
+    threads = max((i.get("num_threads", 1) for i in blas), default=1)
     nb = 10
     Xs, Ys = X[:nb * B], Y[:nb * B]
     lf, t_total, steps = 0.0, 0.0, 0
@@ -83,8 +101,20 @@ def cpu_baseline(X, Y, budget_s):
             "kind": "port",
             "sample": "oracle/samplers.py SGHMC (NumPy f64, bit-exact to the reference) incl. its per-10-minibatch "
                       "log-likelihood logging: %d steps / %.0f leapfrogs on minibatches of B=500 (D=784, K=10), "
-                      "eps=1e-3, lambda=1e-2, %.1f s, %d BLAS threads" % (steps, lf, t_total, threads),
+                      "eps=1e-3, lambda=1e-2, %.1f s, %d BLAS threads, host %s (%d CPUs in affinity mask)" % (
+                          steps, lf, t_total, threads, cpu_model(), len(os.sched_getaffinity(0))),
             "lf_per_s": lf / t_total}
+
+
+def pmc_traffic(dtype, path):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC run of this
+    bench configuration (profiles/pmc_*.json, see tools/gpu_pmc_bench.sh): 2·FETCH_SIZE +
+    WRITE_SIZE (MI355X_MICROARCH.md: FETCH_SIZE counts half of 16-byte streaming reads)."""
+    f = os.path.join(REPO, "profiles", "pmc_r01_%s_%s.json" % (dtype, path))
+    if not os.path.exists(f):
+        return None
+    with open(f) as fh:
+        return json.load(fh).get("traffic_bytes_per_launch")
 
 
 def main():
@@ -184,8 +214,8 @@ def main():
         "leapfrogs_per_s": lf_total / t_max,
         "leapfrogs": lf_total,
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
-                     "frac": achieved / peak, "traffic": None,
-                     "kernel": ("k_sghmc_persist<%s> (one launch per %d-step call)" % (
+                     "frac": achieved / peak, "traffic": pmc_traffic(args.dtype, path),
+                     "kernel": ("k_sghmc_p2<%s,10> (one launch per %d-step call)" % (
                          "double" if args.dtype == "f64" else "float", CHUNK)) if path == "persistent"
                      else "kernel-per-phase sequence of one %d-step call" % CHUNK,
                      "launch_ms": launch_ms, "flop_per_launch": flop_per_launch},
@@ -194,8 +224,8 @@ def main():
         "cpu_baseline": None,
     }
     if world == 1 and args.cpu_seconds > 0:
-        cb = cpu_baseline(X, Y, args.cpu_seconds)
-        out["cpu_baseline"] = cb
+        out["cpu_baseline"] = cpu_baseline(X, Y, args.cpu_seconds)
+        out["cpu_baseline_1thread"] = cpu_baseline(X, Y, args.cpu_seconds, threads=1)
     print(json.dumps(out))
 
 

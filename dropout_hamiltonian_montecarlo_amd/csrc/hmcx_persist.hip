@@ -680,8 +680,12 @@ int sghmc_persist_t(hmcx_ctx* ctx, const hmcx_sampler_args* s, const PersistPlan
                                     (int)pl.lds));
   void* kargs[] = {&a};
   if ((rc = timing_begin(ctx, ctx->stream))) return rc;
-  HMCX_HIP(ctx, hipLaunchCooperativeKernel((const void*)k_sghmc_persist<T>, dim3(G), dim3(PTH), kargs,
-                                           (unsigned)pl.lds, ctx->stream));
+  int per_cu = 0;
+  HMCX_HIP(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_sghmc_persist<T>, PTH, pl.lds));
+  if ((long)per_cu * ctx->num_cus < G)
+    return set_error(ctx, HMCX_EUNSUPPORTED, "persistent SGHMC: workgroups cannot be co-resident");
+  HMCX_HIP(ctx, hipLaunchKernel((const void*)k_sghmc_persist<T>, dim3(G), dim3(PTH), kargs, (unsigned)pl.lds,
+                                ctx->stream));
   if ((rc = timing_end(ctx, ctx->stream))) return rc;
   // the abort flag is checked synchronously: a timed-out barrier must not pass silently
   int flag = 0;

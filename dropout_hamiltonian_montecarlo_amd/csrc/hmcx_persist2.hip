@@ -809,7 +809,13 @@ int sghmc_p2_t(hmcx_ctx* ctx, const hmcx_sampler_args* s, const PersistPlan2& pl
   HMCX_HIP(ctx, hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.lds));
   void* kargs[] = {&a};
   if ((rc = timing_begin(ctx, ctx->stream))) return rc;
-  HMCX_HIP(ctx, hipLaunchCooperativeKernel(kfn, dim3(G), dim3(QTH), kargs, (unsigned)pl.lds, ctx->stream));
+  // co-residency of all G workgroups is checked here (occupancy query × CUs); a plain launch then
+  // has the same residency as a cooperative one without its per-launch host cost
+  int per_cu = 0;
+  HMCX_HIP(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, QTH, pl.lds));
+  if ((long)per_cu * ctx->num_cus < G)
+    return set_error(ctx, HMCX_EUNSUPPORTED, "persistent SGHMC: workgroups cannot be co-resident");
+  HMCX_HIP(ctx, hipLaunchKernel(kfn, dim3(G), dim3(QTH), kargs, (unsigned)pl.lds, ctx->stream));
   if ((rc = timing_end(ctx, ctx->stream))) return rc;
   int flag = 0;
   HMCX_HIP(ctx, hipMemcpyAsync(&flag, a.abort_flag, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
