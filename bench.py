@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--dtype", choices=["f64", "f32"], default="f64")
     ap.add_argument("--path", choices=["auto", "kernels", "persistent"], default="auto")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline time budget (0 = skip)")
+    ap.add_argument("--batched-chains", type=int, default=1024,
+                    help="chains per GPU of the secondary chain-batched measurement (0 = skip)")
     return ap.parse_args()
 
 
@@ -117,6 +119,39 @@ def pmc_traffic(dtype, path):
         return json.load(fh).get("traffic_bytes_per_launch")
 
 
+def batched_chains(model, X, Y, data, C, n_steps, rank):
+    """Secondary measurement: C independent chains on this GPU sharing every
+    minibatch, i.e. the chain-batched gradient GEMMs [B×D]·[D×10C] and [D×B]·[B×10C]
+    (hmcx_batch.h).  Returns throughput and the GEMM roofline of that path."""
+    import torch
+    from dropout_hamiltonian_montecarlo_amd.hamiltonian.inference.gpu.sghmc import sghmc
+    s = sghmc(model, {"weights": np.zeros((D, K)), "bias": np.zeros(K)}, path_length=LAMBDA, step_size=EPS,
+              noise="philox", seed=7, chain=rank * C, chains=C)
+    s.out = io.StringIO()
+    state = s._init_state()
+    nb = N_DATA // B
+    rows = [(i % nb) * B for i in range(n_steps)]
+    s.trace = []
+    s._run(state, data, rows[:4], [EPS] * 4, None, B)          # warm-up (workspace, code objects)
+    torch.cuda.synchronize()
+    s.trace = []
+    model.ctx.set_timing(True)
+    t0 = time.perf_counter()
+    s._run(state, data, rows, [EPS] * n_steps, None, B)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    kms, kn = model.ctx.get_timing()
+    model.ctx.set_timing(False)
+    lf = float(sum(np.maximum(0.0, t["L"] - 1).sum() for t in s.trace))
+    achieved = FLOP_PER_LEAPFROG * lf / (kms * 1e-3) / 1e12
+    return {"chains_per_gpu": C, "steps": n_steps, "leapfrogs": lf, "leapfrogs_per_s": lf / dt,
+            "value": lf / dt * P, "unit": "leapfrog-steps/s x param-dim", "ms": dt * 1e3,
+            "roofline": {"bound": "mfma", "achieved": achieved, "peak": MFMA_PEAK_TFLOPS["f64" if model.dtype.itemsize == 8 else "f32"],
+                         "unit": "TFLOP/s", "frac": achieved / MFMA_PEAK_TFLOPS["f64" if model.dtype.itemsize == 8 else "f32"],
+                         "kernel": "k_bfwd + k_bgrad + step kernels of one hmcx_sghmc_run call",
+                         "device_ms": kms, "flop": FLOP_PER_LEAPFROG * lf}}
+
+
 def main():
     args = parse()
     import torch
@@ -186,6 +221,11 @@ def main():
     allt = parallel.gather_traces(trace, device=dev)
     diag = parallel.chain_diagnostics(allt) if allt.shape[1] >= 4 else {"rhat": np.nan, "ess": np.nan}
 
+    batched = None
+    if args.batched_chains > 0:
+        model.ctx.set_sghmc_path(0)
+        batched = batched_chains(model, X, Y, data, args.batched_chains, 24, rank)
+        parallel.barrier()
     if rank != 0:
         return
     path = "persistent" if (args.path != "kernels") else "kernels"
@@ -222,6 +262,7 @@ def main():
         "diagnostics": {"rhat_ll": float(np.ravel(diag["rhat"])[0]), "ess_ll": float(np.ravel(diag["ess"])[0]),
                         "gather": "torch.distributed all_gather (%s)" % ("nccl/RCCL" if world > 1 else "local")},
         "cpu_baseline": None,
+        "chain_batched": batched,
     }
     if world == 1 and args.cpu_seconds > 0:
         out["cpu_baseline"] = cpu_baseline(X, Y, args.cpu_seconds)

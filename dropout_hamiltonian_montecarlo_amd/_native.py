@@ -210,3 +210,27 @@ def philox_normals(seed, chain, step, slot, e0, n):
 
 SLOT_PATH = 0xFFFFFFFE
 SLOT_ACCEPT = 0xFFFFFFFD
+
+
+def philox_uniforms_chains(seed, chains, step, slot, idx=0):
+    """Philox4x32-10 uniform of element `idx` for every (step, chain): `chains` and `step` broadcast
+    against each other (vectorised host twin of hmcx_common.h::philox_uniform, bit-identical to
+    hmcx_philox_uniforms)."""
+    import numpy as np
+    M0, M1 = np.uint64(0xD2511F53), np.uint64(0xCD9E8D57)
+    mask = np.uint64(0xFFFFFFFF)
+    ch, st = np.broadcast_arrays(np.asarray(chains, dtype=np.uint64) & mask,
+                                 np.asarray(step, dtype=np.uint64) & mask)
+    c0 = np.full(ch.shape, idx, dtype=np.uint64)
+    c1 = np.full(ch.shape, slot & 0xFFFFFFFF, dtype=np.uint64)
+    c2 = st.copy()
+    c3 = ch.copy()
+    k0, k1 = seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF
+    for _ in range(10):
+        p0 = M0 * c0
+        p1 = M1 * c2
+        c0, c1, c2, c3 = ((p1 >> np.uint64(32)) ^ c1 ^ np.uint64(k0)), p1 & mask, \
+                         ((p0 >> np.uint64(32)) ^ c3 ^ np.uint64(k1)), p0 & mask
+        k0 = (k0 + 0x9E3779B9) & 0xFFFFFFFF
+        k1 = (k1 + 0xBB67AE85) & 0xFFFFFFFF
+    return ((c0 << np.uint64(21)) ^ (c1 >> np.uint64(11))).astype(np.float64) * (1.0 / 9007199254740992.0)

@@ -1,0 +1,410 @@
+// hmcx_batch.h — chain-batched SGHMC leapfrog GEMMs: C chains sharing one minibatch (C >= 16, K = 10).
+//
+// Same arithmetic as k_fwd / k_grad (hmcx_softmax.hip; reference cpu/sghmc.py:28-34 and
+// cpu/softmax.py:38-61), re-tiled for the chain-batched gradient GEMMs of SURVEY §8d,
+// [B×D]·[D×10C] and [D×B]·[B×10C]:
+//
+//  * k_bfwd: tile = 32 minibatch rows × 16 chains (160 columns); the D loop is staged through LDS in
+//    32-deep chunks (register prefetch of the next chunk), 4 waves × (16 rows × 80 columns) of
+//    v_mfma_*_16x16x4.  Epilogue per (row, chain): both softmaxes (at b and b' = b + ε·pb), diff,
+//    bias colsum partial, log-likelihood partial.
+//  * k_bgrad: tile = 32 features × 16 chains; the minibatch loop staged the same way; the friction
+//    noise of the tile is generated into LDS before the loop (one Philox block per 4 elements), the
+//    SGHMC update (gradient, momentum, drift, kinetic partial) runs on the accumulators in registers;
+//    workgroups of feature tile 0 finish the bias sub-step.
+//  * Active-chain compaction: per step the host orders chains by path length (descending); at
+//    leapfrog iteration `it` only ranks < c_act(it) are launched, so the work is proportional to the
+//    leapfrog count, not to max_c L_c.
+#pragma once
+#include "hmcx_common.h"
+#include "hmcx_internal.h"
+
+namespace hmcx {
+
+constexpr int BCT = 16;           // chains per tile
+constexpr int BKC = 10;           // classes (compiled for K = 10)
+constexpr int BNT = BCT * BKC;    // 160 columns per tile
+constexpr int BRW = 32;           // rows (k_bfwd) / features (k_bgrad) per tile
+constexpr int BCH = 32;           // depth of one staged k-chunk
+constexpr int BXP = BCH + 1;      // LDS pitch of the X chunk
+constexpr int BWP = BNT + 2;      // LDS pitch of the W / diff chunk
+
+template <typename T> struct BFwdArgs {
+  const T* X; const T* Y;           // minibatch rows (offset to the step's first row)
+  const T* W; const T* b; const T* pb;
+  int B, D, C, N, mode, iter, c_act;
+  T eps;
+  const int32_t* n_iter;            // [C] of this step
+  const int32_t* perm;              // [C] chain of each rank (path length descending)
+  T* diff;                          // [B][N]
+  T* colsum_part;                   // [nRB][N]
+  double* ll_part;                  // [nRB][C]
+};
+
+template <typename T> struct BGradArgs {
+  const T* X; const T* diff; const T* colsum_part;
+  int B, D, C, N, nRB, iter, c_act, P;
+  T alpha, eps, one_minus_eps, noise_scale;
+  const int32_t* n_iter; const int32_t* perm;
+  T* W; T* b; T* pW; T* pb;
+  double* kin_part;                 // [nDB][C]
+  double* kinb;                     // [C]
+  int noise_mode; const double* noise; const int64_t* noff;
+  uint64_t seed; uint32_t chain0, step, slot;
+};
+
+// Staging map of one 32-deep chunk: X part [32][32] as 512 two-element vectors (thread: 2), W/diff
+// part [32][16 chains × 10] as 2560 vectors (thread: 10); vector j of the W part covers row
+// j / 80, chain slot (j % 80) / 5, classes 2·(j % 5) .. +1, so 5 consecutive lanes read one chain's
+// contiguous 10-value row segment.
+template <typename T, int XM = 1> struct StageMap {
+  typedef T v2 __attribute__((ext_vector_type(2)));
+  int xr[2 * XM], xc[2 * XM];
+  int wr[10], wcol[10], wls[10];
+  bool wok[10];
+  __device__ StageMap(int tid, const int* chs) {
+#pragma unroll
+    for (int u = 0; u < 2 * XM; ++u) {
+      const int j = tid + 256 * u;
+      xr[u] = j >> 4;
+      xc[u] = (j & 15) * 2;
+    }
+#pragma unroll
+    for (int u = 0; u < 10; ++u) {
+      const int j = tid + 256 * u;
+      const int row = j / 80, rem = j - row * 80, cs = rem / 5, pp = rem - cs * 5;
+      const int ch = chs[cs];
+      wr[u] = row;
+      wok[u] = ch >= 0;
+      wcol[u] = (ch >= 0 ? ch : 0) * BKC + 2 * pp;
+      wls[u] = cs * BKC + 2 * pp;
+    }
+  }
+};
+// two consecutive elements (zero when !ok; only the first when avail == 1)
+template <typename T>
+__device__ inline typename StageMap<T>::v2 ld2(const T* p, bool ok, int avail) {
+  typename StageMap<T>::v2 v = {T(0), T(0)};
+  if (ok && avail >= 2) {
+    v = *reinterpret_cast<const typename StageMap<T>::v2*>(p);
+  } else if (ok && avail == 1) {
+    v[0] = p[0];
+  }
+  return v;
+}
+template <typename T> __device__ inline void st2(T* p, typename StageMap<T>::v2 v) { p[0] = v[0]; p[1] = v[1]; }
+
+// MT = m-tiles per wave: the tile is 32·MT minibatch rows × 16 chains (MT = 2 halves the W
+// staging per MFMA; used when enough chains are active to fill the chip).
+template <typename T, int MT>
+__global__ __launch_bounds__(256) void k_bfwd(BFwdArgs<T> a) {
+  using M = mfma16<T>;
+  constexpr int ROWS = 32 * MT;
+  __shared__ T Xs[ROWS * BXP];
+  __shared__ T Ws[BCH * BWP];          // also the epilogue tile, 32 rows at a time
+  __shared__ double Lt[ROWS][BCT];
+  __shared__ int chs[BCT];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lg = lane >> 4;
+  const int m0 = blockIdx.x * ROWS, rank0 = blockIdx.y * BCT;
+  const int nrow = min(ROWS, a.B - m0);
+  const int D = a.D, N = a.N;
+  if (tid < BCT) chs[tid] = rank0 + tid < a.c_act ? a.perm[rank0 + tid] : -1;
+  __syncthreads();
+
+  // staging: 2-element vectors; X chunk [ROWS][32 d] (2·MT per thread), W chunk
+  // [32 d][16 chains × 10] = 2560 vectors (10 per thread, consecutive lanes walk one chain's row)
+  StageMap<T, MT> sm(tid, chs);
+  const T* xsrc[2 * MT];
+#pragma unroll
+  for (int u = 0; u < 2 * MT; ++u) xsrc[u] = a.X + (size_t)(m0 + min(sm.xr[u], nrow - 1)) * D + sm.xc[u];
+  typename StageMap<T>::v2 xv[2 * MT], wv[10];
+  auto fetch = [&](int k0) {
+#pragma unroll
+    for (int u = 0; u < 2 * MT; ++u) xv[u] = ld2<T>(xsrc[u] + k0, sm.xr[u] < nrow, D - k0 - sm.xc[u]);
+#pragma unroll
+    for (int u = 0; u < 10; ++u) {
+      const int d = k0 + sm.wr[u];
+      wv[u] = ld2<T>(a.W + (size_t)min(d, D - 1) * N + sm.wcol[u], sm.wok[u] && d < D, 2);
+    }
+  };
+  auto stash = [&]() {
+#pragma unroll
+    for (int u = 0; u < 2 * MT; ++u) st2<T>(Xs + sm.xr[u] * BXP + sm.xc[u], xv[u]);
+#pragma unroll
+    for (int u = 0; u < 10; ++u) st2<T>(Ws + sm.wr[u] * BWP + sm.wls[u], wv[u]);
+  };
+
+  const int wm = wave & 1, nh = wave >> 1;            // rows [16·(wm·MT + i)], 5 n-tiles per wave
+  typename M::acc_t acc[MT][5];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < 5; ++j) acc[i][j] = M::zero();
+  fetch(0);
+  for (int k0 = 0; k0 < D; k0 += BCH) {
+    __syncthreads();
+    stash();
+    __syncthreads();
+    if (k0 + BCH < D) fetch(k0 + BCH);                 // next chunk in flight during the MFMAs
+    const int nks = min(BCH, D - k0 + 3) / 4;
+#pragma unroll 2
+    for (int ks = 0; ks < nks; ++ks) {
+      T av[MT], bv[5];
+#pragma unroll
+      for (int i = 0; i < MT; ++i) av[i] = Xs[((wm * MT + i) * 16 + lr) * BXP + ks * 4 + lg];
+#pragma unroll
+      for (int j = 0; j < 5; ++j) bv[j] = Ws[(ks * 4 + lg) * BWP + (nh * 5 + j) * 16 + lr];
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < 5; ++j) acc[i][j] = M::fma(av[i], bv[j], acc[i][j]);
+    }
+  }
+
+  // ---- epilogue, 32 rows at a time through Zt: softmax.py:32-36 (clip, max, exp, normalise), :52
+  const T hi = (T)CLIP_HI, lo = (T)CLIP_LO;
+  const bool sghmc = a.mode == FWD_SGHMC;
+  T* Zt = Ws;                                          // [32][BWP] logits, then y − ŷ'
+  T cs_acc = T(0);                                     // thread t < 160: Σ_rows (y − ŷ') of column t
+  for (int half = 0; half < MT; ++half) {
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      // wave rows of m-tile (wm·MT + i) fall in half (wm·MT + i) / 2
+      const int mtile = wm * MT + i;
+      if ((mtile >> 1) != half) continue;
+#pragma unroll
+      for (int j = 0; j < 5; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          Zt[((mtile & 1) * 16 + M::row(lane, q)) * BWP + (nh * 5 + j) * 16 + lr] = acc[i][j][q];
+    }
+    __syncthreads();
+    for (int pr = tid; pr < 32 * BCT; pr += 256) {
+      const int il = pr >> 4, cs = pr & 15, ch = chs[cs];
+      const int i = half * 32 + il;
+      if (ch < 0 || i >= nrow) { Lt[i][cs] = 0.0; continue; }
+      const bool last = sghmc && a.iter == a.n_iter[ch] - 1;
+      T z[BKC], y[BKC];
+#pragma unroll
+      for (int k = 0; k < BKC; ++k) {
+        z[k] = Zt[il * BWP + cs * BKC + k];
+        y[k] = a.Y[(size_t)(m0 + i) * BKC + k];
+      }
+      // variant 1: bias b (weights sub-step diff / LL mode)
+      T zc[BKC], m = T(0), s = T(0);
+#pragma unroll
+      for (int k = 0; k < BKC; ++k) {
+        zc[k] = clipz(z[k] + a.b[ch * BKC + k], hi, lo);
+        m = k == 0 ? zc[0] : max_nan(m, zc[k]);
+      }
+      T e[BKC];
+#pragma unroll
+      for (int k = 0; k < BKC; ++k) { e[k] = exp(zc[k] - m); s += e[k]; }
+      if (!sghmc) {
+        const T lse = log(s) + m;
+        double ll = 0.0;
+#pragma unroll
+        for (int k = 0; k < BKC; ++k) ll += (double)(y[k] * (zc[k] - lse));
+        Lt[i][cs] = ll;
+        continue;
+      }
+      T* drow = a.diff + (size_t)(m0 + i) * N + ch * BKC;
+#pragma unroll
+      for (int k = 0; k < BKC; ++k) drow[k] = y[k] - e[k] / s;
+      // variant 2: bias b' = b + ε·pb (bias sub-step, sghmc.py:32 on the bias)
+      T m2 = T(0), s2 = T(0);
+#pragma unroll
+      for (int k = 0; k < BKC; ++k) {
+        const T bp = a.b[ch * BKC + k] + a.eps * a.pb[ch * BKC + k];
+        zc[k] = clipz(z[k] + bp, hi, lo);
+        m2 = k == 0 ? zc[0] : max_nan(m2, zc[k]);
+      }
+#pragma unroll
+      for (int k = 0; k < BKC; ++k) { e[k] = exp(zc[k] - m2); s2 += e[k]; }
+#pragma unroll
+      for (int k = 0; k < BKC; ++k) Zt[il * BWP + cs * BKC + k] = y[k] - e[k] / s2;
+      double ll = 0.0;
+      if (last) {
+        const T lse = log(s2) + m2;
+#pragma unroll
+        for (int k = 0; k < BKC; ++k) ll += (double)(y[k] * (zc[k] - lse));
+      }
+      Lt[i][cs] = ll;
+    }
+    __syncthreads();
+    if (sghmc && tid < BNT) {
+      const int nr = min(32, nrow - half * 32);
+      for (int il = 0; il < nr; ++il) cs_acc += Zt[il * BWP + tid];
+    }
+  }
+  if (sghmc && tid < BNT) {                            // Σ_rows (y − ŷ') of this tile
+    const int cs = tid / BKC, ch = chs[cs];
+    if (ch >= 0) a.colsum_part[(size_t)blockIdx.x * N + ch * BKC + (tid - cs * BKC)] = cs_acc;
+  }
+  if (tid < BCT) {
+    const int ch = chs[tid];
+    if (ch >= 0 && (!sghmc || a.iter == a.n_iter[ch] - 1)) {
+      double v = 0.0;
+      for (int i = 0; i < nrow; ++i) v += Lt[i][tid];
+      a.ll_part[(size_t)blockIdx.x * a.C + ch] = v;
+    }
+  }
+}
+
+template <typename T>
+__device__ inline T bnoise(const BGradArgs<T>& a, int ch, uint32_t e, const float* z4) {
+  if (a.noise_mode == HMCX_NOISE_BUFFER) return (T)a.noise[a.noff[ch] + (int64_t)a.slot * a.P + e];
+  return (T)z4[e & 3];
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_bgrad(BGradArgs<T> a) {
+  using M = mfma16<T>;
+  __shared__ T Xs[BCH * BXP];          // [row][feature]
+  __shared__ T Ds[BCH * BWP];          // [row][column]; later the p² tile
+  __shared__ float Nz[BRW * BNT];      // friction noise of the tile
+  __shared__ int chs[BCT];
+  __shared__ T pbs[BNT];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lg = lane >> 4;
+  const int d0 = blockIdx.x * BRW, rank0 = blockIdx.y * BCT;
+  const int nfeat = min(BRW, a.D - d0);
+  const int D = a.D, N = a.N, B = a.B;
+  if (tid < BCT) chs[tid] = rank0 + tid < a.c_act ? a.perm[rank0 + tid] : -1;
+  __syncthreads();
+
+  // noise of the tile: chain slot cs, elements e = d·K + k (d in [d0, d0+nfeat)), 4 per Philox block
+  if (a.noise_mode != HMCX_NOISE_BUFFER) {
+    const int e0 = d0 * BKC, ne = nfeat * BKC;
+    const int g0 = e0 >> 2, ng = ((e0 + ne + 3) >> 2) - g0;
+    for (int t = tid; t < BCT * ng; t += 256) {
+      const int cs = t / ng, g = g0 + (t - cs * ng), ch = chs[cs];
+      if (ch < 0) continue;
+      float z4[4];
+      philox_normal4(a.seed, a.chain0 + ch, a.step, a.slot, (uint32_t)g, z4);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int e = 4 * g + q - e0;
+        if (e >= 0 && e < ne) Nz[(e / BKC) * BNT + cs * BKC + (e % BKC)] = z4[q];
+      }
+    }
+  }
+
+  StageMap<T> sm(tid, chs);                          // X chunk [32 rows][32 features], diff [32 rows][160]
+  typename StageMap<T>::v2 xv[2], dv[10];
+  auto fetch = [&](int r0) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int r = r0 + sm.xr[u];
+      xv[u] = ld2<T>(a.X + (size_t)min(r, B - 1) * D + d0 + sm.xc[u], r < B, nfeat - sm.xc[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 10; ++u) {
+      const int r = r0 + sm.wr[u];
+      dv[u] = ld2<T>(a.diff + (size_t)min(r, B - 1) * N + sm.wcol[u], sm.wok[u] && r < B, 2);
+    }
+  };
+  auto stash = [&]() {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) st2<T>(Xs + sm.xr[u] * BXP + sm.xc[u], xv[u]);
+#pragma unroll
+    for (int u = 0; u < 10; ++u) st2<T>(Ds + sm.wr[u] * BWP + sm.wls[u], dv[u]);
+  };
+
+  const int mt = wave & 1, nh = wave >> 1;
+  typename M::acc_t acc[5];
+#pragma unroll
+  for (int j = 0; j < 5; ++j) acc[j] = M::zero();
+  fetch(0);
+  for (int r0 = 0; r0 < B; r0 += BCH) {
+    __syncthreads();
+    stash();
+    __syncthreads();
+    if (r0 + BCH < B) fetch(r0 + BCH);
+    const int nks = min(BCH, B - r0 + 3) / 4;
+#pragma unroll 2
+    for (int ks = 0; ks < nks; ++ks) {
+      const T av = Xs[(ks * 4 + lg) * BXP + mt * 16 + lr];          // A(feature, row) = X[row][feature]
+      T bv[5];
+#pragma unroll
+      for (int j = 0; j < 5; ++j) bv[j] = Ds[(ks * 4 + lg) * BWP + (nh * 5 + j) * 16 + lr];
+#pragma unroll
+      for (int j = 0; j < 5; ++j) acc[j] = M::fma(av, bv[j], acc[j]);
+    }
+  }
+  __syncthreads();
+
+  // ---- epilogue on the accumulators: softmax.py:57-58 gradient, sghmc.py:31,34 momentum, :32 drift
+  T* P2 = Ds;                                        // [BRW][BWP] p² of chains ending here
+#pragma unroll
+  for (int j = 0; j < 5; ++j)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int fi = mt * 16 + M::row(lane, q), col = (nh * 5 + j) * 16 + lr;
+      const int cs = col / BKC, k = col - cs * BKC, ch = chs[cs];
+      T p2 = T(0);
+      if (ch >= 0 && fi < nfeat) {
+        const int d = d0 + fi;
+        const size_t idx = (size_t)d * N + ch * BKC + k;
+        const T w = a.W[idx];
+        const T gr = -(acc[j][q] - a.alpha * w);
+        const T z = a.noise_mode == HMCX_NOISE_BUFFER
+                        ? (T)a.noise[a.noff[ch] + (int64_t)a.slot * a.P + (uint32_t)(d * BKC + k)]
+                        : (T)Nz[fi * BNT + col];
+        const T p = (a.one_minus_eps * a.pW[idx] + a.eps * gr) + a.noise_scale * z;
+        a.pW[idx] = p;
+        const int n = a.n_iter[ch];
+        if (a.iter < n - 1) a.W[idx] = w + a.eps * p;
+        else p2 = p * p;
+      }
+      P2[fi * BWP + col] = p2;
+    }
+  __syncthreads();
+  if (tid < BCT) {                                   // Σ pW² per chain ending at this iteration
+    const int ch = chs[tid];
+    if (ch >= 0 && a.iter == a.n_iter[ch] - 1) {
+      double v = 0.0;
+      for (int fi = 0; fi < nfeat; ++fi)
+        for (int k = 0; k < BKC; ++k) v += (double)P2[fi * BWP + tid * BKC + k];
+      a.kin_part[(size_t)blockIdx.x * a.C + ch] = v;
+    }
+  }
+  if (blockIdx.x == 0 && tid < BNT) {                // bias sub-step (sghmc.py:32-34 on the bias)
+    const int cs = tid / BKC, k = tid - cs * BKC, ch = chs[cs];
+    T pb_new = T(0);
+    if (ch >= 0) {
+      const int col = ch * BKC + k;
+      T c = T(0);
+      for (int rb = 0; rb < a.nRB; ++rb) c += a.colsum_part[(size_t)rb * N + col];
+      const T bb = a.b[col];
+      T p = a.pb[col];
+      const T bp = bb + a.eps * p;
+      const T gr = -(c - a.alpha * bp);
+      float z4[4] = {0.f, 0.f, 0.f, 0.f};
+      const uint32_t e = (uint32_t)(D * BKC + k);
+      if (a.noise_mode != HMCX_NOISE_BUFFER) philox_normal4(a.seed, a.chain0 + ch, a.step, a.slot, e >> 2, z4);
+      const T z = bnoise(a, ch, e, z4);
+      p = (a.one_minus_eps * p + a.eps * gr) + a.noise_scale * z;
+      a.pb[col] = p;
+      a.b[col] = bp;
+      pb_new = p;
+    }
+    pbs[tid] = pb_new;
+  }
+  if (blockIdx.x == 0) {
+    __syncthreads();
+    if (tid < BCT) {
+      const int ch = chs[tid];
+      if (ch >= 0 && a.iter == a.n_iter[ch] - 1) {
+        double v = 0.0;
+        for (int k = 0; k < BKC; ++k) {
+          const double p = (double)pbs[tid * BKC + k];
+          v += p * p;
+        }
+        a.kinb[ch] = v;
+      }
+    }
+  }
+}
+
+}  // namespace hmcx

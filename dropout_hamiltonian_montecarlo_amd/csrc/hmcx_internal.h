@@ -129,7 +129,7 @@ template <typename T> struct CommitArgs {
 };
 
 template <typename T> struct AcceptArgs {
-  int C, nRB, nDB;
+  int C, nRB, nDB, nDB1;     // nDB: blocks of kin0_part, nDB1: blocks of kin1_part
   const int32_t* n_iter; const double* u;
   double neg_inv_n, log_prior;
   const double* kin0_part; const double* kin0b; const double* kin1_part; const double* kin1b;

@@ -24,6 +24,10 @@
 #include "hmcx_common.h"
 #include "hmcx_internal.h"
 #include "hmcx_persist.h"
+#include "hmcx_batch.h"
+#include <algorithm>
+#include <numeric>
+#include <vector>
 
 namespace hmcx {
 
@@ -523,7 +527,7 @@ __global__ __launch_bounds__(64) void k_sghmc_accept(AcceptArgs<T> a) {
   double ll1 = 0.0, S1W = 0.0;
   if (n > 0) {
     ll1 = block_sum64(a.ll1_part + c, a.nRB, a.C, sh);
-    S1W = block_sum64(a.kin1_part + c, a.nDB, a.C, sh);
+    S1W = block_sum64(a.kin1_part + c, a.nDB1, a.C, sh);
   }
   if (threadIdx.x == 0) {
     const double K0 = (0.0 + 0.5 * S0W) + 0.5 * a.kin0b[c];
@@ -676,6 +680,146 @@ int softmax_predict_t(hmcx_ctx* ctx, const void* X, int B, int D, int K, int C, 
   return HMCX_OK;
 }
 
+// C chains, K = 10: per step k_sghmc_init, k_bfwd(LL) at q0, then per leapfrog iteration k_bfwd +
+// k_bgrad over the chains still moving (ranks < c_act(it), ranks = chains by path length
+// descending), k_sghmc_accept; the last step's proposal is committed by k_sghmc_commit.
+template <typename T>
+int sghmc_batch_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
+  const int B = s->B, D = s->D, K = s->K, C = s->C, N = C * K;
+  // row tiles of 64 (k_bfwd<T,2>) whenever the step's first iteration has >= 32 tiles of chains;
+  // colsum/ll partials are laid out per 64-row tile (a 32-row launch writes two tiles' worth)
+  const bool big = C >= 512;
+  const int RT = big ? 64 : 32;
+  const int nRB = (B + RT - 1) / RT, nDB = (D + BRW - 1) / BRW, nDB16 = (D + 15) / 16;
+  const size_t nsc = (size_t)s->n_steps * C;
+  // host: chain order per step (path length descending, stable) and active counts per iteration
+  std::vector<int32_t> perm(nsc);
+  for (int st = 0; st < s->n_steps; ++st) {
+    int32_t* pr = perm.data() + (size_t)st * C;
+    std::iota(pr, pr + C, 0);
+    const int32_t* ni = s->n_iter + (size_t)st * C;
+    std::stable_sort(pr, pr + C, [&](int32_t x, int32_t y) { return ni[x] > ni[y]; });
+  }
+  Workspace ws(ctx);
+  T *Wwork, *bwork, *pW, *pb, *diff, *csp;
+  double *ll0, *ll1, *k0p, *k0b, *k1p, *k1b, *d_u;
+  int32_t *d_niter, *d_perm;
+  int64_t* d_noff;
+  do {
+    ws.reset();
+    Wwork = ws.take<T>((size_t)D * N);
+    bwork = ws.take<T>(N);
+    pW = ws.take<T>((size_t)D * N);
+    pb = ws.take<T>(N);
+    diff = ws.take<T>((size_t)B * N);
+    csp = ws.take<T>((size_t)nRB * N);
+    ll0 = ws.take<double>((size_t)nRB * C);
+    ll1 = ws.take<double>((size_t)nRB * C);
+    k0p = ws.take<double>((size_t)nDB16 * C);
+    k1p = ws.take<double>((size_t)nDB * C);
+    k0b = ws.take<double>(C);
+    k1b = ws.take<double>(C);
+    d_niter = ws.take<int32_t>(nsc);
+    d_perm = ws.take<int32_t>(nsc);
+    d_u = ws.take<double>(nsc);
+    d_noff = ws.take<int64_t>(nsc);
+  } while (ws.retry());
+  if (ws.failed) return HMCX_ENOMEM;
+  begin_call(ctx);
+  int rc = upload(ctx, d_niter, s->n_iter, nsc * sizeof(int32_t));
+  if (rc) return rc;
+  if ((rc = upload(ctx, d_perm, perm.data(), nsc * sizeof(int32_t)))) return rc;
+  if ((rc = upload(ctx, d_u, s->u_accept, nsc * sizeof(double)))) return rc;
+  if (s->noise_mode == HMCX_NOISE_BUFFER && (rc = upload(ctx, d_noff, s->noise_off, nsc * sizeof(int64_t))))
+    return rc;
+
+  const T* X = (const T*)s->X;
+  const T* Y = (const T*)s->Y;
+  if ((rc = timing_begin(ctx, ctx->stream))) return rc;
+  GraphScope gs(ctx);
+  hipStream_t st = ctx->stream;
+  for (int st_i = 0; st_i < s->n_steps; ++st_i) {
+    const T* Xs = X + (size_t)s->row0[st_i] * D;
+    const T* Ys = Y + (size_t)s->row0[st_i] * K;
+    const double eps = s->eps[st_i];
+    const int32_t* ni_h = s->n_iter + (size_t)st_i * C;
+    int maxit = 0;
+    for (int c = 0; c < C; ++c) maxit = std::max(maxit, (int)ni_h[c]);
+    const int32_t* niter = d_niter + (size_t)st_i * C;
+    const int32_t* prm = d_perm + (size_t)st_i * C;
+    const int64_t* noff = d_noff + (size_t)st_i * C;
+    const uint32_t step_id = s->step_base + (uint32_t)st_i;
+
+    InitArgs<T> ia{};
+    ia.D = D; ia.K = K; ia.C = C; ia.N = N; ia.nDB = nDB16;
+    ia.eps = (T)eps; ia.n_iter = niter;
+    ia.prev_acc = st_i > 0 ? s->out_accepted + (size_t)(st_i - 1) * C : nullptr;
+    ia.noise_mode = s->noise_mode; ia.noise = s->noise; ia.noff = noff;
+    ia.seed = s->seed; ia.chain0 = s->chain0; ia.step = step_id;
+    ia.W = (T*)s->W; ia.b = (T*)s->b;
+    ia.Wwork = Wwork; ia.bwork = bwork; ia.pW = pW; ia.pb = pb;
+    ia.kin0_part = k0p; ia.kin0b = k0b;
+    hipLaunchKernelGGL((k_sghmc_init<T>), dim3(nDB16, C), dim3(256), 0, st, ia);
+    HMCX_HIP(ctx, hipGetLastError());
+
+    BFwdArgs<T> f{};
+    f.X = Xs; f.Y = Ys; f.B = B; f.D = D; f.C = C; f.N = N; f.eps = (T)eps;
+    f.n_iter = niter; f.perm = prm;
+    f.mode = FWD_LL; f.iter = -1; f.c_act = C;                      // E_current at q0 (all chains)
+    f.W = (const T*)s->W; f.b = (const T*)s->b; f.pb = pb;
+    f.ll_part = ll0;
+    if (big) hipLaunchKernelGGL((k_bfwd<T, 2>), dim3(nRB, (C + BCT - 1) / BCT), dim3(256), 0, st, f);
+    else hipLaunchKernelGGL((k_bfwd<T, 1>), dim3(nRB, (C + BCT - 1) / BCT), dim3(256), 0, st, f);
+    HMCX_HIP(ctx, hipGetLastError());
+
+    f.mode = FWD_SGHMC; f.W = Wwork; f.b = bwork;
+    f.diff = diff; f.colsum_part = csp; f.ll_part = ll1;
+    BGradArgs<T> g{};
+    g.X = Xs; g.diff = diff; g.colsum_part = csp;
+    g.B = B; g.D = D; g.C = C; g.N = N; g.nRB = nRB; g.P = D * K + K;
+    g.alpha = (T)s->alpha; g.eps = (T)eps; g.one_minus_eps = (T)(1.0 - eps); g.noise_scale = (T)(2.0 * eps);
+    g.n_iter = niter; g.perm = prm;
+    g.W = Wwork; g.b = bwork; g.pW = pW; g.pb = pb;
+    g.kin_part = k1p; g.kinb = k1b;
+    g.noise_mode = s->noise_mode; g.noise = s->noise; g.noff = noff;
+    g.seed = s->seed; g.chain0 = s->chain0; g.step = step_id;
+    for (int it = 0; it < maxit; ++it) {
+      int c_act = 0;
+      while (c_act < C && ni_h[perm[(size_t)st_i * C + c_act]] > it) ++c_act;
+      f.iter = it; f.c_act = c_act;
+      if (big) hipLaunchKernelGGL((k_bfwd<T, 2>), dim3(nRB, (c_act + BCT - 1) / BCT), dim3(256), 0, st, f);
+      else hipLaunchKernelGGL((k_bfwd<T, 1>), dim3(nRB, (c_act + BCT - 1) / BCT), dim3(256), 0, st, f);
+      HMCX_HIP(ctx, hipGetLastError());
+      g.iter = it; g.c_act = c_act; g.slot = (uint32_t)(it + 1);
+      hipLaunchKernelGGL((k_bgrad<T>), dim3(nDB, (c_act + BCT - 1) / BCT), dim3(256), 0, st, g);
+      HMCX_HIP(ctx, hipGetLastError());
+    }
+    AcceptArgs<T> aa{};
+    aa.C = C; aa.nRB = nRB; aa.nDB = nDB16; aa.nDB1 = nDB;
+    aa.n_iter = niter; aa.u = d_u + (size_t)st_i * C;
+    aa.neg_inv_n = -1.0 / (double)B; aa.log_prior = s->log_prior;
+    aa.kin0_part = k0p; aa.kin0b = k0b; aa.kin1_part = k1p; aa.kin1b = k1b;
+    aa.ll0_part = ll0; aa.ll1_part = ll1;
+    aa.out_A = s->out_A + (size_t)st_i * C;
+    aa.out_acc = s->out_accepted + (size_t)st_i * C;
+    aa.out_ll = s->out_ll + (size_t)st_i * C;
+    aa.out_E = s->out_E ? s->out_E + (size_t)st_i * C * 2 : nullptr;
+    hipLaunchKernelGGL((k_sghmc_accept<T>), dim3(C), dim3(64), 0, st, aa);
+    HMCX_HIP(ctx, hipGetLastError());
+  }
+  CommitArgs<T> ca{};
+  ca.D = D; ca.K = K; ca.C = C; ca.N = N;
+  ca.acc = s->out_accepted + (size_t)(s->n_steps - 1) * C;
+  ca.Wwork = Wwork; ca.bwork = bwork; ca.W = (T*)s->W; ca.b = (T*)s->b;
+  hipLaunchKernelGGL((k_sghmc_commit<T>), dim3(nDB16, C), dim3(256), 0, st, ca);
+  HMCX_HIP(ctx, hipGetLastError());
+  hipLaunchKernelGGL(k_fix_acc, dim3((unsigned)((nsc + 255) / 256)), dim3(256), 0, st, d_niter, d_u,
+                     s->out_accepted, (int)nsc);
+  HMCX_HIP(ctx, hipGetLastError());
+  if ((rc = gs.finish())) return rc;
+  return timing_end(ctx, ctx->stream);
+}
+
 template <typename T>
 int sghmc_run_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
   const int B = s->B, D = s->D, K = s->K, C = s->C, N = C * K;
@@ -691,6 +835,8 @@ int sghmc_run_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
   } else if (ctx->sghmc_path == 2) {
     return set_error(ctx, HMCX_EUNSUPPORTED, "persistent SGHMC needs C == 1");
   }
+  static const bool no_batch = getenv("HMCX_NO_BATCH") && getenv("HMCX_NO_BATCH")[0] == '1';
+  if (C >= 16 && K == BKC && D % 2 == 0 && !no_batch) return sghmc_batch_t<T>(ctx, s);   // chain-batched GEMMs
   const Tiling t = make_tiling(B, D, K, C);
   const size_t nsc = (size_t)s->n_steps * C;
   Workspace ws(ctx);
@@ -773,7 +919,7 @@ int sghmc_run_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
       HMCX_HIP(ctx, launch_grad<T>(g, t, st));
     }
     AcceptArgs<T> aa{};
-    aa.C = C; aa.nRB = t.nRB; aa.nDB = t.nDB;
+    aa.C = C; aa.nRB = t.nRB; aa.nDB = t.nDB; aa.nDB1 = t.nDB;
     aa.n_iter = niter; aa.u = d_u + (size_t)st_i * C;
     aa.neg_inv_n = -1.0 / (double)B; aa.log_prior = s->log_prior;
     aa.kin0_part = k0p; aa.kin0b = k0b; aa.kin1_part = k1p; aa.kin1b = k1b;

@@ -35,54 +35,65 @@ class sghmc(sgmcmc):
 
     # ------------------------------------------------------------------ schedule
     def _schedule(self, n_steps, eps, rng, P):
-        """Host-side randomness of n_steps steps, in the reference's draw order."""
-        n_iter = np.empty(n_steps, dtype=np.int32)
-        u = np.empty(n_steps, dtype=np.float64)
-        noise_off = np.zeros(n_steps, dtype=np.int64)
+        """Host-side randomness of n_steps steps, in the reference's draw order.  Arrays are
+        [n_steps, C] (step-major) for C = self.chains."""
+        C = self.chains
+        n_iter = np.empty((n_steps, C), dtype=np.int32)
+        u = np.empty((n_steps, C), dtype=np.float64)
+        noise_off = np.zeros((n_steps, C), dtype=np.int64)
         chunks = []
         off = 0
+        Ls = np.empty((n_steps, C))
+        if self.noise == 'philox':
+            # per-step path-length and accept uniforms of every chain, all steps in one pass
+            g = ((self.global_step + np.arange(n_steps)) & 0xFFFFFFFF)[:, None]
+            chain_ids = (self.chain + np.arange(C))[None, :]
+            uL = nat.philox_uniforms_chains(self.seed, chain_ids, g, nat.SLOT_PATH)
+            Ls[:] = np.ceil(2 * uL * self.path_length / np.asarray(eps, dtype=np.float64)[:, None])
+            if not np.all(np.isfinite(Ls)):
+                raise HmcxError("non-finite path length (step size 0?)")
+            n_iter[:] = np.maximum(0, np.ceil(Ls - 1)).astype(np.int32)
+            u[:] = nat.philox_uniforms_chains(self.seed, chain_ids, g, nat.SLOT_ACCEPT)
         for s in range(n_steps):
             e = eps[s]
             if self.noise == 'numpy':
                 # sghmc.py:21 momentum (rng) → :25 path length (global np.random) → :31 per-iteration
                 # noise rng.normal(0, 2ε) = 2ε·N(0,1) (scaled on the device) → :36 accept uniform.
+                # With C > 1 every chain replays the same streams (replicas).
                 L = np.ceil(2 * np.random.rand() * self.path_length / e)
                 ni = _n_iter(L)
                 z = rng.standard_normal(P * (1 + ni))
                 chunks.append(z)
-                noise_off[s] = off
+                noise_off[s, :] = off
                 off += z.size
-                u[s] = np.random.rand()
-            else:
-                g = (self.global_step + s) & 0xFFFFFFFF
-                uL = nat.philox_uniforms(self.seed, self.chain, g, nat.SLOT_PATH, 1)[0]
-                L = np.ceil(2 * uL * self.path_length / e)
-                ni = _n_iter(L)
-                u[s] = nat.philox_uniforms(self.seed, self.chain, g, nat.SLOT_ACCEPT, 1)[0]
-            n_iter[s] = ni
+                Ls[s, :] = L
+                n_iter[s, :] = ni
+                u[s, :] = np.random.rand()
             if self.trace is not None:
-                self.trace.append({'L': float(L), 'eps': float(e)})
+                self.trace.append({'L': float(Ls[s, 0]) if C == 1 else Ls[s].copy(), 'eps': float(e)})
         noise = np.concatenate(chunks) if chunks else None
         return n_iter, u, noise, noise_off
 
     def _run(self, state, data, rows, eps, rng, batch_size):
         Xd, Yd = data
         W, b = state['weights'], state['bias']
-        D, K = W.shape
+        C = self.chains
+        D, K = W.shape[0], W.shape[1] // C
         P = D * K + K
         n_steps = len(rows)
         n_iter, u, noise, noise_off = self._schedule(n_steps, eps, rng, P)
+        n_iter, u, noise_off = (np.ascontiguousarray(x.reshape(-1)) for x in (n_iter, u, noise_off))
         dev = self.model.device
         noise_d = torch.from_numpy(noise).to(dev) if noise is not None else None
-        out_A = torch.empty(n_steps, dtype=torch.float64, device=dev)
-        out_acc = torch.empty(n_steps, dtype=torch.int32, device=dev)
-        out_ll = torch.empty(n_steps, dtype=torch.float64, device=dev)
-        out_E = torch.empty(2 * n_steps, dtype=torch.float64, device=dev)
+        out_A = torch.empty(n_steps * C, dtype=torch.float64, device=dev)
+        out_acc = torch.empty(n_steps * C, dtype=torch.int32, device=dev)
+        out_ll = torch.empty(n_steps * C, dtype=torch.float64, device=dev)
+        out_E = torch.empty(2 * n_steps * C, dtype=torch.float64, device=dev)
         row0 = np.asarray(rows, dtype=np.int64)
         eps_a = np.asarray(eps, dtype=np.float64)
         a = nat.SamplerArgs()
         a.dtype = self.model.code
-        a.B, a.D, a.K, a.C = batch_size, D, K, 1
+        a.B, a.D, a.K, a.C = batch_size, D, K, C
         a.n_steps = n_steps
         a.alpha = self.model.alpha
         a.log_prior = self._log_prior()
@@ -100,14 +111,19 @@ class sghmc(sgmcmc):
         ctx = nat.context(dev)
         ctx.check(ctx.lib.hmcx_sghmc_run(ctx.h, a), "hmcx_sghmc_run")
         self.global_step += n_steps
-        res = RunResult(out_A.cpu().numpy(), out_acc.cpu().numpy().astype(bool), out_ll.cpu().numpy(),
-                        out_E.cpu().numpy().reshape(n_steps, 2))
+        if C == 1:
+            res = RunResult(out_A.cpu().numpy(), out_acc.cpu().numpy().astype(bool), out_ll.cpu().numpy(),
+                            out_E.cpu().numpy().reshape(n_steps, 2))
+        else:
+            res = RunResult(out_A.cpu().numpy().reshape(n_steps, C),
+                            out_acc.cpu().numpy().astype(bool).reshape(n_steps, C),
+                            out_ll.cpu().numpy().reshape(n_steps, C), out_E.cpu().numpy().reshape(n_steps, C, 2))
         del noise_d
         if self.trace is not None:
             for s in range(n_steps):
                 t = self.trace[len(self.trace) - n_steps + s]
-                t['A'] = float(res.A[s])
-                t['accepted'] = bool(res.accepted[s])
+                t['A'] = float(res.A[s]) if C == 1 else res.A[s].copy()
+                t['accepted'] = bool(res.accepted[s]) if C == 1 else res.accepted[s].copy()
         return res
 
     # ------------------------------------------------------------------ single step (API parity)
@@ -116,6 +132,8 @@ class sghmc(sgmcmc):
 
         q is a dict of device tensors.  The final momentum stays on the device (the reference
         returns it but ``sample`` discards it; draw_momentum redraws it every step)."""
+        if self.chains != 1:
+            raise HmcxError("step() is the reference's single-chain API; use sample() for chains > 1")
         X, y = args['X_train'], args['y_train']
         data = self._upload_data(X, y)
         st = {var: torch.as_tensor(np.asarray(state[var]) if not isinstance(state[var], torch.Tensor)

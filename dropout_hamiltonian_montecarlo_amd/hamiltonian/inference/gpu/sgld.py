@@ -26,11 +26,13 @@ class sgld(sgmcmc):
     def _run(self, state, data, rows, eps, rng, batch_size):
         Xd, Yd = data
         W, b = state['weights'], state['bias']
-        D, K = W.shape
+        C = self.chains
+        D, K = W.shape[0], W.shape[1] // C
         P = D * K + K
         n_steps = len(rows)
         dev = self.model.device
-        noise_off = np.arange(n_steps, dtype=np.int64) * P
+        # noise offsets [n_steps, C]; numpy mode: every chain replays the same stream (replicas)
+        noise_off = np.repeat(np.arange(n_steps, dtype=np.int64) * P, C)
         noise_d = None
         if self.noise == 'numpy':
             # sgld.py:45: rng.normal(0, 2ε, shape) per var = 2ε·N(0,1) (scaled on the device)
@@ -38,12 +40,12 @@ class sgld(sgmcmc):
         want = np.zeros(n_steps, dtype=np.uint8)
         want[::self.log_every] = 1
         want[-1] = 1
-        out_ll = torch.zeros(n_steps, dtype=torch.float64, device=dev)
+        out_ll = torch.zeros(n_steps * C, dtype=torch.float64, device=dev)
         row0 = np.asarray(rows, dtype=np.int64)
         eps_a = np.asarray(eps, dtype=np.float64)
         a = nat.SamplerArgs()
         a.dtype = self.model.code
-        a.B, a.D, a.K, a.C = batch_size, D, K, 1
+        a.B, a.D, a.K, a.C = batch_size, D, K, C
         a.n_steps = n_steps
         a.alpha = self.model.alpha
         a.log_prior = self._log_prior()
@@ -61,11 +63,15 @@ class sgld(sgmcmc):
         ctx.check(ctx.lib.hmcx_sgld_run(ctx.h, a), "hmcx_sgld_run")
         self.global_step += n_steps
         ll = out_ll.cpu().numpy()
+        if C > 1:
+            ll = ll.reshape(n_steps, C)
         if self.trace is not None:
             self.trace.extend({'L': 1.0, 'A': 1.0, 'accepted': True, 'eps': float(e)} for e in eps)
         return RunResult(np.ones(n_steps), np.ones(n_steps, dtype=bool), ll)
 
     def step(self, state, momentum, rng, **args):                         # sgld.py:31-39
+        if self.chains != 1:
+            raise HmcxError("step() is the reference's single-chain API; use sample() for chains > 1")
         X, y = args['X_train'], args['y_train']
         data = self._upload_data(X, y)
         st = {var: torch.as_tensor(np.asarray(state[var]) if not isinstance(state[var], torch.Tensor)

@@ -17,6 +17,13 @@ same streams, in the same order, as the reference (``rng`` RandomState for momen
 the global ``np.random`` for path lengths and accept uniforms), so a float64 run reproduces
 the NumPy reference's integer bookkeeping bit for bit.  ``noise='philox'`` generates all noise
 on the device (counter-based, keyed by (seed, chain, step)) — the fast mode.
+
+Several chains on one device (``chains=C``, an extension; the reference runs one chain per
+process).  The chains share every minibatch and run in one libhmcx call; with C ≥ 16 the
+gradient GEMMs are chain-batched ([B×D]·[D×10C]).  ``noise='philox'`` gives
+independent chains (Philox key chain + c); ``noise='numpy'`` drives all C chains with the SAME
+reference streams (replicas — a parity test mode).  With C > 1, ``posterior[var]`` is
+[C, epochs, *shape] and ``logp`` is [C, epochs].
 """
 import sys
 
@@ -36,7 +43,7 @@ class RunResult:
 
 class sgmcmc:
     def __init__(self, model, start_p, path_length=1.0, step_size=0.1, verbose=True,
-                 noise='numpy', seed=0, chain=0):
+                 noise='numpy', seed=0, chain=0, chains=1):
         self.start = {var: np.asarray(start_p[var]) for var in start_p.keys()}   # sgmcmc.py:17
         self.step_size = step_size
         self.path_length = path_length
@@ -47,6 +54,9 @@ class sgmcmc:
         self.noise = noise
         self.seed = int(seed)
         self.chain = int(chain)
+        self.chains = int(chains)
+        if self.chains < 1:
+            raise ValueError("chains must be >= 1")
         self.global_step = 0
         self.trace = None          # optional list: per-step dict(L, A, accepted, eps)
         self.out = sys.stdout
@@ -76,12 +86,29 @@ class sgmcmc:
         return Xd, Yd
 
     def _state_to_host(self, state):
-        return {var: state[var].detach().cpu().numpy().astype(np.float64).reshape(self.start[var].shape)
-                for var in self.start}
+        C = self.chains
+        out = {}
+        for var in self.start:
+            h = state[var].detach().cpu().numpy().astype(np.float64)
+            shape = self.start[var].shape
+            if C == 1:
+                out[var] = h.reshape(shape)
+            elif len(shape) == 2:                      # [D, C·K] chain-interleaved → [C, D, K]
+                out[var] = h.reshape(shape[0], C, shape[1]).transpose(1, 0, 2).copy()
+            else:                                      # [C·K] → [C, K]
+                out[var] = h.reshape(C, *shape)
+        return out
 
     def _init_state(self):
         dt, dev = self.model.dtype, self.model.device
-        return {var: torch.as_tensor(self.start[var]).to(dev, dt).contiguous().clone() for var in self.start}
+        C = self.chains
+        st = {}
+        for var in self.start:
+            a = self.start[var]
+            if C > 1:
+                a = np.tile(a, (1, C)) if a.ndim == 2 else np.tile(a, C)
+            st[var] = torch.as_tensor(a).to(dev, dt).contiguous().clone()
+        return st
 
     # ------------------------------------------------------------------ outer loop (sgmcmc.py:40-86)
     def sample(self, epochs=1, burnin=1, batch_size=1, rng=None, **args):
@@ -104,9 +131,9 @@ class sgmcmc:
             res = self._run(state, data, rows, eps, rng, batch_size)
             for j in range(len(rows)):
                 if (j % self.log_every) == 0:
-                    ll = -1.0 * res.ll[j]
+                    ll = -1.0 * np.ravel(res.ll[j])[0]
                     print('burnin {0}, loss: {1:.4f}, mini-batch update : {2}'.format(i, ll, j), file=self.out)
-        logp_samples = np.zeros(epochs)
+        logp_samples = np.zeros(epochs) if self.chains == 1 else np.zeros((epochs, self.chains))
         posterior = {var: [] for var in self.start.keys()}
         print('start sampling', file=self.out)
         initial_step_size = self.step_size
@@ -118,7 +145,7 @@ class sgmcmc:
             res = self._run(state, data, rows, eps, rng, batch_size)
             for j in range(len(rows)):
                 if (j % self.log_every) == 0:
-                    ll = -1.0 * res.ll[j]
+                    ll = -1.0 * np.ravel(res.ll[j])[0]
                     print('epoch {0}, loss: {1:.4f}, mini-batch update : {2}'.format(i, ll, j), file=self.out)
             # sgmcmc.py:79 — negative_log_posterior(q, last minibatch) from the device log-likelihood
             logp_samples[i] = (-1.0 / batch_size) * (res.ll[-1] + self._log_prior())
@@ -126,9 +153,13 @@ class sgmcmc:
             for var in self.start.keys():
                 posterior[var].append(host[var])
             if self.verbose and (i % (epochs / 10) == 0):
-                print('loss: {0:.4f}'.format(logp_samples[i]), file=self.out)
+                print('loss: {0:.4f}'.format(np.ravel(logp_samples[i])[0]), file=self.out)
         for var in self.start.keys():
             posterior[var] = np.array(posterior[var])
+            if self.chains > 1:
+                posterior[var] = np.moveaxis(posterior[var], 1, 0)     # [C, epochs, *shape]
+        if self.chains > 1:
+            logp_samples = logp_samples.T.copy()
         self.last_state = state
         return posterior, logp_samples
 

@@ -1,0 +1,94 @@
+"""Several chains on one GPU (``chains=C``): the chain-batched GEMM path (C >= 16, K = 10,
+hmcx_batch.h) and the kernel-per-phase path (C < 16) against the NumPy oracle.
+
+Replica mode (noise='numpy' with C chains) drives every chain with the reference's own streams, so
+every chain must reproduce the oracle's single-chain trajectory: bit-exact path lengths and accept
+flags, float64 states within rel 1e-9.  Philox mode checks that chain c of a batched run equals
+the single-chain run keyed by chain c."""
+import io
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from oracle import inputs as gi  # noqa: E402
+
+from test_gpu_samplers import _run_oracle  # noqa: E402
+
+
+def _classes():
+    from dropout_hamiltonian_montecarlo_amd.hamiltonian.models.gpu.softmax import softmax
+    from dropout_hamiltonian_montecarlo_amd.hamiltonian.inference.gpu.sghmc import sghmc
+    from dropout_hamiltonian_montecarlo_amd.hamiltonian.inference.gpu.sgld import sgld
+    return softmax, sghmc, sgld
+
+
+def _run_chains(c, chains, dtype=torch.float64, noise="numpy", seed=0, chain=0, path=0):
+    softmax, sghmc, sgld = _classes()
+    X, Y = gi.dataset(c["data_seed"], c["N"], c["D"], c["K"])
+    cls = sghmc if c["kind"] == "sghmc" else sgld
+    m = softmax({"alpha": c["alpha"]}, dtype=dtype, device="cuda:0")
+    m.ctx.set_sghmc_path(path)
+    s = cls(m, {"weights": np.zeros((c["D"], c["K"])), "bias": np.zeros(c["K"])},
+            path_length=c["path_length"], step_size=c["step_size"], verbose=True, noise=noise, seed=seed,
+            chain=chain, chains=chains)
+    s.trace = []
+    s.out = io.StringIO()
+    np.random.seed(c["np_seed"])
+    post, logp = s.sample(epochs=c["epochs"], burnin=c["burnin"], batch_size=c["B"],
+                          rng=np.random.RandomState(c["rng_seed"]), X_train=X, y_train=Y)
+    return post, logp, s.trace
+
+
+@pytest.mark.parametrize("name,chains", [("sghmc_small", 16), ("sghmc_small", 4), ("sghmc_mnist", 16), ("sghmc_small", 512),
+                                         ("sghmc_hot", 32), ("sgld_small", 16)])
+def test_replica_chains_match_oracle(name, chains):
+    c = gi.TRAJ_CONFIGS[name]
+    post_r, logp_r, tr_r, _ = _run_oracle(c)
+    post_g, logp_g, tr_g = _run_chains(c, chains)
+    assert post_g["weights"].shape == (chains, c["epochs"], c["D"], c["K"])
+    assert logp_g.shape == (chains, c["epochs"])
+    if c["kind"] == "sghmc":
+        for t_g, t_r in zip(tr_g, tr_r):
+            assert np.all(t_g["L"] == t_r["L"])
+            assert np.all(t_g["accepted"] == t_r["accepted"])
+    for ch in range(chains):
+        for v in ("weights", "bias"):
+            np.testing.assert_allclose(post_g[v][ch], post_r[v], rtol=1e-9, atol=1e-12)
+        np.testing.assert_allclose(logp_g[ch], logp_r, rtol=1e-10)
+
+
+def test_batched_chains_equal_single_chain_runs():
+    """Philox noise: chain c of a 16-chain batched run == the single-chain run with chain=c."""
+    c = dict(gi.TRAJ_CONFIGS["sghmc_small"])
+    post_b, logp_b, tr_b = _run_chains(c, 16, noise="philox", seed=11, chain=3)
+    for ch in (0, 5, 15):
+        post_1, logp_1, tr_1 = _run_chains(c, 1, noise="philox", seed=11, chain=3 + ch, path=1)
+        assert [t["L"] for t in tr_1] == [float(t["L"][ch]) for t in tr_b]
+        assert [t["accepted"] for t in tr_1] == [bool(t["accepted"][ch]) for t in tr_b]
+        for v in ("weights", "bias"):
+            np.testing.assert_allclose(post_b[v][ch], post_1[v], rtol=1e-9, atol=1e-12)
+        np.testing.assert_allclose(logp_b[ch], logp_1, rtol=1e-10)
+
+
+def test_batched_chains_mnist_philox_properties():
+    """MNIST shape, 64 independent chains: finite, distinct chains, deterministic under a seed."""
+    c = dict(gi.TRAJ_CONFIGS["sghmc_mnist"])
+    p1, l1, t1 = _run_chains(c, 64, noise="philox", seed=5)
+    p2, l2, t2 = _run_chains(c, 64, noise="philox", seed=5)
+    assert np.all(np.isfinite(p1["weights"])) and np.all(np.isfinite(l1))
+    np.testing.assert_array_equal(p1["weights"], p2["weights"])
+    np.testing.assert_array_equal(l1, l2)
+    assert np.std(p1["weights"][:, -1].reshape(64, -1), axis=0).max() > 0      # chains differ
+    acc = np.mean([np.mean(t["accepted"]) for t in t1])
+    assert 0.05 < acc <= 1.0
+
+
+def test_batched_chains_f32_close_to_f64():
+    c = dict(gi.TRAJ_CONFIGS["sghmc_small"])
+    p64, l64, _ = _run_chains(c, 16, noise="philox", seed=2)
+    p32, l32, _ = _run_chains(c, 16, dtype=torch.float32, noise="philox", seed=2)
+    np.testing.assert_allclose(l32, l64, rtol=1e-4)
