@@ -159,6 +159,8 @@ def main():
     rank, world, local = parallel.init()
     if world != args.gpus and rank == 0:
         print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, world), file=sys.stderr)
+    if os.environ.get("HMCX_BENCH_SHARED_GPU") == "1":      # rehearsal: several ranks on one GPU (gloo)
+        local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     from dropout_hamiltonian_montecarlo_amd.hamiltonian.models.gpu.softmax import softmax
@@ -260,7 +262,7 @@ def main():
                      else "kernel-per-phase sequence of one %d-step call" % CHUNK,
                      "launch_ms": launch_ms, "flop_per_launch": flop_per_launch},
         "diagnostics": {"rhat_ll": float(np.ravel(diag["rhat"])[0]), "ess_ll": float(np.ravel(diag["ess"])[0]),
-                        "gather": "torch.distributed all_gather (%s)" % ("nccl/RCCL" if world > 1 else "local")},
+                        "gather": "torch.distributed all_gather (%s)" % (parallel.backend_name() if world > 1 else "local")},
         "cpu_baseline": None,
         "chain_batched": batched,
     }

@@ -21,19 +21,27 @@ from . import diagnostics
 
 
 def init(backend=None):
-    """Initialise the process group from the environment; returns (rank, world, local_rank)."""
+    """Initialise the process group from the environment; returns (rank, world, local_rank).
+    Backend: `backend`, else $HMCX_DIST_BACKEND, else "nccl" (RCCL) with a GPU and "gloo" without."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
     if world > 1 and not dist.is_initialized():
         if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
+            backend = os.environ.get("HMCX_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         if backend == "nccl":
             torch.cuda.set_device(local)
             dist.init_process_group(backend, device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
     return rank, world, local
+
+
+def backend_name():
+    if not dist.is_initialized():
+        return "none"
+    b = dist.get_backend()
+    return "nccl (RCCL over xGMI)" if b == "nccl" else b
 
 
 def chains_of_rank(n_chains, rank, world):
@@ -46,10 +54,17 @@ def barrier():
         dist.barrier()
 
 
+def _dev(device):
+    """Collectives run on `device` with RCCL; gloo takes host tensors."""
+    if dist.is_initialized() and dist.get_backend() == "gloo":
+        return torch.device("cpu")
+    return device
+
+
 def allreduce_max(x, device=None):
     if not dist.is_initialized():
         return float(x)
-    t = torch.tensor([float(x)], dtype=torch.float64, device=device)
+    t = torch.tensor([float(x)], dtype=torch.float64, device=_dev(device))
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -57,7 +72,7 @@ def allreduce_max(x, device=None):
 def allreduce_sum(x, device=None):
     if not dist.is_initialized():
         return float(x)
-    t = torch.tensor([float(x)], dtype=torch.float64, device=device)
+    t = torch.tensor([float(x)], dtype=torch.float64, device=_dev(device))
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return float(t.item())
 
@@ -68,6 +83,7 @@ def gather_traces(local_traces, device=None):
     x = torch.as_tensor(np.ascontiguousarray(local_traces), dtype=torch.float64)
     if not dist.is_initialized():
         return x.numpy()
+    device = _dev(device)
     x = x.to(device) if device is not None else x
     out = [torch.empty_like(x) for _ in range(dist.get_world_size())]
     dist.all_gather(out, x)
