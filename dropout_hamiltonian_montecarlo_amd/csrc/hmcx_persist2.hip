@@ -35,12 +35,16 @@
 #include "hmcx_persist.h"
 #include <cstdio>
 #include <cstdlib>
+#include <vector>
 
 namespace hmcx {
 
 constexpr int QTH = 256;                 // threads per workgroup (4 waves)
 constexpr int QNW = QTH / 64;
 constexpr int QNPM = 16;                 // largest team (producers per gather)
+#ifndef HMCX_P2_SLEEP
+#define HMCX_P2_SLEEP 1
+#endif
 constexpr unsigned long long QTIMEOUT = 400000000ull;   // s_memrealtime ticks (100 MHz): 4 s
 
 typedef unsigned int gran_t __attribute__((ext_vector_type(4)));
@@ -60,7 +64,9 @@ struct Q2Args {
   int* abort_flag;                          // inside the arena
   double* out_A; int32_t* out_acc; double* out_ll; double* out_E;
   unsigned long long* prof;                 // HMCX_PERSIST_PROF=1: per-segment s_memtime totals (workgroup 0)
+  unsigned long long* trace;                // HMCX_P2_TRACE=1: [G][P2TR_IT][8] s_memrealtime stamps (step 0)
 };
+constexpr int P2TR_IT = 16;                 // traced leapfrog iterations
 
 // Segment profiler (workgroup 0, thread 0): s_memtime deltas accumulate in LDS (a global
 // read-modify-write per stamp would add a memory round trip to the critical path); flushed once.
@@ -133,7 +139,7 @@ __device__ inline bool poll_nb(__amdgpu_buffer_rsrc_t rs, int base0, int pstride
       __hip_atomic_store(abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return false;
     }
-    __builtin_amdgcn_s_sleep(1);
+    if (HMCX_P2_SLEEP) __builtin_amdgcn_s_sleep(1);
   }
   if (!valid) return true;
   if (SUM) {
@@ -352,6 +358,11 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
   if (own) wv = Wf[wl];
 
   P2Prof prof{(bid == 0 && tid == 0) ? a.prof : nullptr, profacc, 0ull, 0};
+  // round trace: slot 2·round = payload published, 2·round + 1 = consumed (rounds A, D, B, W)
+  unsigned long long* trb = a.trace ? a.trace + (size_t)bid * P2TR_IT * 8 : nullptr;
+  auto tstamp = [&](int s_, int it_, int slot) {
+    if (trb && tid == 0 && s_ == 0 && it_ >= 0 && it_ < P2TR_IT) trb[it_ * 8 + slot] = __builtin_amdgcn_s_memrealtime();
+  };
   unsigned ep = 0;                                    // round epoch (same sequence in every workgroup)
   unsigned uA = 0, uD = 0, uB = 0, uW = 0, uS = 0;    // per-region use counters (buffer parity)
 
@@ -482,6 +493,7 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
       // ===== A-RS: partial logits → owners of the row slices
       prof.stamp(1);
       roundA();
+      tstamp(s, it, 0);
       prof.stamp(2);
       // friction noise of this iteration (sghmc.py:31), generated while the partials travel
       T zb = T(0);
@@ -497,6 +509,7 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
       }
       prof.stamp(3);
       if (!consumeA()) return;
+      tstamp(s, it, 1);
       prof.stamp(4);
 
       // ===== softmaxes of my rows: diff at b (weights sub-step), y − ŷ' at b' (bias sub-step)
@@ -533,21 +546,22 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
       {
         ++ep;
         const int reg = a.oXD + (((int)(uD & 1) * Gr + r) * Gf + f) * NXA;
-        if (tid < NXA) {
+        for (int t = tid; t < NXA; t += QTH) {
           double v;
-          if (tid < KC) {
+          if (t < KC) {
             T c = T(0);
-            for (int ii = 0; ii < nro; ++ii) c += Csr[ii * 16 + tid];
+            for (int ii = 0; ii < nro; ++ii) c += Csr[ii * 16 + t];
             v = (double)c;
-          } else if (tid == KC) {
+          } else if (t == KC) {
             v = 0.0;
             if (last) for (int ii = 0; ii < nro; ++ii) v += rowll[ii];
           } else {
-            const int m = tid - HA;
+            const int m = t - HA;
             v = (double)Dme[(m / KC) * 16 + (m % KC)];
           }
-          put(rs, reg + tid, v, ep);
+          put(rs, reg + t, v, ep);
         }
+        tstamp(s, it, 2);
         const int base0 = a.oXD + ((int)(uD & 1) * Gr + r) * Gf * NXA;
         ++uD;
         bool ok;
@@ -559,6 +573,7 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
                            Ds + (m / KC) * 16 + (m % KC), Ro * 16);
         }
         if (!all_ok(ok, ish)) return;
+        tstamp(s, it, 3);
       }
 
       // ===== B-RS: partial gradient X[R_r,F_f]ᵀ·diff → owners of the feature slices
@@ -594,6 +609,7 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
         }
         const int base0 = a.oXB + ((int)(uB & 1) * Gf + f) * Gr * NXB;
         ++uB;
+        tstamp(s, it, 4);
         prof.stamp(7);
         // threads [0, nfo·KC): owned gradient element; threads [nfo·KC, nfo·KC + HA): header
         const int ng = nfo * KC;
@@ -603,6 +619,7 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
         const bool ok = poll<true>(rs, base0, NXB, Gr, -1, offB, isg || ish_, ep, nullptr, 0, &sum, a.abort_flag);
         if (ish_) hdr[tid - ng] = sum;
         if (!all_ok(ok, ish)) return;
+        tstamp(s, it, 5);
         prof.stamp(8);
         // owned weight: gradient (softmax.py:57-58), momentum (sghmc.py:31,34), drift (:32)
         if (own) {
@@ -627,6 +644,7 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
         const int per = Fo * KC;
         const int reg = a.oXW + (((int)(uW & 1) * Gf + f) * Gr + r) * per;
         if (tid < nfo * KC) put(rs, reg + tid, own ? (double)wv : 0.0, ep);
+        tstamp(s, it, 6);
         if (own) Wf[wl] = wv;
         const int base0 = a.oXW + ((int)(uW & 1) * Gf + f) * Gr * per;
         ++uW;
@@ -635,6 +653,7 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
         const bool ok = poll<false>(rs, base0, per, npd, r, tid, tid < per, ep, nullptr, 0, nullptr, a.abort_flag,
                                     Wf + dloc * 16 + kk, Fo * 16);
         if (!all_ok(ok, ish)) return;
+        tstamp(s, it, 7);
       }
     }
 
@@ -805,6 +824,14 @@ int sghmc_p2_t(hmcx_ctx* ctx, const hmcx_sampler_args* s, const PersistPlan2& pl
     HMCX_HIP(ctx, hipMemsetAsync(dprof, 0, 16 * sizeof(unsigned long long), ctx->stream));
   }
   a.prof = dprof;
+  static const bool trace_on = getenv("HMCX_P2_TRACE") && getenv("HMCX_P2_TRACE")[0] == '1';
+  unsigned long long* dtrace = nullptr;
+  const size_t ntr = (size_t)G * P2TR_IT * 8;
+  if (trace_on) {
+    HMCX_HIP(ctx, hipMalloc((void**)&dtrace, ntr * sizeof(unsigned long long)));
+    HMCX_HIP(ctx, hipMemsetAsync(dtrace, 0, ntr * sizeof(unsigned long long), ctx->stream));
+  }
+  a.trace = dtrace;
   const void* kfn = KC == 10 ? (const void*)k_sghmc_p2<T, 10> : (const void*)k_sghmc_p2<T, 16>;
   HMCX_HIP(ctx, hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.lds));
   void* kargs[] = {&a};
@@ -833,6 +860,44 @@ int sghmc_p2_t(hmcx_ctx* ctx, const hmcx_sampler_args* s, const PersistPlan2& pl
             pl.Ro, pl.Fo, tot);
     for (int i = 0; i < 12; ++i) fprintf(stderr, " %s %.1f%%", names[i], tot ? 100.0 * h[i] / tot : 0.0);
     fprintf(stderr, "\n");
+  }
+  if (dtrace) {
+    std::vector<unsigned long long> h(ntr);
+    HMCX_HIP(ctx, hipMemcpy(h.data(), dtrace, ntr * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    (void)hipFree(dtrace);
+    // per round: latency = consumed(b) − last publish of b's team; skew = last team publish − publish(b)
+    static const char* rn[4] = {"A-RS", "A-AG", "B-RS", "B-AG"};
+    for (int rd = 0; rd < 4; ++rd) {
+      double lat = 0, skew = 0, lmax = 0;
+      long cnt = 0;
+      for (int it = 1; it < P2TR_IT; ++it)
+        for (int b = 0; b < G; ++b) {
+          const int r = b / pl.Gf, f = b % pl.Gf;
+          const unsigned long long pub = h[((size_t)b * P2TR_IT + it) * 8 + 2 * rd];
+          const unsigned long long done = h[((size_t)b * P2TR_IT + it) * 8 + 2 * rd + 1];
+          if (!pub || !done) continue;
+          unsigned long long mx = 0;
+          const bool rowteam = rd < 2;
+          const int nm = rowteam ? pl.Gf : pl.Gr;
+          bool okm = true;
+          for (int m = 0; m < nm; ++m) {
+            const int pb = rowteam ? r * pl.Gf + m : m * pl.Gf + f;
+            const unsigned long long v = h[((size_t)pb * P2TR_IT + it) * 8 + 2 * rd];
+            if (!v) okm = false;
+            mx = v > mx ? v : mx;
+          }
+          if (!okm) continue;
+          const double l = (double)(long long)(done - mx) * 10.0 / 1000.0;   // µs (100 MHz ticks)
+          lat += l; lmax = l > lmax ? l : lmax;
+          skew += (double)(long long)(mx - pub) * 10.0 / 1000.0;
+          ++cnt;
+        }
+      if (cnt) fprintf(stderr, "[hmcx p2 trace] %s: latency after last team publish %.2f us (max %.2f), own wait for "
+                       "slowest member %.2f us (n=%ld)\n", rn[rd], lat / cnt, lmax, skew / cnt, cnt);
+    }
+    // iteration period from block 0
+    const unsigned long long t1 = h[1 * 8 + 0], t2 = h[(P2TR_IT - 1) * 8 + 0];
+    if (t1 && t2) fprintf(stderr, "[hmcx p2 trace] leapfrog period %.2f us\n", (double)(t2 - t1) * 10.0 / 1000.0 / (P2TR_IT - 2));
   }
   if (flag) return set_error(ctx, HMCX_EHIP, "persistent SGHMC: hand-off timed out (workgroups not co-resident?)");
   return HMCX_OK;
