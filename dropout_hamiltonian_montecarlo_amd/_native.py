@@ -45,12 +45,32 @@ class MvnArgs(ctypes.Structure):
                 ("out_trace", c_void_p)]
 
 
+class MlpParams(ctypes.Structure):
+    _fields_ = [("p", c_void_p * 6)]
+
+
+class MlpSghmcArgs(ctypes.Structure):
+    _fields_ = [("dtype", c_int), ("B", c_int), ("n_in", c_int), ("n_mid", c_int), ("n_out", c_int),
+                ("n_steps", c_int), ("order", c_int * 6), ("alpha", c_double),
+                ("X", c_void_p), ("y", c_void_p), ("row0", c_i64p), ("eps", c_dblp),
+                ("n_iter", c_i32p), ("u_accept", c_dblp),
+                ("noise_mode", c_int), ("noise", c_void_p), ("noise_off", c_i64p),
+                ("mask_mode", c_int), ("masks", c_void_p), ("mask_off", c_i64p),
+                ("seed", ctypes.c_uint64), ("chain", ctypes.c_uint32), ("step_base", ctypes.c_uint32),
+                ("par", MlpParams), ("out_A", c_void_p), ("out_accepted", c_void_p),
+                ("out_loss", c_void_p), ("out_nlp", c_void_p), ("out_E", c_void_p)]
+
+
+MLP_MASK_SLOT0 = 0x80000000
+
+
 # Every symbol include/hmcx.h declares (checked by tests/test_capi.py).
 EXPORTS = ("hmcx_version", "hmcx_create", "hmcx_destroy", "hmcx_last_error", "hmcx_set_stream",
            "hmcx_synchronize", "hmcx_set_graph_mode", "hmcx_set_sghmc_path", "hmcx_set_timing", "hmcx_get_timing",
            "hmcx_philox_uniforms", "hmcx_philox_normals",
            "hmcx_softmax_grad", "hmcx_softmax_loglik", "hmcx_softmax_predict", "hmcx_sghmc_run",
-           "hmcx_sgld_run", "hmcx_hmc_mvn_run")
+           "hmcx_sgld_run", "hmcx_hmc_mvn_run", "hmcx_mlp_masks", "hmcx_mlp_grad", "hmcx_mlp_loss",
+           "hmcx_mlp_sghmc_run")
 
 _lib = None
 _lock = threading.Lock()
@@ -96,6 +116,14 @@ def load_library():
         lib.hmcx_sghmc_run.argtypes = [c_void_p, ctypes.POINTER(SamplerArgs)]
         lib.hmcx_sgld_run.argtypes = [c_void_p, ctypes.POINTER(SamplerArgs)]
         lib.hmcx_hmc_mvn_run.argtypes = [c_void_p, ctypes.POINTER(MvnArgs)]
+        u32, u64 = ctypes.c_uint32, ctypes.c_uint64
+        lib.hmcx_mlp_masks.argtypes = [c_void_p, c_int, c_int, c_int, u64, u32, u32, u32, c_void_p]
+        lib.hmcx_mlp_grad.argtypes = [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                                      ctypes.POINTER(MlpParams), c_void_p, c_double, ctypes.POINTER(MlpParams),
+                                      c_void_p]
+        lib.hmcx_mlp_loss.argtypes = [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                                      ctypes.POINTER(MlpParams), c_void_p, c_void_p, c_void_p]
+        lib.hmcx_mlp_sghmc_run.argtypes = [c_void_p, ctypes.POINTER(MlpSghmcArgs)]
         _lib = lib
         return lib
 

@@ -446,4 +446,73 @@ int hmcx_hmc_mvn_run(hmcx_ctx* ctx, const hmcx_hmc_mvn_args* a) {
   return hmc_mvn_run(ctx, a);
 }
 
+static int check_mlp(hmcx_ctx* ctx, int dtype, int B, int n_in, int n_mid, int n_out) {
+  if (dtype != HMCX_F32 && dtype != HMCX_F64) return set_error(ctx, HMCX_EINVAL, "dtype must be HMCX_F32/HMCX_F64");
+  if (B < 1 || n_in < 1 || n_mid < 1 || n_out < 1) return set_error(ctx, HMCX_EINVAL, "mlp: sizes must be >= 1");
+  if ((long long)B * n_mid * 3 > 0x7fffffffLL || (long long)n_mid * n_in > 0x7fffffffLL ||
+      (long long)n_mid * n_mid > 0x7fffffffLL)
+    return set_error(ctx, HMCX_EUNSUPPORTED, "mlp: layer too large");
+  return HMCX_OK;
+}
+
+static bool mlp_par_ok(const hmcx_mlp_params* p) {
+  if (!p) return false;
+  for (int v = 0; v < 6; ++v)
+    if (!p->p[v]) return false;
+  return true;
+}
+
+int hmcx_mlp_masks(hmcx_ctx* ctx, int dtype, int B, int n_mid, uint64_t seed, uint32_t chain, uint32_t step,
+                   uint32_t slot, void* out) {
+  HMCX_GUARD_CTX(ctx);
+  int rc = check_mlp(ctx, dtype, B, 1, n_mid, 1);
+  if (rc) return rc;
+  if (!out) return set_error(ctx, HMCX_EINVAL, "null pointer");
+  return dtype == HMCX_F64 ? mlp_masks_t<double>(ctx, B, n_mid, seed, chain, step, slot, out)
+                           : mlp_masks_t<float>(ctx, B, n_mid, seed, chain, step, slot, out);
+}
+
+int hmcx_mlp_grad(hmcx_ctx* ctx, int dtype, const void* X, const int32_t* y, int B, int n_in, int n_mid, int n_out,
+                  const hmcx_mlp_params* par, const void* masks, double alpha, hmcx_mlp_params* grads,
+                  double* loss) {
+  HMCX_GUARD_CTX(ctx);
+  int rc = check_mlp(ctx, dtype, B, n_in, n_mid, n_out);
+  if (rc) return rc;
+  if (!X || !y || !mlp_par_ok(par) || !mlp_par_ok(grads)) return set_error(ctx, HMCX_EINVAL, "null pointer");
+  return dtype == HMCX_F64 ? mlp_grad_t<double>(ctx, X, y, B, n_in, n_mid, n_out, par, masks, alpha, grads, loss)
+                           : mlp_grad_t<float>(ctx, X, y, B, n_in, n_mid, n_out, par, masks, alpha, grads, loss);
+}
+
+int hmcx_mlp_loss(hmcx_ctx* ctx, int dtype, const void* X, const int32_t* y, int B, int n_in, int n_mid, int n_out,
+                  const hmcx_mlp_params* par, const void* masks, double* loss, void* logits) {
+  HMCX_GUARD_CTX(ctx);
+  int rc = check_mlp(ctx, dtype, B, n_in, n_mid, n_out);
+  if (rc) return rc;
+  if (!X || !mlp_par_ok(par)) return set_error(ctx, HMCX_EINVAL, "null pointer");
+  if (!y && !logits) return set_error(ctx, HMCX_EINVAL, "mlp_loss: need labels or a logits output");
+  return dtype == HMCX_F64 ? mlp_loss_t<double>(ctx, X, y, B, n_in, n_mid, n_out, par, masks, loss, logits)
+                           : mlp_loss_t<float>(ctx, X, y, B, n_in, n_mid, n_out, par, masks, loss, logits);
+}
+
+int hmcx_mlp_sghmc_run(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* a) {
+  HMCX_GUARD_CTX(ctx);
+  if (!a) return set_error(ctx, HMCX_EINVAL, "null args");
+  int rc = check_mlp(ctx, a->dtype, a->B, a->n_in, a->n_mid, a->n_out);
+  if (rc) return rc;
+  if (a->n_steps < 0) return set_error(ctx, HMCX_EINVAL, "n_steps < 0");
+  if (!a->X || !a->y || !a->row0 || !a->eps || !a->n_iter || !a->u_accept || !mlp_par_ok(&a->par) || !a->out_A ||
+      !a->out_accepted || !a->out_loss)
+    return set_error(ctx, HMCX_EINVAL, "mlp sghmc: null pointer");
+  if (a->noise_mode != HMCX_NOISE_BUFFER && a->noise_mode != HMCX_NOISE_PHILOX)
+    return set_error(ctx, HMCX_EINVAL, "bad noise_mode");
+  if (a->mask_mode != HMCX_NOISE_BUFFER && a->mask_mode != HMCX_NOISE_PHILOX)
+    return set_error(ctx, HMCX_EINVAL, "bad mask_mode");
+  if (a->noise_mode == HMCX_NOISE_BUFFER && (!a->noise || !a->noise_off))
+    return set_error(ctx, HMCX_EINVAL, "BUFFER noise mode needs noise and noise_off");
+  if (a->mask_mode == HMCX_NOISE_BUFFER && (!a->masks || !a->mask_off))
+    return set_error(ctx, HMCX_EINVAL, "BUFFER mask mode needs masks and mask_off");
+  if (a->n_steps == 0) return HMCX_OK;
+  return a->dtype == HMCX_F64 ? mlp_sghmc_t<double>(ctx, a) : mlp_sghmc_t<float>(ctx, a);
+}
+
 }  // extern "C"

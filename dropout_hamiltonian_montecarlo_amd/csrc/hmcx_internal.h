@@ -160,5 +160,11 @@ template <typename T> int softmax_predict_t(hmcx_ctx*, const void*, int, int, in
 template <typename T> int sghmc_run_t(hmcx_ctx*, const hmcx_sampler_args*);
 template <typename T> int sgld_run_t(hmcx_ctx*, const hmcx_sampler_args*);
 int hmc_mvn_run(hmcx_ctx*, const hmcx_hmc_mvn_args*);
+template <typename T> int mlp_grad_t(hmcx_ctx*, const void*, const int32_t*, int, int, int, int,
+                                     const hmcx_mlp_params*, const void*, double, hmcx_mlp_params*, double*);
+template <typename T> int mlp_loss_t(hmcx_ctx*, const void*, const int32_t*, int, int, int, int,
+                                     const hmcx_mlp_params*, const void*, double*, void*);
+template <typename T> int mlp_sghmc_t(hmcx_ctx*, const hmcx_mlp_sghmc_args*);
+template <typename T> int mlp_masks_t(hmcx_ctx*, int, int, uint64_t, uint32_t, uint32_t, uint32_t, void*);
 
 }  // namespace hmcx

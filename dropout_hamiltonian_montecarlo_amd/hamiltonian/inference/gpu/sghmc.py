@@ -28,7 +28,17 @@ def _n_iter(path_length):
 
 class sghmc(sgmcmc):
 
+    mask_provider = None    # MLP parity hook: f(global_step, n_forwards) -> [n_fwd, 3, B, n_mid] masks
+
     def _check_vars(self):
+        if self.model._hmcx_model == 'mlp':
+            from dropout_hamiltonian_montecarlo_amd.hamiltonian.models.gpu.mlp import MLP_PARAM_NAMES
+            if sorted(self.start.keys()) != sorted(MLP_PARAM_NAMES):
+                raise HmcxError("sghmc(mlp): start_p must hold exactly %s" % (MLP_PARAM_NAMES,))
+            if self.chains != 1:
+                raise HmcxError("sghmc(mlp): one chain per sampler (chains=1)")
+            self._order = [MLP_PARAM_NAMES.index(k) for k in self.start.keys()]
+            return
         if self.model._hmcx_model != 'softmax' or list(self.start.keys()) != ['weights', 'bias']:
             raise HmcxError("sghmc: libhmcx implements the softmax model with start_p keys "
                             "['weights', 'bias'] (in that order, sghmc.py:29)")
@@ -75,6 +85,8 @@ class sghmc(sgmcmc):
         return n_iter, u, noise, noise_off
 
     def _run(self, state, data, rows, eps, rng, batch_size):
+        if self.model._hmcx_model == 'mlp':
+            return self._run_mlp(state, data, rows, eps, rng, batch_size)
         Xd, Yd = data
         W, b = state['weights'], state['bias']
         C = self.chains
@@ -124,6 +136,68 @@ class sghmc(sgmcmc):
                 t = self.trace[len(self.trace) - n_steps + s]
                 t['A'] = float(res.A[s]) if C == 1 else res.A[s].copy()
                 t['accepted'] = bool(res.accepted[s]) if C == 1 else res.accepted[s].copy()
+        return res
+
+    def _run_mlp(self, state, data, rows, eps, rng, batch_size):
+        """MLP steps through hmcx_mlp_sghmc_run (hmcx_mlp.hip): same schedule and noise layout as the
+        softmax path; dropout masks from Philox on the device, or from ``mask_provider`` (parity)."""
+        from dropout_hamiltonian_montecarlo_amd.hamiltonian.models.gpu.mlp import MLP_PARAM_NAMES
+        m = self.model
+        Xd, yd = data
+        P = sum(int(np.prod(self.start[k].shape)) for k in self.start)
+        n_steps = len(rows)
+        n_iter, u, noise, noise_off = self._schedule(n_steps, eps, rng, P)
+        n_iter, u, noise_off = (np.ascontiguousarray(x.reshape(-1)) for x in (n_iter, u, noise_off))
+        dev = m.device
+        noise_d = torch.from_numpy(noise).to(dev) if noise is not None else None
+        masks_d, mask_off = None, np.zeros(n_steps, dtype=np.int64)
+        if self.mask_provider is not None:
+            chunks, off = [], 0
+            for s in range(n_steps):
+                mk = np.asarray(self.mask_provider(self.global_step + s, 6 * int(n_iter[s]) + 2))
+                chunks.append(mk.reshape(-1))
+                mask_off[s] = off
+                off += chunks[-1].size
+            masks_d = torch.from_numpy(np.concatenate(chunks)).to(dev, m.dtype)
+        outs = {k: torch.empty(n_steps * w, dtype=torch.float64, device=dev)
+                for k, w in (('A', 1), ('loss', 1), ('nlp', 1), ('E', 2))}
+        out_acc = torch.empty(n_steps, dtype=torch.int32, device=dev)
+        row0 = np.asarray(rows, dtype=np.int64)
+        eps_a = np.asarray(eps, dtype=np.float64)
+        a = nat.MlpSghmcArgs()
+        a.dtype = m.code
+        a.B, a.n_in, a.n_mid, a.n_out, a.n_steps = batch_size, m.n_in, m.n_mid, m.n_out, n_steps
+        for i, v in enumerate(self._order):
+            a.order[i] = v
+        a.alpha = m.alpha
+        a.X, a.y = ptr(Xd), ptr(yd)
+        a.row0 = row0.ctypes.data_as(nat.c_i64p)
+        a.eps = eps_a.ctypes.data_as(nat.c_dblp)
+        a.n_iter = n_iter.ctypes.data_as(nat.c_i32p)
+        a.u_accept = u.ctypes.data_as(nat.c_dblp)
+        a.noise_mode = nat.NOISE_BUFFER if self.noise == 'numpy' else nat.NOISE_PHILOX
+        a.noise = ptr(noise_d)
+        a.noise_off = noise_off.ctypes.data_as(nat.c_i64p)
+        a.mask_mode = nat.NOISE_BUFFER if masks_d is not None else nat.NOISE_PHILOX
+        a.masks = ptr(masks_d)
+        a.mask_off = mask_off.ctypes.data_as(nat.c_i64p)
+        a.seed, a.chain, a.step_base = self.seed, self.chain, self.global_step & 0xFFFFFFFF
+        for i, k in enumerate(MLP_PARAM_NAMES):
+            a.par.p[i] = state[k].data_ptr()
+        a.out_A, a.out_accepted = ptr(outs['A']), ptr(out_acc)
+        a.out_loss, a.out_nlp, a.out_E = ptr(outs['loss']), ptr(outs['nlp']), ptr(outs['E'])
+        ctx = nat.context(dev)
+        ctx.check(ctx.lib.hmcx_mlp_sghmc_run(ctx.h, a), "hmcx_mlp_sghmc_run")
+        self.global_step += n_steps
+        h = {k: v.cpu().numpy() for k, v in outs.items()}
+        res = RunResult(h['A'], out_acc.cpu().numpy().astype(bool), h['loss'], h['E'].reshape(n_steps, 2),
+                        nlp=h['nlp'])
+        del noise_d, masks_d
+        if self.trace is not None:
+            for s in range(n_steps):
+                t = self.trace[len(self.trace) - n_steps + s]
+                t['A'] = float(res.A[s])
+                t['accepted'] = bool(res.accepted[s])
         return res
 
     # ------------------------------------------------------------------ single step (API parity)

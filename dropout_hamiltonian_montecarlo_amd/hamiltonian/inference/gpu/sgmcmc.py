@@ -37,8 +37,8 @@ from dropout_hamiltonian_montecarlo_amd._native import HmcxError, ptr
 class RunResult:
     """Per-step outputs of one libhmcx run call (host numpy arrays)."""
 
-    def __init__(self, A, accepted, ll, E=None):
-        self.A, self.accepted, self.ll, self.E = A, accepted, ll, E
+    def __init__(self, A, accepted, ll, E=None, nlp=None):
+        self.A, self.accepted, self.ll, self.E, self.nlp = A, accepted, ll, E, nlp
 
 
 class sgmcmc:
@@ -82,6 +82,8 @@ class sgmcmc:
     def _upload_data(self, X, y):
         dt, dev = self.model.dtype, self.model.device
         Xd = torch.as_tensor(np.asarray(X) if not isinstance(X, torch.Tensor) else X).to(dev, dt).contiguous()
+        if self.model._hmcx_model == 'mlp':                 # integer labels (mlp.py:52)
+            dt = torch.int32
         Yd = torch.as_tensor(np.asarray(y) if not isinstance(y, torch.Tensor) else y).to(dev, dt).contiguous()
         return Xd, Yd
 
@@ -147,8 +149,11 @@ class sgmcmc:
                 if (j % self.log_every) == 0:
                     ll = -1.0 * np.ravel(res.ll[j])[0]
                     print('epoch {0}, loss: {1:.4f}, mini-batch update : {2}'.format(i, ll, j), file=self.out)
-            # sgmcmc.py:79 — negative_log_posterior(q, last minibatch) from the device log-likelihood
-            logp_samples[i] = (-1.0 / batch_size) * (res.ll[-1] + self._log_prior())
+            # sgmcmc.py:79 — negative_log_posterior(q, last minibatch) from the device energies
+            if res.nlp is not None:
+                logp_samples[i] = res.nlp[-1]
+            else:
+                logp_samples[i] = (-1.0 / batch_size) * (res.ll[-1] + self._log_prior())
             host = self._state_to_host(state)
             for var in self.start.keys():
                 posterior[var].append(host[var])

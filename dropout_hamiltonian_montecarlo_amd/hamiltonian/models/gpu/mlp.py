@@ -1,0 +1,172 @@
+"""HIP-backed dropout MLP — drop-in for the reference's Chainer MLP (config 3).
+
+Reference: /root/reference/hamiltonian/models/gpu/mlp.py:19-96.  ``MyNetwork`` (:19-31) is
+l1 (n_in→n_mid) → dropout(.1) → relu → l2 (n_mid→n_mid) → dropout → relu → dropout → l3
+(n_mid→n_out); ``grad`` (:47-64) returns ∇ mean softmax-CE + ½α·θ per parameter,
+``log_likelihood`` (:66-78) returns the mean CE *loss*, ``log_prior`` (:40-45) is
+−Σ_var ½α·Σθ²/dim and ``negative_log_posterior`` (:80-82) is loss + log_prior.
+
+Parameters use Chainer's ``namedparams`` names and [out, in] weight layout ('/l1/W' [n_mid, n_in],
+'/l1/b', '/l2/W', '/l2/b', '/l3/W' [n_out, n_mid], '/l3/b').  Labels are integers (mlp.py:52).
+Every compute call goes through libhmcx (k_mm MFMA GEMMs with fused bias/dropout/relu/gradient
+epilogues, hmcx_mlp.hip).
+
+Dropout.  Chainer draws fresh masks on every forward (train mode).  Here ``masks=None`` draws them
+on the device from Philox (hmcx_mlp_masks, keyed by the model's seed and a call counter);
+``masks='off'`` disables dropout; an explicit ``masks=[m1, m2, m3]`` (each [B, n_mid]) injects
+them — the parity mode against oracle/models.py::mlp.
+"""
+import numpy as np
+import torch
+
+from dropout_hamiltonian_montecarlo_amd._native import HmcxError, MlpParams, MLP_MASK_SLOT0, context, dtype_code, ptr
+
+from .softmax import _batch, as_device
+
+MLP_PARAM_NAMES = ('/l1/W', '/l1/b', '/l2/W', '/l2/b', '/l3/W', '/l3/b')
+
+
+def mlp_param_shapes(n_in, n_mid, n_out):
+    return {'/l1/W': (n_mid, n_in), '/l1/b': (n_mid,), '/l2/W': (n_mid, n_mid), '/l2/b': (n_mid,),
+            '/l3/W': (n_out, n_mid), '/l3/b': (n_out,)}
+
+
+class mlp:
+    _hmcx_model = 'mlp'
+
+    def __init__(self, _hyper, n_in, n_mid_units, n_out, dtype=torch.float32, device=None, seed=0):
+        self.hyper = _hyper
+        self.alpha = float(np.asarray(_hyper['alpha']))
+        self.n_in, self.n_mid, self.n_out = int(n_in), int(n_mid_units), int(n_out)
+        self.dtype = dtype
+        self.code = dtype_code(dtype)
+        self.ctx = context(device)
+        self.device = self.ctx.device
+        self.seed = int(seed)
+        self._mask_calls = 0
+        self.shapes = mlp_param_shapes(self.n_in, self.n_mid, self.n_out)
+
+    # -------------------------------------------------------------- helpers
+    def init_params(self, seed=0):
+        """Chainer L.Linear defaults: W ~ LeCunNormal (N(0, 1/fan_in)), b = 0 (host numpy, float64)."""
+        rs = np.random.RandomState(seed)
+        out = {}
+        for k in MLP_PARAM_NAMES:
+            shp = self.shapes[k]
+            out[k] = rs.normal(0, 1.0 / np.sqrt(shp[1]), shp) if len(shp) == 2 else np.zeros(shp)
+        return out
+
+    def _dev(self, a):
+        return as_device(a, self.dtype, self.device)
+
+    def _params(self, par):
+        ts = []
+        for k in MLP_PARAM_NAMES:
+            if k not in par:
+                raise HmcxError("mlp: missing parameter %r (expected %s)" % (k, MLP_PARAM_NAMES))
+            t = self._dev(par[k])
+            if tuple(t.shape) != self.shapes[k]:
+                raise HmcxError("mlp: %s has shape %s, expected %s" % (k, tuple(t.shape), self.shapes[k]))
+            ts.append(t)
+        mp = MlpParams()
+        for i, t in enumerate(ts):
+            mp.p[i] = t.data_ptr()
+        return ts, mp
+
+    def _xy(self, args, need_y=True):
+        X, y = _batch(args)
+        X = self._dev(X)
+        if X.dim() != 2 or X.shape[1] != self.n_in:
+            raise HmcxError("mlp: X_train must be [B, %d]" % self.n_in)
+        if not need_y:
+            return X, None
+        yt = y if isinstance(y, torch.Tensor) else torch.as_tensor(np.asarray(y))
+        yt = yt.to(self.device, torch.int32).contiguous()
+        if yt.dim() != 1 or yt.shape[0] != X.shape[0]:
+            raise HmcxError("mlp: y_train must be integer labels [B] (mlp.py:52)")
+        return X, yt
+
+    def draw_masks(self, B):
+        """Fresh Philox dropout masks [3, B, n_mid] on the device (one forward's worth)."""
+        out = torch.empty((3, B, self.n_mid), dtype=self.dtype, device=self.device)
+        slot = (MLP_MASK_SLOT0 + self._mask_calls) & 0xFFFFFFFF
+        self._mask_calls += 1
+        ctx = context(self.device)
+        ctx.check(ctx.lib.hmcx_mlp_masks(ctx.h, self.code, B, self.n_mid, self.seed, 0, 0xFFFFFFFF, slot, ptr(out)),
+                  "hmcx_mlp_masks")
+        return out
+
+    def _masks(self, masks, B):
+        if masks is None:
+            return self.draw_masks(B)
+        if isinstance(masks, str):
+            if masks != 'off':
+                raise ValueError("masks must be None, 'off' or [m1, m2, m3]")
+            return None
+        m = torch.stack([self._dev(x) for x in masks]) if isinstance(masks, (list, tuple)) else self._dev(masks)
+        if tuple(m.shape) != (3, B, self.n_mid):
+            raise HmcxError("mlp: masks must be 3 x [B, n_mid]")
+        return m.contiguous()
+
+    # -------------------------------------------------------------- model surface
+    def grad(self, par, masks=None, **args):                              # mlp.py:47-64
+        X, y = self._xy(args)
+        B = X.shape[0]
+        ts, mp = self._params(par)
+        m = self._masks(masks, B)
+        gs = [torch.empty_like(t) for t in ts]
+        gp = MlpParams()
+        for i, g in enumerate(gs):
+            gp.p[i] = g.data_ptr()
+        ctx = context(self.device)
+        ctx.check(ctx.lib.hmcx_mlp_grad(ctx.h, self.code, ptr(X), ptr(y), B, self.n_in, self.n_mid, self.n_out, mp,
+                                        ptr(m), self.alpha, gp, None), "hmcx_mlp_grad")
+        return {k: g for k, g in zip(MLP_PARAM_NAMES, gs)}
+
+    def loss_device(self, par, masks=None, **args):
+        X, y = self._xy(args)
+        B = X.shape[0]
+        _, mp = self._params(par)
+        m = self._masks(masks, B)
+        out = torch.empty(1, dtype=torch.float64, device=self.device)
+        ctx = context(self.device)
+        ctx.check(ctx.lib.hmcx_mlp_loss(ctx.h, self.code, ptr(X), ptr(y), B, self.n_in, self.n_mid, self.n_out, mp,
+                                        ptr(m), ptr(out), None), "hmcx_mlp_loss")
+        return out
+
+    def log_likelihood(self, par, masks=None, **args):                    # mlp.py:66-78 (returns the loss)
+        return np.float64(self.loss_device(par, masks=masks, **args).item())
+
+    def log_prior(self, par, **args):                                     # mlp.py:40-45
+        K = 0.0
+        for var in par.keys():
+            v = self._dev(par[var]).to(torch.float64)
+            K -= 0.5 * self.alpha * float(torch.sum(v * v)) / v.numel()
+        return K
+
+    def negative_log_posterior(self, par, masks=None, **args):           # mlp.py:80-82
+        return self.log_likelihood(par, masks=masks, **args) + self.log_prior(par, **args)
+
+    def loss(self, par, masks=None, **args):
+        """North-star surface name: the sampler energy U = negative_log_posterior."""
+        return self.negative_log_posterior(par, masks=masks, **args)
+
+    def logits(self, par, X, masks='off'):
+        X = self._dev(X)
+        B = X.shape[0]
+        _, mp = self._params(par)
+        m = self._masks(masks, B)
+        z = torch.empty((B, self.n_out), dtype=self.dtype, device=self.device)
+        ctx = context(self.device)
+        ctx.check(ctx.lib.hmcx_mlp_loss(ctx.h, self.code, ptr(X), None, B, self.n_in, self.n_mid, self.n_out, mp,
+                                        ptr(m), None, ptr(z)), "hmcx_mlp_loss")
+        return z
+
+    def predict(self, par, X_test, prob=False, masks=None):              # mlp.py:84-96
+        """Chainer runs the net in train mode here too, so dropout is on by default (masks=None);
+        pass masks='off' for the deterministic network."""
+        z = self.logits(par, X_test, masks=masks).cpu().numpy()
+        if prob:                                                          # F.softmax on the host (:92)
+            e = np.exp(z - z.max(axis=1, keepdims=True))
+            return e / e.sum(axis=1, keepdims=True)
+        return z.argmax(axis=1)

@@ -151,6 +151,74 @@ typedef struct hmcx_hmc_mvn_args {
 } hmcx_hmc_mvn_args;
 int hmcx_hmc_mvn_run(hmcx_ctx* ctx, const hmcx_hmc_mvn_args* a);
 
+/* ------------------------------------------------------------------ MLP model (config 3)
+ * Replaces hamiltonian/models/gpu/mlp.py:19-31 (MyNetwork: l1 -> relu(dropout) -> l2 ->
+ * relu(dropout) -> dropout -> l3) and :47-82 (grad / log_likelihood / negative_log_posterior)
+ * without Chainer.  Parameters in Chainer's layout, L.Linear W = [out][in]:
+ *   W1 [n_mid][n_in], b1 [n_mid], W2 [n_mid][n_mid], b2 [n_mid], W3 [n_out][n_mid], b3 [n_out].
+ * Dropout (mlp.py:29-31, ratio 0.1, train mode): mask = (u >= 0.1) / 0.9 for the three [B][n_mid]
+ * activations of every forward.  mask_mode BUFFER: masks[...] holds them (3·B·n_mid values per
+ * forward, dtype); PHILOX: u = Philox(seed, chain, step, slot = forward index, element).       */
+typedef struct hmcx_mlp_params {
+  void* p[6];              /* W1, b1, W2, b2, W3, b3 (device, dtype) */
+} hmcx_mlp_params;
+
+/* Philox dropout masks of one forward: out [3][B][n_mid] (dtype) = (u >= 0.1)/0.9 with
+ * u = Philox(seed, chain, step, slot, element) — the masks hmcx_mlp_sghmc_run draws (PHILOX). */
+int hmcx_mlp_masks(hmcx_ctx* ctx, int dtype, int B, int n_mid, uint64_t seed, uint32_t chain, uint32_t step,
+                   uint32_t slot, void* out);
+
+/* grad = ∇ mean softmax-CE(net(X), y) + ½·alpha·θ for all six parameters (mlp.py:47-64).
+ * y: device int32 [B] labels.  masks: device [3][B][n_mid] or NULL (no dropout).
+ * grads: output pointers, same shapes.  loss (device double[1] or NULL): the mean CE. */
+int hmcx_mlp_grad(hmcx_ctx* ctx, int dtype, const void* X, const int32_t* y, int B, int n_in, int n_mid,
+                  int n_out, const hmcx_mlp_params* par, const void* masks, double alpha,
+                  hmcx_mlp_params* grads, double* loss);
+
+/* loss = mean softmax-CE (mlp.py:66-78 returns the loss); logits [B][n_out] optional output
+ * (predict, mlp.py:84-96). */
+int hmcx_mlp_loss(hmcx_ctx* ctx, int dtype, const void* X, const int32_t* y, int B, int n_in, int n_mid,
+                  int n_out, const hmcx_mlp_params* par, const void* masks, double* loss, void* logits);
+
+/* SGHMC steps for the MLP (reference cpu/sghmc.py:19-39 with the A1 completion; energies from
+ * mlp.py:80-82 nlp = loss + log_prior, log_prior = −Σ_var ½·alpha·Σθ²/dim).  Sub-steps follow
+ * order[0..5] (canonical indices 0=W1 1=b1 2=W2 3=b2 4=W3 5=b3 in the caller's start_p order).
+ * Noise BUFFER: per step, normals in the reference's draw order — momentum of every variable
+ * in `order`, then per leapfrog iteration one draw per variable in `order` — from noise_off[s].
+ * PHILOX: slot 0 momentum, slot it+1 iteration it, element = offset of the variable in `order`
+ * + index.  Masks: forward f of step s (f = 0 .. 6·n_iter−1 for the gradient calls, then the
+ * proposal's and the current state's energies) — BUFFER: masks + mask_off[s] + f·3·B·n_mid;
+ * PHILOX: slot 0x80000000 + f.  out_loss[s] = mean CE loss (log_likelihood, mlp.py:66-78) and out_nlp[s] =
+ * loss + log_prior (negative_log_posterior) of the state kept after step s, both under the masks
+ * of that state's energy forward. */
+typedef struct hmcx_mlp_sghmc_args {
+  int dtype;
+  int B, n_in, n_mid, n_out, n_steps;
+  int order[6];
+  double alpha;
+  const void* X;           /* device [N][n_in] */
+  const int32_t* y;        /* device [N] labels */
+  const int64_t* row0;     /* host [n_steps] */
+  const double* eps;       /* host [n_steps] */
+  const int32_t* n_iter;   /* host [n_steps] */
+  const double* u_accept;  /* host [n_steps] */
+  int noise_mode;
+  const double* noise;     /* device, BUFFER */
+  const int64_t* noise_off;/* host [n_steps], BUFFER */
+  int mask_mode;
+  const void* masks;       /* device, BUFFER (dtype) */
+  const int64_t* mask_off; /* host [n_steps], BUFFER */
+  uint64_t seed;
+  uint32_t chain, step_base;
+  hmcx_mlp_params par;     /* state, updated in place */
+  double* out_A;           /* device [n_steps] */
+  int32_t* out_accepted;   /* device [n_steps] */
+  double* out_loss;        /* device [n_steps] */
+  double* out_nlp;         /* device [n_steps] or NULL */
+  double* out_E;           /* device [n_steps*2] (E_current, E_new) or NULL */
+} hmcx_mlp_sghmc_args;
+int hmcx_mlp_sghmc_run(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* a);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,215 @@
+"""GPU parity of the dropout MLP (config 3, hmcx_mlp.hip) against the NumPy restatement
+oracle/models.py::mlp (itself cross-checked with torch autograd in test_oracle_golden.py; the
+Chainer reference is not runnable here, so MLP parity is pinned to that restatement only).
+
+Dropout masks are injected (the same [3, B, n_mid] arrays on both sides).  Tolerances:
+float64 gradients/losses within rel 1e-9 of the largest entry (GEMM summation order only);
+float32 within 2e-4 of the largest entry; SGHMC path lengths and accept flags bit-exact, float64
+states within rel 1e-8."""
+import io
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from oracle import models as om  # noqa: E402
+from oracle import samplers as osm  # noqa: E402
+
+
+def _mlp_cls():
+    from dropout_hamiltonian_montecarlo_amd.hamiltonian.models.gpu.mlp import mlp
+    from dropout_hamiltonian_montecarlo_amd.hamiltonian.inference.gpu.sghmc import sghmc
+    return mlp, sghmc
+
+
+def _problem(seed, B, n_in, n_mid, n_out, wscale=0.3):
+    rs = np.random.RandomState(seed)
+    par = {k: rs.normal(0, wscale, s) for k, s in om.mlp_param_shapes(n_in, n_mid, n_out).items()}
+    X = rs.rand(B, n_in)
+    y = rs.randint(0, n_out, B)
+    masks = om.dropout_masks(rs, B, n_mid, dtype=np.float64)
+    return par, X, y, masks
+
+
+def _close(a, b, rel):
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    scale = max(np.abs(b).max(), 1e-30)
+    err = np.abs(a - b).max()
+    assert err <= rel * scale, "max abs err %.3e > %.1e x %.3e" % (err, rel, scale)
+
+
+SHAPES = [(32, 784, 256, 10), (19, 50, 37, 7), (500, 784, 256, 10), (1, 3, 1, 2), (70, 33, 64, 40)]
+
+
+@pytest.mark.parametrize("B,n_in,n_mid,n_out", SHAPES)
+@pytest.mark.parametrize("dropout", [True, False])
+def test_grad_f64_matches_oracle(B, n_in, n_mid, n_out, dropout):
+    mlp, _ = _mlp_cls()
+    par, X, y, masks = _problem(1, B, n_in, n_mid, n_out)
+    ref = om.mlp({"alpha": 0.01}, n_in, n_mid, n_out)
+    mk = masks if dropout else None
+    g_ref = ref.grad(par, masks=mk, X_train=X, y_train=y)
+    m = mlp({"alpha": 0.01}, n_in, n_mid, n_out, dtype=torch.float64, device="cuda:0")
+    g = m.grad(par, masks=(masks if dropout else 'off'), X_train=X, y_train=y)
+    for k in om.MLP_PARAM_NAMES:
+        assert tuple(g[k].shape) == g_ref[k].shape
+        _close(g[k].cpu().numpy(), g_ref[k], 1e-9)
+    l_ref = ref.log_likelihood(par, masks=mk, X_train=X, y_train=y)
+    l = m.log_likelihood(par, masks=(masks if dropout else 'off'), X_train=X, y_train=y)
+    assert abs(l - l_ref) <= 1e-11 * max(1.0, abs(l_ref))
+    nlp_ref = ref.negative_log_posterior(par, masks=mk, X_train=X, y_train=y)
+    nlp = m.negative_log_posterior(par, masks=(masks if dropout else 'off'), X_train=X, y_train=y)
+    assert abs(nlp - nlp_ref) <= 1e-11 * max(1.0, abs(nlp_ref))
+
+
+@pytest.mark.parametrize("B,n_in,n_mid,n_out", SHAPES[:3])
+def test_grad_f32_close_to_oracle(B, n_in, n_mid, n_out):
+    mlp, _ = _mlp_cls()
+    par, X, y, masks = _problem(2, B, n_in, n_mid, n_out)
+    # the oracle at float32-rounded inputs
+    par32 = {k: v.astype(np.float32).astype(np.float64) for k, v in par.items()}
+    X32 = X.astype(np.float32).astype(np.float64)
+    mk32 = [mm.astype(np.float32).astype(np.float64) for mm in masks]
+    g_ref = om.mlp({"alpha": 0.01}, n_in, n_mid, n_out).grad(par32, masks=mk32, X_train=X32, y_train=y)
+    m = mlp({"alpha": 0.01}, n_in, n_mid, n_out, dtype=torch.float32, device="cuda:0")
+    g = m.grad(par, masks=masks, X_train=X, y_train=y)
+    for k in om.MLP_PARAM_NAMES:
+        assert g[k].dtype == torch.float32
+        _close(g[k].cpu().numpy(), g_ref[k], 2e-4)
+
+
+def test_predict_matches_oracle():
+    mlp, _ = _mlp_cls()
+    par, X, y, masks = _problem(3, 64, 40, 24, 6)
+    ref = om.mlp({"alpha": 0.01}, 40, 24, 6)
+    m = mlp({"alpha": 0.01}, 40, 24, 6, dtype=torch.float64, device="cuda:0")
+    np.testing.assert_array_equal(m.predict(par, X, masks='off'), ref.predict(par, X))
+    np.testing.assert_allclose(m.predict(par, X, prob=True, masks='off'), ref.predict(par, X, prob=True),
+                               rtol=1e-11, atol=1e-14)
+    np.testing.assert_allclose(m.predict(par, X, prob=True, masks=masks),
+                               ref.predict(par, X, prob=True, masks=masks), rtol=1e-11, atol=1e-14)
+
+
+def test_philox_masks_properties():
+    mlp, _ = _mlp_cls()
+    m = mlp({"alpha": 0.01}, 784, 256, 10, dtype=torch.float32, device="cuda:0", seed=9)
+    a = m.draw_masks(500).cpu().numpy()
+    b = m.draw_masks(500).cpu().numpy()
+    scale = np.float32(1 / 0.9)
+    assert a.shape == (3, 500, 256)
+    assert set(np.unique(a)) <= {np.float32(0), scale}
+    assert abs(np.mean(a == 0) - 0.1) < 0.005                      # keep probability 0.9
+    assert np.mean(a != b) > 0.1                                    # fresh masks per forward
+    m2 = mlp({"alpha": 0.01}, 784, 256, 10, dtype=torch.float32, device="cuda:0", seed=9)
+    np.testing.assert_array_equal(m2.draw_masks(500).cpu().numpy(), a)   # deterministic under the seed
+
+
+# ----------------------------------------------------------------------------- SGHMC parity
+def _mask_stream(B, n_mid):
+    """Masks of forward f of global step k: sequential draws of RandomState(1000 + k)."""
+    cache = {}
+
+    def get(k, n):
+        rs = np.random.RandomState(1000 + k)
+        return np.stack([np.stack(om.dropout_masks(rs, B, n_mid, dtype=np.float64)) for _ in range(n)])
+
+    def one(k, f):
+        if k not in cache or cache[k].shape[0] <= f:
+            cache[k] = get(k, max(f + 1, 2 * (f + 1)))
+        return cache[k][f]
+    return get, one
+
+
+class _MaskedOracleMLP:
+    """oracle mlp whose grad / accept energies take injected masks in the sampler's call order."""
+
+    def __init__(self, inner, one):
+        self.inner, self.one = inner, one
+        self.k, self.f, self.in_step = 0, 0, False
+
+    def grad(self, par, **args):
+        m = self.one(self.k, self.f)
+        self.f += 1
+        return self.inner.grad(par, masks=list(m), **args)
+
+    def negative_log_posterior(self, par, **args):
+        if not self.in_step:
+            return self.inner.negative_log_posterior(par, masks=None, **args)
+        m = self.one(self.k, self.f)
+        self.f += 1
+        return self.inner.negative_log_posterior(par, masks=list(m), **args)
+
+    def log_likelihood(self, par, **args):
+        return self.inner.log_likelihood(par, masks=None, **args)
+
+
+class _OracleSghmc(osm.sghmc):
+    def step(self, state, momentum, rng, **args):
+        self.model.in_step, self.model.f = True, 0
+        out = super().step(state, momentum, rng, **args)
+        self.model.in_step = False
+        self.model.k += 1
+        return out
+
+
+@pytest.mark.parametrize("order", [list(om.MLP_PARAM_NAMES), ['/l3/b', '/l1/W', '/l2/b', '/l3/W', '/l1/b', '/l2/W']])
+def test_sghmc_mlp_matches_oracle(order):
+    mlp, sghmc = _mlp_cls()
+    n_in, n_mid, n_out, N, B = 24, 20, 5, 120, 30
+    rs = np.random.RandomState(4)
+    X = rs.rand(N, n_in)
+    y = rs.randint(0, n_out, N)
+    start = {k: rs.normal(0, 0.2, s) for k, s in om.mlp_param_shapes(n_in, n_mid, n_out).items()}
+    start = {k: start[k] for k in order}
+    get, one = _mask_stream(B, n_mid)
+    kw = dict(path_length=0.02, step_size=0.005, verbose=True)
+
+    o = _OracleSghmc(_MaskedOracleMLP(om.mlp({"alpha": 0.01}, n_in, n_mid, n_out), one), start, **kw)
+    o.trace, o.out = [], io.StringIO()
+    np.random.seed(7)
+    post_r, _ = o.sample(epochs=2, burnin=1, batch_size=B, rng=np.random.RandomState(8), X_train=X, y_train=y)
+
+    m = mlp({"alpha": 0.01}, n_in, n_mid, n_out, dtype=torch.float64, device="cuda:0")
+    s = sghmc(m, start, noise='numpy', **kw)
+    s.mask_provider = get
+    s.trace, s.out = [], io.StringIO()
+    np.random.seed(7)
+    post_g, logp_g = s.sample(epochs=2, burnin=1, batch_size=B, rng=np.random.RandomState(8), X_train=X, y_train=y)
+
+    assert len(s.trace) == len(o.trace) == 12
+    assert [t["L"] for t in s.trace] == [t["L"] for t in o.trace]
+    assert max(t["L"] for t in o.trace) >= 3                       # real trajectories
+    assert [t["accepted"] for t in s.trace] == [t["accepted"] for t in o.trace]
+    np.testing.assert_allclose([t["A"] for t in s.trace], [t["A"] for t in o.trace], rtol=1e-8, atol=1e-12)
+    for k in order:
+        np.testing.assert_allclose(post_g[k], post_r[k], rtol=1e-8, atol=1e-10)
+    assert np.all(np.isfinite(logp_g))
+
+
+def test_sghmc_mlp_config3_philox():
+    """Config 3 shape (784-256-256-10, B = 500), float32, device masks and noise: finite, mixing,
+    deterministic under the seed."""
+    mlp, sghmc = _mlp_cls()
+    N, B = 3000, 500
+    rs = np.random.RandomState(0)
+    X = rs.rand(N, 784).astype(np.float32)
+    y = rs.randint(0, 10, N)
+
+    def run():
+        m = mlp({"alpha": 0.01}, 784, 256, 10, dtype=torch.float32, device="cuda:0")
+        s = sghmc(m, m.init_params(1), path_length=0.005, step_size=1e-3, noise='philox', seed=3)
+        s.trace, s.out = [], io.StringIO()
+        post, logp = s.sample(epochs=1, burnin=1, batch_size=B, X_train=X, y_train=y)
+        return post, logp, s.trace
+
+    p1, l1, t1 = run()
+    p2, l2, t2 = run()
+    assert all(np.all(np.isfinite(v)) for v in p1.values()) and np.all(np.isfinite(l1))
+    for k in p1:
+        np.testing.assert_array_equal(p1[k], p2[k])
+    assert [t["L"] for t in t1] == [t["L"] for t in t2]
+    assert np.mean([t["accepted"] for t in t1]) > 0.2
