@@ -5,25 +5,29 @@
 // log_likelihood returns the mean CE, nlp = loss + log_prior).  Chainer/CuPy are not available, so
 // the arithmetic follows the NumPy restatement in oracle/models.py::mlp (parity with injected masks).
 //
-// Names: a1 = X·W1ᵀ + b1, h1 = max(a1·m0, 0), h2 = max((h1·W2ᵀ + b2)·m1, 0), d3 = h2·m2,
+// Names: xw = X·W1ᵀ, a1 = xw + b1, h1 = max(a1·m0, 0), h2 = max((h1·W2ᵀ + b2)·m1, 0), d3 = h2·m2,
 // z = d3·W3ᵀ + b3; m0, m1, m2 are the three dropout masks of one forward ([B][n_mid] each).
+// xw is stored without the bias, so a move of b1 never re-runs the 784-deep layer-1 GEMM: every
+// consumer forms a1 = xw + b1 on the fly (the same rounding as the reference's X·W1ᵀ + b1).
 //
 // Kernels:
-//  * k_mm<T, EPI, AOP, BOP>: C = op(A)·op(B) on v_mfma_*_16x16x4, 32x32 output tile per workgroup,
-//    K split over its 8 waves (three k chunks in flight per wave, 16-byte vector loads along k for
-//    k-contiguous operands, fixed-order LDS combine).
-//    Operand transform OP_H1 builds h1 = max(a1·m0, 0) on the fly, so h1 is never stored.  Fused
-//    epilogues: bias (a1, logits), layer 2 (bias, dropout, relu, next dropout → h2, d3), layer 3
-//    with the softmax cross-entropy (gz = (softmax − onehot)/B and per-row-block loss partials),
-//    the two relu/dropout backward gates (ga2, ga1), gradient + prior, and the SGHMC update of one
-//    variable (sghmc.py:31,34) which also writes the NEXT iteration's drifted position (sghmc.py:32)
-//    into the other half of a double buffer — no separate drift launch.
-//  * k_colsum: bias gradients Σ_rows (fixed order) with the same gradient / SGHMC epilogues.
+//  * k_mm<T, EPI, AOP, BOP, ...>: C = op(A)·op(B) on v_mfma_*_16x16x4, 32x32 output tile per
+//    workgroup, K split over its 8 waves (three k chunks in flight per wave, 16-byte vector loads
+//    along k for k-contiguous operands, fixed-order LDS combine).  OP_H1 builds h1 from xw, b1 and
+//    m0 on the fly (h1 is never stored).  Epilogues: layer 2 (bias, dropout, relu, next dropout →
+//    h2, d3); layer 3 + softmax cross-entropy, which in the same workgroup also forms ga2 (the
+//    layer-2 backward) and the row-block partials of the b2 / b3 / W3 gradients; the layer-1
+//    backward ga1 (+ b1 partials); the weight gradients with the gradient + prior or the SGHMC
+//    epilogue (sghmc.py:31-34), which also writes the NEXT iteration's drifted position into the
+//    other half of a double buffer (no drift launch).
+//  * Deferred updates: the gradient of a bias (or of W3) is a sum of per-row-block partials; its
+//    gradient / SGHMC update runs in the prologue of whatever kernel is launched next (none of them
+//    reads the momentum or the next-position buffer it writes) — no reduction launch.
 //  * k_mlp_keep: the keep flags of every dropout mask of one SGHMC step (Philox, one launch/step).
 //  * k_mlp_init / k_sumsq12 / k_mlp_accept / k_mlp_commit: momentum draw + first drift + energy
 //    partials, end-of-trajectory energy partials, MH accept (hmc.py:67-79), commit on accept.
-// Per leapfrog iteration at order (W1, b1, W2, b2, W3, b3): 26 launches, ≈1.2 GFLOP at
-// 784-256-256-10, B = 500 (layer 1 is recomputed only after W1 or b1 moved).
+// Per leapfrog iteration at order (W1, b1, W2, b2, W3, b3): 17 launches, ≈1.0 GFLOP at
+// 784-256-256-10, B = 500 (layer 1 runs once, after W1 moved).
 #include "hmcx_common.h"
 #include "hmcx_internal.h"
 #include <algorithm>
@@ -33,7 +37,9 @@ namespace hmcx {
 
 // Mask slots live above the noise slots (0 = momentum, it+1 = iteration it) of the same counter space.
 constexpr uint32_t MASK_SLOT0 = 0x80000000u;
-constexpr int NPART = 32;   // blocks per variable in the energy partial sums
+constexpr int NPART = 32;     // blocks per variable in the energy partial sums
+constexpr int MM_NW = 8;      // waves per k_mm workgroup; the K range is split over them
+constexpr int MM_NT = MM_NW * 64;
 
 // Dropout masks of one forward: m0, m1, m2 at offsets 0, mn, 2·mn.
 template <typename T> struct MaskSrc {
@@ -48,12 +54,75 @@ template <typename T> __device__ inline T mval(const MaskSrc<T>& s, int which, s
   if (s.keep) return s.keep[e] ? s.scale : T(0);
   return T(1);
 }
+// V consecutive mask values from an element index that is a multiple of V (V = 16 / sizeof T)
+template <typename T, int V> __device__ inline void mvals(const MaskSrc<T>& s, int which, size_t i, T (&m)[V]) {
+  const size_t e = (size_t)which * s.mn + i;
+  if (s.vals) {
+#pragma unroll
+    for (int q = 0; q < V; ++q) m[q] = s.vals[e + q];
+  } else if (s.keep) {
+    if constexpr (V == 4) {
+      const uint32_t k = *reinterpret_cast<const uint32_t*>(s.keep + e);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) m[q] = ((k >> (8 * q)) & 0xFF) ? s.scale : T(0);
+    } else {
+      const uint16_t k = *reinterpret_cast<const uint16_t*>(s.keep + e);
+      m[0] = (k & 0xFF) ? s.scale : T(0);
+      m[1] = (k >> 8) ? s.scale : T(0);
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < V; ++q) m[q] = T(1);
+  }
+}
 
 __device__ inline bool keep_flag(uint32_t w) {                // Chainer dropout: keep iff u >= ratio
   return (float)(w >> 8) * 5.9604644775390625e-08f >= 0.1f;
 }
 
-enum MMEpi { MM_BIAS = 0, MM_L2 = 1, MM_L3CE = 2, MM_GA2 = 3, MM_GA1 = 4, MM_GRAD = 5, MM_SGHMC = 6 };
+// Gradient + prior (mlp.py:63) or the SGHMC momentum update (sghmc.py:31,34) of one variable.
+template <typename T> struct Upd {
+  const T* W; T* P; T* Qn; T* G;     // θ, momentum, next drifted θ (or null), gradient output (GRAD)
+  T half_alpha, eps, one_minus_eps, noise_scale;
+  int noise_mode; const double* noise;
+  uint64_t seed; uint32_t chain, step, slot, e0;
+};
+enum UpdMode { UPD_NONE = 0, UPD_GRAD = 1, UPD_SGHMC = 2 };
+
+template <typename T>
+__device__ inline void apply_upd(const Upd<T>& u, int mode, size_t i, T v) {
+  if (mode == UPD_GRAD) {
+    u.G[i] = v + u.half_alpha * u.W[i];
+  } else {
+    const T g = v + u.half_alpha * u.W[i];
+    const T z = u.noise_mode == HMCX_NOISE_BUFFER ? (T)u.noise[i]
+                                                  : (T)philox_normal(u.seed, u.chain, u.step, u.slot, u.e0 + (uint32_t)i);
+    const T p = (u.one_minus_eps * u.P[i] + u.eps * g) + u.noise_scale * z;
+    u.P[i] = p;
+    if (u.Qn) u.Qn[i] = u.W[i] + u.eps * p;                   // sghmc.py:32 of the next iteration
+  }
+}
+
+// A gradient given as nparts row-block partials [nparts][n], applied by the next kernel's prologue.
+template <typename T> struct Pending {
+  int mode, n, nparts;
+  const T* part;
+  Upd<T> u;
+};
+template <typename T>
+__device__ inline void run_pending(const Pending<T>& pd) {
+  if (pd.mode == UPD_NONE) return;
+  const int nthr = gridDim.x * gridDim.y * blockDim.x;
+  for (int i = (blockIdx.y * gridDim.x + blockIdx.x) * blockDim.x + threadIdx.x; i < pd.n; i += nthr) {
+    T s = pd.part[i];
+    for (int b = 1; b < pd.nparts; ++b) s += pd.part[(size_t)b * pd.n + i];
+    apply_upd(pd.u, pd.mode, i, s);
+  }
+}
+template <typename T>
+__global__ __launch_bounds__(256) void k_pending(Pending<T> pd) { run_pending(pd); }
+
+enum MMEpi { MM_STORE = 0, MM_L2 = 1, MM_L3CE = 2, MM_GA1 = 3, MM_UPD = 4 };
 enum MMOp { OP_PLAIN = 0, OP_H1 = 1 };
 
 template <typename T> struct MMArgs {
@@ -61,78 +130,27 @@ template <typename T> struct MMArgs {
   const T* A; int lda, ta;           // A(m,k) = ta ? A[k·lda + m] : A[m·lda + k]
   const T* B; int ldb, tb;           // B(k,n) = tb ? B[n·ldb + k] : B[k·ldb + n]
   T* C; int ldc;                     // output [M][ldc]
-  const T* bias;                     // [N]
+  const T* bias;                     // L2: b2, L3CE: b3
+  const T* b1;                       // OP_H1 / GA1: layer-1 bias
   MaskSrc<T> ms;
-  const T* H;                        // GA2: h2, GA1: a1 (the relu gate)
+  const T* H;                        // GA1: xw (the relu gate is (xw + b1)·m0 > 0)
   T* C2;                             // L2: d3
-  double* lpart;                     // L3CE: Σ −log p[label] of each 32-row block
-  const int32_t* y;                  // L3CE: labels
-  const T* W; T* P; T* Qn;           // GRAD/SGHMC: θ of the variable, momentum, next drifted θ
-  T half_alpha, eps, one_minus_eps, noise_scale;
-  int noise_mode; const double* noise;
-  uint64_t seed; uint32_t chain, step, slot, e0;
+  T* colpart;                        // GA1: b1 partials [gridDim.x][ldc]
+  // L3CE extras (per 32-row block): loss, ga2 and the b2 / b3 / W3 gradient partials
+  double* lpart; const int32_t* y;
+  const T* W3; const T* h2; const T* d3; int n_mid;
+  T* ga2; T* pb2; T* pb3; T* pw3;
+  int upd_mode; Upd<T> u;            // MM_UPD
+  Pending<T> pend;                   // run first, by the whole grid
 };
 
-template <typename T, int EPI>
-__device__ inline void mm_epilogue(const MMArgs<T>& a, int m, int n, T v) {
-  const size_t i = (size_t)m * a.ldc + n;
-  if constexpr (EPI == MM_BIAS) {
-    a.C[i] = v + a.bias[n];
-  } else if constexpr (EPI == MM_L2) {                          // mlp.py:30-31
-    const T t = (v + a.bias[n]) * mval(a.ms, 1, i);
-    const T h = t > T(0) ? t : T(0);
-    a.C[i] = h;
-    a.C2[i] = h * mval(a.ms, 2, i);
-  } else if constexpr (EPI == MM_GA2) {                         // ((gz·W3)·m2)·[h2>0]·m1
-    T t = v * mval(a.ms, 2, i);
-    t = t * (a.H[i] > T(0) ? T(1) : T(0));
-    a.C[i] = t * mval(a.ms, 1, i);
-  } else if constexpr (EPI == MM_GA1) {                         // (ga2·W2)·[a1·m0>0]·m0
-    const T m0 = mval(a.ms, 0, i);
-    a.C[i] = (v * (a.H[i] * m0 > T(0) ? T(1) : T(0))) * m0;
-  } else if constexpr (EPI == MM_GRAD) {                        // mlp.py:63 grad + ½αθ
-    a.C[i] = v + a.half_alpha * a.W[i];
-  } else if constexpr (EPI == MM_SGHMC) {                       // sghmc.py:31-34
-    const T g = v + a.half_alpha * a.W[i];
-    const T z = a.noise_mode == HMCX_NOISE_BUFFER ? (T)a.noise[i]
-                                                  : (T)philox_normal(a.seed, a.chain, a.step, a.slot, a.e0 + (uint32_t)i);
-    const T p = (a.one_minus_eps * a.P[i] + a.eps * g) + a.noise_scale * z;
-    a.P[i] = p;
-    if (a.Qn) a.Qn[i] = a.W[i] + a.eps * p;
+template <typename T, int OP>
+__device__ inline T op_apply(T x, T mask, T bias) {
+  if constexpr (OP == OP_H1) {
+    const T t = (x + bias) * mask;                             // h1 = max((xw + b1)·m0, 0)
+    return t > T(0) ? t : T(0);
   }
-}
-
-// Softmax cross-entropy of the rows of one 32-row block held in LDS (F.softmax_cross_entropy, mean):
-// gz = (softmax − onehot)/B, lpart[block] = Σ_rows −log p[label] (fixed order).
-template <typename T>
-__device__ inline void ce_rows(T (*zt)[33], double* rowl, int m0, int M, int N, const int32_t* y, T* gz, int ldg,
-                               double* lpart, int blk) {
-  const int t = threadIdx.x;
-  if (t < 32) {
-    const int m = m0 + t;
-    double l = 0.0;
-    if (m < M) {
-      T mx = zt[t][0];
-      for (int k = 1; k < N; ++k) mx = zt[t][k] > mx ? zt[t][k] : mx;
-      T s = T(0);
-      for (int k = 0; k < N; ++k) s += exp(zt[t][k] - mx);
-      const T ls = log(s);
-      const int lab = y[m];
-      l = -(double)((zt[t][lab] - mx) - ls);
-      for (int k = 0; k < N; ++k) {
-        T g = exp((zt[t][k] - mx) - ls);
-        if (k == lab) g -= T(1);
-        gz[(size_t)m * ldg + k] = g / (T)M;
-      }
-    }
-    rowl[t] = l;
-  }
-  __syncthreads();
-  if (t == 0) {
-    double s = 0.0;
-    for (int r = 0; r < 32; ++r) s += rowl[r];
-    lpart[blk] = s;
-  }
+  return x;
 }
 
 // k offset, inside a 16-wide k chunk, of MFMA step u (0..3) for lane group lg: each lane's k values
@@ -141,21 +159,13 @@ template <typename T> __device__ inline int kmap(int u, int lg);
 template <> __device__ inline int kmap<float>(int u, int lg) { return 4 * lg + u; }
 template <> __device__ inline int kmap<double>(int u, int lg) { return ((u >> 1) << 3) + 2 * lg + (u & 1); }
 
-template <typename T, int OP>
-__device__ inline T op_apply(T x, size_t idx, const MaskSrc<T>& ms) {
-  if constexpr (OP == OP_H1) {
-    const T t = x * mval(ms, 0, idx);
-    return t > T(0) ? t : T(0);
-  }
-  return x;
-}
-
 // Operand values of one 16-k chunk for rows (A) / columns (B) r0 + 16·i + lr, i = 0, 1:
 // x[u][i] = Op(r, k0 + kmap(u, lg)).  TR: element (r, k) at P[k·ld + r], else P[r·ld + k].
 // VEC (requires !TR, ld % (16/sizeof T) == 0 and a 16-byte aligned P): 16-byte vector loads along k.
+// OP_H1 masks index the stored matrix (element idx); its bias column is TR ? r : k.
 template <typename T, int OP, int TR, int VEC>
 __device__ inline void load_chunk(T (&x)[4][2], const T* P, int ld, int r0, int R, int k0, int ke, int lr, int lg,
-                                  const MaskSrc<T>& ms) {
+                                  const MaskSrc<T>& ms, const T* b1) {
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int r = r0 + 16 * i + lr;
@@ -167,19 +177,29 @@ __device__ inline void load_chunk(T (&x)[4][2], const T* P, int ld, int r0, int 
         const int kv = k0 + (sizeof(T) == 8 ? 8 * h + 2 * lg : 4 * lg);
         const size_t base = (size_t)r * ld + kv;
         if (rok && kv + V <= ke) {
+          T v[V], m[V], bb[V];
           if constexpr (V == 4) {
-            const float4 v = *reinterpret_cast<const float4*>(P + base);
-            x[0][i] = op_apply<T, OP>(v.x, base, ms); x[1][i] = op_apply<T, OP>(v.y, base + 1, ms);
-            x[2][i] = op_apply<T, OP>(v.z, base + 2, ms); x[3][i] = op_apply<T, OP>(v.w, base + 3, ms);
+            const float4 w = *reinterpret_cast<const float4*>(P + base);
+            v[0] = w.x; v[1] = w.y; v[2] = w.z; v[3] = w.w;
           } else {
-            const double2 v = *reinterpret_cast<const double2*>(P + base);
-            x[2 * h][i] = op_apply<T, OP>(v.x, base, ms);
-            x[2 * h + 1][i] = op_apply<T, OP>(v.y, base + 1, ms);
+            const double2 w = *reinterpret_cast<const double2*>(P + base);
+            v[0] = w.x; v[1] = w.y;
           }
+          if constexpr (OP == OP_H1) {
+            mvals<T, V>(ms, 0, base, m);
+#pragma unroll
+            for (int q = 0; q < V; ++q) bb[q] = b1[kv + q];
+          }
+#pragma unroll
+          for (int q = 0; q < V; ++q) x[h * V + q][i] = op_apply<T, OP>(v[q], m[q], bb[q]);
         } else {
 #pragma unroll
-          for (int q = 0; q < V; ++q)
-            x[h * V + q][i] = (rok && kv + q < ke) ? op_apply<T, OP>(P[base + q], base + q, ms) : T(0);
+          for (int q = 0; q < V; ++q) {
+            const bool ok = rok && kv + q < ke;
+            x[h * V + q][i] = ok ? op_apply<T, OP>(P[base + q], OP == OP_H1 ? mval(ms, 0, base + q) : T(1),
+                                                   OP == OP_H1 ? b1[kv + q] : T(0))
+                                 : T(0);
+          }
         }
       }
     } else {
@@ -187,19 +207,165 @@ __device__ inline void load_chunk(T (&x)[4][2], const T* P, int ld, int r0, int 
       for (int u = 0; u < 4; ++u) {
         const int k = k0 + kmap<T>(u, lg);
         const size_t idx = TR ? (size_t)k * ld + r : (size_t)r * ld + k;
-        x[u][i] = (rok && k < ke) ? op_apply<T, OP>(P[idx], idx, ms) : T(0);
+        const bool ok = rok && k < ke;
+        x[u][i] = ok ? op_apply<T, OP>(P[idx], OP == OP_H1 ? mval(ms, 0, idx) : T(1),
+                                       OP == OP_H1 ? b1[TR ? r : k] : T(0))
+                     : T(0);
       }
     }
   }
 }
 
-constexpr int MM_NW = 8;   // waves per workgroup; the K range is split over them
+// Softmax cross-entropy of the rows of one 32-row block held in LDS zt[32][zs] (F.softmax_cross_entropy,
+// mean): gz = (softmax − onehot)/M replaces z in LDS and goes to gz[m][ldg]; lpart[blk] = Σ −log p[y].
+template <typename T>
+__device__ inline void ce_rows(T* zt, int zs, double* rowl, int m0, int M, int N, const int32_t* y, T* gz, int ldg,
+                               double* lpart, int blk) {
+  const int t = threadIdx.x;
+  if (t < 32) {
+    T* zr = zt + t * zs;
+    const int m = m0 + t;
+    double l = 0.0;
+    if (m < M) {
+      T mx = zr[0];
+      for (int k = 1; k < N; ++k) mx = zr[k] > mx ? zr[k] : mx;
+      T s = T(0);
+      for (int k = 0; k < N; ++k) s += exp(zr[k] - mx);
+      const T ls = log(s);
+      const int lab = y[m];
+      l = -(double)((zr[lab] - mx) - ls);
+      for (int k = 0; k < N; ++k) {
+        T g = exp((zr[k] - mx) - ls);
+        if (k == lab) g -= T(1);
+        g = g / (T)M;
+        zr[k] = g;
+        gz[(size_t)m * ldg + k] = g;
+      }
+    } else {
+      for (int k = 0; k < N; ++k) zr[k] = T(0);
+    }
+    rowl[t] = l;
+  }
+  __syncthreads();
+  if (t == 0) {
+    double s = 0.0;
+    for (int r = 0; r < 32; ++r) s += rowl[r];
+    lpart[blk] = s;
+  }
+}
+
+// Layer-3 backward of one 32-row block from gz in LDS (zt[32][zs], N = n_out columns; rows past M
+// hold zeros):  ga2 = ((gz·W3)·m2)·[h2>0]·m1 and its column sums (b2 partial), column sums of gz
+// (b3 partial), and gzᵀ·d3 over the block's rows (W3 partial).  Threads own a column j and a row
+// group (rows ≡ g mod R, R = blockDim / n_mid); W3 is staged in LDS scratch `scr` when it fits.
+template <typename T>
+__device__ inline void l3_backward(const MMArgs<T>& a, const T* zt, int zs, int m0, int blk, T* scr, int scr_n) {
+  const int N = a.N, nm = a.n_mid;
+  const int rows = min(32, a.M - m0);
+  const int tid = threadIdx.x, nt = blockDim.x;
+  if (a.ga2) {
+    const bool wl = N * nm + nt <= scr_n;                      // W3 in LDS (+ nt values for the combine)
+    T* w3 = scr + nt;
+    if (wl) {
+      for (int e = tid; e < N * nm; e += nt) w3[e] = a.W3[e];
+      __syncthreads();
+    }
+    const int R = max(1, nt / nm), cols = nt / R;
+#pragma unroll 1
+    for (int jb = 0; jb < nm; jb += cols) {
+      const int j = jb + tid % cols, g = tid / cols;
+      const bool act = g < R && j < nm;
+      T cs = T(0);
+      if (act) {
+#pragma unroll 1
+        for (int r0 = g; r0 < rows; r0 += 8 * R) {
+          // 8 rows per pass: their h2 / mask loads go out first, then 8 independent dot products
+          T hv[8], m1v[8], m2v[8], acc8[8];
+#pragma unroll
+          for (int c = 0; c < 8; ++c) {
+            const int r = min(r0 + c * R, rows - 1);
+            const size_t i = (size_t)(m0 + r) * nm + j;
+            hv[c] = a.h2[i];
+            m1v[c] = mval(a.ms, 1, i);
+            m2v[c] = mval(a.ms, 2, i);
+            acc8[c] = T(0);
+          }
+#pragma unroll 1
+          for (int o = 0; o < N; ++o) {
+            const T w = wl ? w3[o * nm + j] : a.W3[(size_t)o * nm + j];
+#pragma unroll
+            for (int c = 0; c < 8; ++c) acc8[c] += zt[min(r0 + c * R, 31) * zs + o] * w;
+          }
+#pragma unroll
+          for (int c = 0; c < 8; ++c) {
+            const int r = r0 + c * R;
+            T t = acc8[c] * m2v[c];
+            t = t * (hv[c] > T(0) ? T(1) : T(0));
+            t = t * m1v[c];
+            if (r < rows) {
+              a.ga2[(size_t)(m0 + r) * nm + j] = t;
+              cs += t;
+            }
+          }
+        }
+      }
+      if (a.pb2) {
+        scr[tid] = cs;
+        __syncthreads();
+        if (act && g == 0) {
+          T t = scr[tid];
+          for (int q = 1; q < R; ++q) t += scr[q * cols + tid];
+          a.pb2[(size_t)blk * nm + j] = t;
+        }
+        __syncthreads();
+      }
+    }
+  }
+  if (a.pb3) {
+    for (int j = tid; j < N; j += nt) {
+      T cs = T(0);
+      for (int r = 0; r < rows; ++r) cs += zt[r * zs + j];
+      a.pb3[(size_t)blk * N + j] = cs;
+    }
+  }
+  if (a.pw3) {
+#pragma unroll 1
+    for (int j = tid; j < nm; j += nt) {                       // one column of d3 per thread, all rows
+      T dv[32];
+#pragma unroll
+      for (int r = 0; r < 32; ++r) dv[r] = a.d3[(size_t)(m0 + min(r, rows - 1)) * nm + j];
+#pragma unroll 1
+      for (int o = 0; o < N; ++o) {
+        T sacc = T(0);
+#pragma unroll
+        for (int r = 0; r < 32; ++r) sacc += zt[r * zs + o] * dv[r];   // rows past M: gz = 0
+        a.pw3[(size_t)blk * N * nm + (size_t)o * nm + j] = sacc;
+      }
+    }
+  }
+}
+
+template <typename T, int EPI>
+__device__ inline void mm_epilogue(const MMArgs<T>& a, int m, int n, T v) {
+  const size_t i = (size_t)m * a.ldc + n;
+  if constexpr (EPI == MM_STORE) {
+    a.C[i] = v;
+  } else if constexpr (EPI == MM_L2) {                          // mlp.py:30-31
+    const T t = (v + a.bias[n]) * mval(a.ms, 1, i);
+    const T h = t > T(0) ? t : T(0);
+    a.C[i] = h;
+    a.C2[i] = h * mval(a.ms, 2, i);
+  } else if constexpr (EPI == MM_UPD) {
+    apply_upd(a.u, a.upd_mode, i, v);
+  }
+}
 
 template <typename T, int EPI, int AOP, int BOP, int TA, int TB, int AV, int BV>
-__global__ __launch_bounds__(MM_NW * 64) void k_mm(MMArgs<T> a) {
+__global__ __launch_bounds__(MM_NT) void k_mm(MMArgs<T> a) {
   using M = mfma16<T>;
   __shared__ T red[MM_NW][32][33];
   __shared__ double rowl[32];
+  run_pending(a.pend);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lg = lane >> 4;
   const int m0 = blockIdx.x * 32, n0 = blockIdx.y * 32;
   const int Kq = ((a.K + 16 * MM_NW - 1) / (16 * MM_NW)) * 16;   // k range per wave (multiple of 16)
@@ -212,8 +378,8 @@ __global__ __launch_bounds__(MM_NW * 64) void k_mm(MMArgs<T> a) {
   // three chunks in flight (register ring), then one MFMA batch per chunk
   T av[3][4][2], bv[3][4][2];
   auto load = [&](int s, int k0) {
-    load_chunk<T, AOP, TA, AV>(av[s], a.A, a.lda, m0, a.M, k0, ke, lr, lg, a.ms);
-    load_chunk<T, BOP, !TB, BV>(bv[s], a.B, a.ldb, n0, a.N, k0, ke, lr, lg, a.ms);
+    load_chunk<T, AOP, TA, AV>(av[s], a.A, a.lda, m0, a.M, k0, ke, lr, lg, a.ms, a.b1);
+    load_chunk<T, BOP, !TB, BV>(bv[s], a.B, a.ldb, n0, a.N, k0, ke, lr, lg, a.ms, a.b1);
   };
   auto mfma = [&](int s) {
 #pragma unroll
@@ -246,75 +412,63 @@ __global__ __launch_bounds__(MM_NW * 64) void k_mm(MMArgs<T> a) {
       for (int q = 0; q < 4; ++q) red[wave][16 * i + M::row(lane, q)][16 * j + lr] = acc[i][j][q];
   __syncthreads();
 #pragma unroll
-  for (int u = 0; u < 1024 / (MM_NW * 64); ++u) {
-    const int e = tid + MM_NW * 64 * u, mm = e >> 5, nn = e & 31;
+  for (int u = 0; u < 1024 / MM_NT; ++u) {
+    const int e = tid + MM_NT * u, mm = e >> 5, nn = e & 31;
     const int m = m0 + mm, n = n0 + nn;
     T v = red[0][mm][nn];
 #pragma unroll
     for (int w = 1; w < MM_NW; ++w) v += red[w][mm][nn];
     if constexpr (EPI == MM_L3CE) {
       red[0][mm][nn] = (n < a.N) ? v + a.bias[n] : T(0);     // logits of the block (one writer each)
+    } else if constexpr (EPI == MM_GA1) {                      // (ga2·W2)·[(xw + b1)·m0 > 0]·m0
+      T g = T(0);
+      if (m < a.M && n < a.N) {
+        const size_t i = (size_t)m * a.ldc + n;
+        const T m0v = mval(a.ms, 0, i);
+        g = (v * ((a.H[i] + a.b1[n]) * m0v > T(0) ? T(1) : T(0))) * m0v;
+        a.C[i] = g;
+      }
+      red[0][mm][nn] = g;
     } else {
       if (m < a.M && n < a.N) mm_epilogue<T, EPI>(a, m, n, v);
     }
   }
   if constexpr (EPI == MM_L3CE) {
     __syncthreads();
-    ce_rows<T>(red[0], rowl, m0, a.M, a.N, a.y, a.C, a.ldc, a.lpart, blockIdx.x);
+    ce_rows<T>(&red[0][0][0], 33, rowl, m0, a.M, a.N, a.y, a.C, a.ldc, a.lpart, blockIdx.x);
+    __syncthreads();
+    l3_backward<T>(a, &red[0][0][0], 33, m0, blockIdx.x, &red[1][0][0], (MM_NW - 1) * 32 * 33);
   }
-}
-
-// Cross-entropy for n_out > 32 (logits z already stored): one 32-row block per workgroup.
-template <typename T>
-__global__ __launch_bounds__(256) void k_mlp_ce(const T* z, const int32_t* y, int B, int K, T* gz, double* lpart) {
-  __shared__ double rowl[32];
-  const int t = threadIdx.x, m0 = blockIdx.x * 32;
-  if (t < 32) {
-    const int m = m0 + t;
-    double l = 0.0;
-    if (m < B) {
-      const T* zr = z + (size_t)m * K;
-      T mx = zr[0];
-      for (int k = 1; k < K; ++k) mx = zr[k] > mx ? zr[k] : mx;
-      T s = T(0);
-      for (int k = 0; k < K; ++k) s += exp(zr[k] - mx);
-      const T ls = log(s);
-      const int lab = y[m];
-      l = -(double)((zr[lab] - mx) - ls);
-      for (int k = 0; k < K; ++k) {
-        T g = exp((zr[k] - mx) - ls);
-        if (k == lab) g -= T(1);
-        gz[(size_t)m * K + k] = g / (T)B;
+  if constexpr (EPI == MM_GA1) {
+    if (a.colpart) {
+      __syncthreads();
+      if (tid < 32 && n0 + tid < a.N) {
+        T s = T(0);
+        for (int r = 0; r < 32; ++r) s += red[0][r][tid];
+        a.colpart[(size_t)blockIdx.x * a.ldc + n0 + tid] = s;
       }
     }
-    rowl[t] = l;
-  }
-  __syncthreads();
-  if (t == 0) {
-    double s = 0.0;
-    for (int r = 0; r < 32; ++r) s += rowl[r];
-    lpart[blockIdx.x] = s;
   }
 }
 
-// Bias gradient Σ_rows g[m][n] (rows split over 8 groups, fixed combine order) + epilogue at (0, n).
-template <typename T, int EPI>
-__global__ __launch_bounds__(256) void k_colsum(const T* g, int rows, int N, MMArgs<T> a) {
-  __shared__ T part[8][32];
-  const int c = threadIdx.x & 31, grp = threadIdx.x >> 5, n = blockIdx.x * 32 + c;
-  T s = T(0);
-  if (n < N) {
-#pragma unroll 4
-    for (int m = grp; m < rows; m += 8) s += g[(size_t)m * N + n];
+// Layer 3 for n_out > 32: xw-free logits d3·W3ᵀ already stored in z; one 32-row block per
+// workgroup, rows (+ b3) staged in dynamic LDS, then the same cross-entropy and layer-3 backward.
+template <typename T>
+__global__ __launch_bounds__(MM_NT) void k_l3_wide(MMArgs<T> a, const T* z) {
+  extern __shared__ unsigned char dsm[];
+  double* rowl = reinterpret_cast<double*>(dsm);
+  T* scr = reinterpret_cast<T*>(dsm + 32 * sizeof(double));
+  T* zt = scr + MM_NT;
+  const int N = a.N, zs = N + 1, m0 = blockIdx.x * 32;
+  run_pending(a.pend);
+  for (int e = threadIdx.x; e < 32 * N; e += blockDim.x) {
+    const int r = e / N, k = e - r * N;
+    zt[r * zs + k] = (m0 + r < a.M) ? z[(size_t)(m0 + r) * N + k] + a.bias[k] : T(0);
   }
-  part[grp][c] = s;
   __syncthreads();
-  if (grp == 0 && n < N) {
-    T t = part[0][c];
-#pragma unroll
-    for (int j = 1; j < 8; ++j) t += part[j][c];
-    mm_epilogue<T, EPI>(a, 0, n, t);
-  }
+  ce_rows<T>(zt, zs, rowl, m0, a.M, N, a.y, a.C, a.ldc, a.lpart, blockIdx.x);
+  __syncthreads();
+  l3_backward<T>(a, zt, zs, m0, blockIdx.x, scr, MM_NT);
 }
 
 // Keep flags of F forwards (blockIdx.y = forward f, Philox slot MASK_SLOT0 + f), 3·mn per forward.
@@ -340,6 +494,12 @@ __global__ void k_mlp_masks(T* masks, int n3, uint64_t seed, uint32_t chain, uin
 #pragma unroll
   for (int q = 0; q < 4; ++q)
     if (4 * g + q < n3) masks[4 * g + q] = keep_flag(r.v[q]) ? scale : T(0);
+}
+
+template <typename T>
+__global__ void k_bias_into_z(T* z, const T* b, int n, int N) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) z[i] = z[i] + b[i % N];
 }
 
 // Six variables in the caller's order (position i of `order`).
@@ -466,13 +626,20 @@ __global__ void k_loss_final(const double* lpart, int nlb, int B, double* out) {
 // ------------------------------------------------------------------ host side
 namespace {
 
+inline bool vec_ok(const void* p, int ld, int elt) {
+  return ((uintptr_t)p % 16 == 0) && ((size_t)ld * elt) % 16 == 0;
+}
+
 template <typename T>
 struct MlpNet {
   int B, n_in, n_mid, n_out, nlb;
   const T* X; const int32_t* y;
-  T *a1, *h2, *d3, *z, *gz, *ga2, *ga1;
+  T *xw, *h2, *d3, *z, *gz, *ga2, *ga1;
+  T *pb1, *pb2, *pb3, *pw3;              // gradient partials of b1, b2, b3, W3 ([nlb][...])
   hipStream_t st;
-  bool a1_valid = false;
+  bool xw_valid = false;
+  bool vec_masks = true;                 // masks may be read as 4-/2-element vectors
+  Pending<T> pend{};                     // consumed by the next launch
   int nvar(int v) const {
     switch (v) {
       case 0: return n_mid * n_in;  case 1: return n_mid;
@@ -482,17 +649,23 @@ struct MlpNet {
   }
 };
 
-inline bool vec_ok(const void* p, int ld, int elt) {
-  return ((uintptr_t)p % 16 == 0) && ((size_t)ld * elt) % 16 == 0;
+template <typename T>
+void net_init(MlpNet<T>& net, int B, int n_in, int n_mid, int n_out, hipStream_t st) {
+  net.B = B; net.n_in = n_in; net.n_mid = n_mid; net.n_out = n_out; net.nlb = (B + 31) / 32; net.st = st;
+  net.vec_masks = n_mid % 4 == 0;
 }
 
 // Launch k_mm for a call site with compile-time operand layouts (TA: A stored [K][M], TB: B stored
-// [N][K]); k-contiguous operands take the 16-byte vector path when aligned.
+// [N][K]); k-contiguous operands take the 16-byte vector path when aligned.  Takes the pending update.
 template <typename T, int EPI, int TA, int TB, int AOP = OP_PLAIN, int BOP = OP_PLAIN>
-hipError_t mm(const MMArgs<T>& a, hipStream_t st) {
+hipError_t mm(MlpNet<T>& net, MMArgs<T>& a) {
   if (a.ta != TA || a.tb != TB) return hipErrorInvalidValue;
-  dim3 grid((a.M + 31) / 32, (a.N + 31) / 32), blk(MM_NW * 64);
-  const bool av = !TA && vec_ok(a.A, a.lda, sizeof(T)), bv = TB && vec_ok(a.B, a.ldb, sizeof(T));
+  a.pend = net.pend;
+  net.pend.mode = UPD_NONE;
+  dim3 grid((a.M + 31) / 32, (a.N + 31) / 32), blk(MM_NT);
+  const bool h1ok = AOP != OP_H1 || net.vec_masks;
+  const bool av = !TA && h1ok && vec_ok(a.A, a.lda, sizeof(T)), bv = TB && vec_ok(a.B, a.ldb, sizeof(T));
+  hipStream_t st = net.st;
   if (av && bv) hipLaunchKernelGGL((k_mm<T, EPI, AOP, BOP, TA, TB, !TA, TB>), grid, blk, 0, st, a);
   else if (av) hipLaunchKernelGGL((k_mm<T, EPI, AOP, BOP, TA, TB, !TA, 0>), grid, blk, 0, st, a);
   else if (bv) hipLaunchKernelGGL((k_mm<T, EPI, AOP, BOP, TA, TB, 0, TB>), grid, blk, 0, st, a);
@@ -505,88 +678,113 @@ void mm_set(MMArgs<T>& a, int M, int N, int K, const T* A, int lda, int ta, cons
   a.M = M; a.N = N; a.K = K; a.A = A; a.lda = lda; a.ta = ta; a.B = B; a.ldb = ldb; a.tb = tb; a.C = C; a.ldc = ldc;
 }
 
-// Forward with masks `ms` at parameters q; loss partials into lpart.  Layer 1 only when a1 is stale.
+// What the layer-3 kernel produces besides the loss
+struct L3Want { bool ga2, pb2, pb3, pw3; };
+
+// Forward with masks `ms` at parameters q (+ the requested layer-3 backward pieces); loss partials
+// into lpart (null: no loss); logits (optional) stored without b3.  Layer 1 only when xw is stale.
 template <typename T>
-hipError_t mlp_forward(MlpNet<T>& net, T* const* q, const MaskSrc<T>& ms, double* lpart, T* logits = nullptr) {
+hipError_t mlp_forward(MlpNet<T>& net, T* const* q, const MaskSrc<T>& ms, double* lpart, L3Want w,
+                       T* logits = nullptr) {
   const int B = net.B, nm = net.n_mid;
   hipError_t e;
-  if (!net.a1_valid) {                                        // a1 = X·W1ᵀ + b1
+  if (!net.xw_valid) {                                        // xw = X·W1ᵀ
     MMArgs<T> a{};
-    mm_set<T>(a, B, nm, net.n_in, net.X, net.n_in, 0, q[0], net.n_in, 1, net.a1, nm);
-    a.bias = q[1];
-    if ((e = mm<T, MM_BIAS, 0, 1>(a, net.st))) return e;
-    net.a1_valid = true;
+    mm_set<T>(a, B, nm, net.n_in, net.X, net.n_in, 0, q[0], net.n_in, 1, net.xw, nm);
+    if ((e = mm<T, MM_STORE, 0, 1>(net, a))) return e;
+    net.xw_valid = true;
   }
-  {                                                           // h2, d3 from h1 = max(a1·m0, 0) on the fly
+  {                                                           // h2, d3 from h1 = max((xw + b1)·m0, 0)
     MMArgs<T> a{};
-    mm_set<T>(a, B, nm, nm, net.a1, nm, 0, q[2], nm, 1, net.h2, nm);
-    a.bias = q[3]; a.ms = ms; a.C2 = net.d3;
-    if ((e = mm<T, MM_L2, 0, 1, OP_H1>(a, net.st))) return e;
+    mm_set<T>(a, B, nm, nm, net.xw, nm, 0, q[2], nm, 1, net.h2, nm);
+    a.bias = q[3]; a.b1 = q[1]; a.ms = ms; a.C2 = net.d3;
+    if ((e = mm<T, MM_L2, 0, 1, OP_H1>(net, a))) return e;
   }
   if (logits) {
     MMArgs<T> a{};
     mm_set<T>(a, B, net.n_out, nm, net.d3, nm, 0, q[4], nm, 1, logits, net.n_out);
-    a.bias = q[5];
-    if ((e = mm<T, MM_BIAS, 0, 1>(a, net.st))) return e;
+    if ((e = mm<T, MM_STORE, 0, 1>(net, a))) return e;
   }
   if (!lpart) return hipSuccess;
   MMArgs<T> a{};
-  if (net.n_out <= 32) {                                      // z and the cross-entropy in one kernel
+  a.bias = q[5]; a.y = net.y; a.lpart = lpart; a.ms = ms;
+  a.W3 = q[4]; a.h2 = net.h2; a.d3 = net.d3; a.n_mid = nm;
+  a.ga2 = w.ga2 ? net.ga2 : nullptr;
+  a.pb2 = w.pb2 ? net.pb2 : nullptr;
+  a.pb3 = w.pb3 ? net.pb3 : nullptr;
+  a.pw3 = w.pw3 ? net.pw3 : nullptr;
+  if (net.n_out <= 32) {                                      // z, cross-entropy, layer-3 backward
     mm_set<T>(a, B, net.n_out, nm, net.d3, nm, 0, q[4], nm, 1, net.gz, net.n_out);
-    a.bias = q[5]; a.y = net.y; a.lpart = lpart;
-    return mm<T, MM_L3CE, 0, 1>(a, net.st);
+    return mm<T, MM_L3CE, 0, 1>(net, a);
   }
-  mm_set<T>(a, B, net.n_out, nm, net.d3, nm, 0, q[4], nm, 1, net.z, net.n_out);
-  a.bias = q[5];
-  if ((e = mm<T, MM_BIAS, 0, 1>(a, net.st))) return e;
-  hipLaunchKernelGGL(k_mlp_ce<T>, dim3(net.nlb), dim3(256), 0, net.st, net.z, net.y, B, net.n_out, net.gz, lpart);
+  {
+    MMArgs<T> az{};
+    mm_set<T>(az, B, net.n_out, nm, net.d3, nm, 0, q[4], nm, 1, net.z, net.n_out);
+    if ((e = mm<T, MM_STORE, 0, 1>(net, az))) return e;       // d3·W3ᵀ; b3 is added in k_l3_wide
+  }
+  a.M = B; a.N = net.n_out; a.C = net.gz; a.ldc = net.n_out;
+  a.pend = net.pend;
+  net.pend.mode = UPD_NONE;
+  const size_t lds = 32 * sizeof(double) + ((size_t)MM_NT + (size_t)32 * (net.n_out + 1)) * sizeof(T);
+  hipLaunchKernelGGL(k_l3_wide<T>, dim3(net.nlb), dim3(MM_NT), lds, net.st, a, (const T*)net.z);
   return hipGetLastError();
 }
 
 template <typename T>
-hipError_t mlp_ga2(MlpNet<T>& net, T* const* q, const MaskSrc<T>& ms) {
-  MMArgs<T> a{};
-  mm_set<T>(a, net.B, net.n_mid, net.n_out, net.gz, net.n_out, 0, q[4], net.n_mid, 0, net.ga2, net.n_mid);
-  a.ms = ms; a.H = net.h2;
-  return mm<T, MM_GA2, 0, 0>(a, net.st);
-}
-template <typename T>
-hipError_t mlp_ga1(MlpNet<T>& net, T* const* q, const MaskSrc<T>& ms) {
+hipError_t mlp_ga1(MlpNet<T>& net, T* const* q, const MaskSrc<T>& ms, bool want_pb1) {
   MMArgs<T> a{};
   mm_set<T>(a, net.B, net.n_mid, net.n_mid, net.ga2, net.n_mid, 0, q[2], net.n_mid, 0, net.ga1, net.n_mid);
-  a.ms = ms; a.H = net.a1;
-  return mm<T, MM_GA1, 0, 0>(a, net.st);
+  a.ms = ms; a.H = net.xw; a.b1 = q[1];
+  a.colpart = want_pb1 ? net.pb1 : nullptr;
+  return mm<T, MM_GA1, 0, 0>(net, a);
 }
 
-// Gradient of variable v into the epilogue `a` (GRAD: a.C = output; SGHMC: a.P / a.Qn / noise).
-template <typename T, int EPI>
-hipError_t mlp_var_grad(MlpNet<T>& net, const MaskSrc<T>& ms, int v, MMArgs<T> a) {
+// Weight gradient of W1 / W2 through the k_mm epilogue (biases and W3 come from partials).
+template <typename T>
+hipError_t mlp_wgrad(MlpNet<T>& net, T* const* q, const MaskSrc<T>& ms, int v, int mode, const Upd<T>& u) {
   const int B = net.B, nm = net.n_mid;
-  T* out = a.C;
-  switch (v) {
-    case 4: mm_set<T>(a, net.n_out, nm, B, net.gz, net.n_out, 1, net.d3, nm, 0, out, nm);      // gzᵀ·d3
-            return mm<T, EPI, 1, 0>(a, net.st);
-    case 2: mm_set<T>(a, nm, nm, B, net.ga2, nm, 1, net.a1, nm, 0, out, nm);                   // ga2ᵀ·h1
-            a.ms = ms;
-            return mm<T, EPI, 1, 0, OP_PLAIN, OP_H1>(a, net.st);
-    case 0: mm_set<T>(a, nm, net.n_in, B, net.ga1, nm, 1, net.X, net.n_in, 0, out, net.n_in);  // ga1ᵀ·X
-            return mm<T, EPI, 1, 0>(a, net.st);
-    default: {                                                 // biases: Σ_rows of gz / ga2 / ga1
-      const T* g = v == 5 ? net.gz : (v == 3 ? net.ga2 : net.ga1);
-      const int N = v == 5 ? net.n_out : nm;
-      a.ldc = N;
-      hipLaunchKernelGGL((k_colsum<T, EPI>), dim3((N + 31) / 32), dim3(256), 0, net.st, g, B, N, a);
-      return hipGetLastError();
-    }
+  MMArgs<T> a{};
+  a.upd_mode = mode; a.u = u;
+  if (v == 2) {                                               // ga2ᵀ·h1
+    mm_set<T>(a, nm, nm, B, net.ga2, nm, 1, net.xw, nm, 0, nullptr, nm);
+    a.ms = ms; a.b1 = q[1];
+    return mm<T, MM_UPD, 1, 0, OP_PLAIN, OP_H1>(net, a);
   }
+  mm_set<T>(a, nm, net.n_in, B, net.ga1, nm, 1, net.X, net.n_in, 0, nullptr, net.n_in);   // ga1ᵀ·X
+  return mm<T, MM_UPD, 1, 0>(net, a);
+}
+
+template <typename T>
+void set_pending(MlpNet<T>& net, int v, int mode, const Upd<T>& u) {
+  Pending<T>& p = net.pend;
+  p.mode = mode; p.u = u; p.nparts = net.nlb;
+  switch (v) {
+    case 1: p.part = net.pb1; p.n = net.n_mid; break;
+    case 3: p.part = net.pb2; p.n = net.n_mid; break;
+    case 4: p.part = net.pw3; p.n = net.n_out * net.n_mid; break;
+    default: p.part = net.pb3; p.n = net.n_out; break;
+  }
+}
+
+template <typename T>
+hipError_t flush_pending(MlpNet<T>& net) {
+  if (net.pend.mode == UPD_NONE) return hipSuccess;
+  const int n = net.pend.n;
+  hipLaunchKernelGGL(k_pending<T>, dim3((n + 255) / 256), dim3(256), 0, net.st, net.pend);
+  net.pend.mode = UPD_NONE;
+  return hipGetLastError();
 }
 
 template <typename T>
 void mlp_workspace(Workspace& ws, MlpNet<T>& net) {
   const size_t mn = (size_t)net.B * net.n_mid;
-  net.a1 = ws.take<T>(mn); net.h2 = ws.take<T>(mn); net.d3 = ws.take<T>(mn);
+  net.xw = ws.take<T>(mn); net.h2 = ws.take<T>(mn); net.d3 = ws.take<T>(mn);
   net.ga2 = ws.take<T>(mn); net.ga1 = ws.take<T>(mn);
   net.z = ws.take<T>((size_t)net.B * net.n_out); net.gz = ws.take<T>((size_t)net.B * net.n_out);
+  net.pb1 = ws.take<T>((size_t)net.nlb * net.n_mid);
+  net.pb2 = ws.take<T>((size_t)net.nlb * net.n_mid);
+  net.pb3 = ws.take<T>((size_t)net.nlb * net.n_out);
+  net.pw3 = ws.take<T>((size_t)net.nlb * net.n_out * net.n_mid);
 }
 
 }  // namespace
@@ -605,24 +803,28 @@ template <typename T>
 int mlp_grad_t(hmcx_ctx* ctx, const void* X, const int32_t* y, int B, int n_in, int n_mid, int n_out,
                const hmcx_mlp_params* par, const void* masks, double alpha, hmcx_mlp_params* grads, double* loss) {
   MlpNet<T> net{};
-  net.B = B; net.n_in = n_in; net.n_mid = n_mid; net.n_out = n_out; net.nlb = (B + 31) / 32;
-  net.X = (const T*)X; net.y = y; net.st = ctx->stream;
+  net_init(net, B, n_in, n_mid, n_out, ctx->stream);
+  net.X = (const T*)X; net.y = y;
   Workspace ws(ctx);
   double* lpart;
   do { ws.reset(); mlp_workspace<T>(ws, net); lpart = ws.take<double>(net.nlb); } while (ws.retry());
   if (ws.failed) return HMCX_ENOMEM;
   const MaskSrc<T> ms{(const T*)masks, nullptr, T(1), B * n_mid};
+  if (masks && (uintptr_t)masks % 16) net.vec_masks = false;
   T* q[6];
   for (int v = 0; v < 6; ++v) q[v] = (T*)par->p[v];
-  HMCX_HIP(ctx, mlp_forward<T>(net, q, ms, lpart));
-  HMCX_HIP(ctx, mlp_ga2<T>(net, q, ms));
-  HMCX_HIP(ctx, mlp_ga1<T>(net, q, ms));
-  MMArgs<T> a{};
-  a.half_alpha = (T)(0.5 * alpha);
-  for (int v = 0; v < 6; ++v) {
-    a.C = (T*)grads->p[v];
-    a.W = q[v];
-    HMCX_HIP(ctx, (mlp_var_grad<T, MM_GRAD>(net, ms, v, a)));
+  HMCX_HIP(ctx, mlp_forward<T>(net, q, ms, lpart, L3Want{true, true, true, true}));
+  HMCX_HIP(ctx, mlp_ga1<T>(net, q, ms, true));
+  Upd<T> u{};
+  u.half_alpha = (T)(0.5 * alpha);
+  for (int v : {0, 2}) {
+    u.W = q[v]; u.G = (T*)grads->p[v];
+    HMCX_HIP(ctx, mlp_wgrad<T>(net, q, ms, v, UPD_GRAD, u));
+  }
+  for (int v : {1, 3, 4, 5}) {
+    u.W = q[v]; u.G = (T*)grads->p[v];
+    set_pending(net, v, UPD_GRAD, u);
+    HMCX_HIP(ctx, flush_pending(net));
   }
   if (loss) {
     hipLaunchKernelGGL(k_loss_final, dim3(1), dim3(1), 0, ctx->stream, lpart, net.nlb, B, loss);
@@ -635,16 +837,22 @@ template <typename T>
 int mlp_loss_t(hmcx_ctx* ctx, const void* X, const int32_t* y, int B, int n_in, int n_mid, int n_out,
                const hmcx_mlp_params* par, const void* masks, double* loss, void* logits) {
   MlpNet<T> net{};
-  net.B = B; net.n_in = n_in; net.n_mid = n_mid; net.n_out = n_out; net.nlb = (B + 31) / 32;
-  net.X = (const T*)X; net.y = y; net.st = ctx->stream;
+  net_init(net, B, n_in, n_mid, n_out, ctx->stream);
+  net.X = (const T*)X; net.y = y;
   Workspace ws(ctx);
   double* lpart;
   do { ws.reset(); mlp_workspace<T>(ws, net); lpart = ws.take<double>(net.nlb); } while (ws.retry());
   if (ws.failed) return HMCX_ENOMEM;
   const MaskSrc<T> ms{(const T*)masks, nullptr, T(1), B * n_mid};
+  if (masks && (uintptr_t)masks % 16) net.vec_masks = false;
   T* q[6];
   for (int v = 0; v < 6; ++v) q[v] = (T*)par->p[v];
-  HMCX_HIP(ctx, mlp_forward<T>(net, q, ms, y ? lpart : nullptr, (T*)logits));
+  HMCX_HIP(ctx, mlp_forward<T>(net, q, ms, y ? lpart : nullptr, L3Want{false, false, false, false}, (T*)logits));
+  if (logits) {
+    const int n = B * n_out;
+    hipLaunchKernelGGL(k_bias_into_z<T>, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, (T*)logits, q[5], n, n_out);
+    HMCX_HIP(ctx, hipGetLastError());
+  }
   if (y && loss) {
     hipLaunchKernelGGL(k_loss_final, dim3(1), dim3(1), 0, ctx->stream, lpart, net.nlb, B, loss);
     HMCX_HIP(ctx, hipGetLastError());
@@ -655,21 +863,20 @@ int mlp_loss_t(hmcx_ctx* ctx, const void* X, const int32_t* y, int B, int n_in, 
 template <typename T>
 int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
   MlpNet<T> net{};
-  net.B = s->B; net.n_in = s->n_in; net.n_mid = s->n_mid; net.n_out = s->n_out; net.st = ctx->stream;
-  net.nlb = (s->B + 31) / 32;
+  net_init(net, s->B, s->n_in, s->n_mid, s->n_out, ctx->stream);
   const int mn = s->B * s->n_mid, n3 = 3 * mn;
   int off_v[6], dim[6], P = 0;                                // element offset of each variable in `order`
-  for (int i = 0; i < 6; ++i) {
-    const int v = s->order[i];
-    if (v < 0 || v > 5) return set_error(ctx, HMCX_EINVAL, "mlp sghmc: order must be a permutation of 0..5");
-    off_v[v] = P;
-    dim[v] = net.nvar(v);
-    P += dim[v];
-  }
   {
     int seen = 0;
-    for (int i = 0; i < 6; ++i) seen |= 1 << s->order[i];
-    if (seen != 63) return set_error(ctx, HMCX_EINVAL, "mlp sghmc: order must be a permutation of 0..5");
+    for (int i = 0; i < 6; ++i) {
+      const int v = s->order[i];
+      if (v < 0 || v > 5 || ((seen >> v) & 1))
+        return set_error(ctx, HMCX_EINVAL, "mlp sghmc: order must be a permutation of 0..5");
+      seen |= 1 << v;
+      off_v[v] = P;
+      dim[v] = net.nvar(v);
+      P += dim[v];
+    }
   }
   int maxF = 2;
   for (int si = 0; si < s->n_steps; ++si) {
@@ -677,6 +884,13 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
     maxF = std::max(maxF, 6 * s->n_iter[si] + 2);
   }
   const bool philox_masks = s->mask_mode == HMCX_NOISE_PHILOX;
+  if (philox_masks) {
+    if (n3 % 4) net.vec_masks = false;
+  } else {
+    if ((uintptr_t)s->masks % 16 || ((size_t)n3 * sizeof(T)) % 16) net.vec_masks = false;
+    for (int si = 0; si < s->n_steps; ++si)
+      if ((s->mask_off[si] * sizeof(T)) % 16) net.vec_masks = false;
+  }
   Workspace ws(ctx);
   T *pv[6], *qa[6], *qb[6];
   double *part_cur, *part_new, *lp_cur, *lp_new, *lp_scr;
@@ -709,7 +923,7 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
   for (int si = 0; si < s->n_steps; ++si) {
     net.X = Xall + (size_t)s->row0[si] * s->n_in;
     net.y = s->y + s->row0[si];
-    net.a1_valid = false;
+    net.xw_valid = false;
     const double eps = s->eps[si];
     const int n = s->n_iter[si], F = 6 * n + 2;
     const uint32_t step_id = s->step_base + (uint32_t)si;
@@ -737,27 +951,29 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
       for (int i = 0; i < 6; ++i) {
         const int v = s->order[i];
         cur[v] = (it & 1) ? qb[v] : qa[v];                    // drifted position of this iteration
-        if (v <= 1) net.a1_valid = false;
+        if (v == 0) net.xw_valid = false;
         const MaskSrc<T> ms = masks_for(fwd++);
-        HMCX_HIP(ctx, mlp_forward<T>(net, cur, ms, lp_scr));
-        if (v <= 3) HMCX_HIP(ctx, mlp_ga2<T>(net, cur, ms));
-        if (v <= 1) HMCX_HIP(ctx, mlp_ga1<T>(net, cur, ms));
-        MMArgs<T> a{};
-        a.W = cur[v]; a.P = pv[v];
-        a.Qn = it + 1 < n ? ((it & 1) ? qa[v] : qb[v]) : nullptr;
-        a.half_alpha = (T)(0.5 * s->alpha); a.eps = (T)eps; a.one_minus_eps = (T)(1.0 - eps);
-        a.noise_scale = (T)(2.0 * eps);
-        a.noise_mode = s->noise_mode;
-        a.noise = nz ? nz + (size_t)P * (it + 1) + off_v[v] : nullptr;   // BUFFER: one block of P per iteration
-        a.seed = s->seed; a.chain = s->chain; a.step = step_id; a.slot = (uint32_t)(it + 1);
-        a.e0 = (uint32_t)off_v[v];
-        HMCX_HIP(ctx, (mlp_var_grad<T, MM_SGHMC>(net, ms, v, a)));
+        Upd<T> u{};
+        u.W = cur[v]; u.P = pv[v];
+        u.Qn = it + 1 < n ? ((it & 1) ? qa[v] : qb[v]) : nullptr;
+        u.half_alpha = (T)(0.5 * s->alpha); u.eps = (T)eps; u.one_minus_eps = (T)(1.0 - eps);
+        u.noise_scale = (T)(2.0 * eps);
+        u.noise_mode = s->noise_mode;
+        u.noise = nz ? nz + (size_t)P * (it + 1) + off_v[v] : nullptr;   // BUFFER: one block of P per iteration
+        u.seed = s->seed; u.chain = s->chain; u.step = step_id; u.slot = (uint32_t)(it + 1);
+        u.e0 = (uint32_t)off_v[v];
+        const L3Want w{v <= 3, v == 3, v == 5, v == 4};
+        HMCX_HIP(ctx, mlp_forward<T>(net, cur, ms, lp_scr, w));
+        if (v <= 1) HMCX_HIP(ctx, mlp_ga1<T>(net, cur, ms, v == 1));
+        if (v == 0 || v == 2) HMCX_HIP(ctx, mlp_wgrad<T>(net, cur, ms, v, UPD_SGHMC, u));
+        else set_pending(net, v, UPD_SGHMC, u);
       }
     }
     // energies (hmc.py:67-71: E_new first, then E_current), each with fresh masks
-    HMCX_HIP(ctx, mlp_forward<T>(net, cur, masks_for(fwd++), lp_new));
-    net.a1_valid = false;
-    HMCX_HIP(ctx, mlp_forward<T>(net, par, masks_for(fwd++), lp_cur));
+    HMCX_HIP(ctx, mlp_forward<T>(net, cur, masks_for(fwd++), lp_new, L3Want{false, false, false, false}));
+    net.xw_valid = false;
+    HMCX_HIP(ctx, mlp_forward<T>(net, par, masks_for(fwd++), lp_cur, L3Want{false, false, false, false}));
+    HMCX_HIP(ctx, flush_pending(net));
     VarTab ve{};
     for (int i = 0; i < 6; ++i) {
       const int v = s->order[i];
