@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline time budget (0 = skip)")
     ap.add_argument("--batched-chains", type=int, default=1024,
                     help="chains per GPU of the secondary chain-batched measurement (0 = skip)")
+    ap.add_argument("--mlp-steps", type=int, default=40,
+                    help="SGHMC steps of the secondary config-3 MLP measurement (0 = skip)")
     return ap.parse_args()
 
 
@@ -152,6 +154,70 @@ def batched_chains(model, X, Y, data, C, n_steps, rank):
                          "device_ms": kms, "flop": FLOP_PER_LEAPFROG * lf}}
 
 
+MLP_SHAPE = (784, 256, 10)                   # MyNetwork(784, 256, 10): two hidden layers (mlp.py:24-26)
+MLP_P = 256 * 784 + 256 + 256 * 256 + 256 + 10 * 256 + 10          # 269,322
+MLP_FLOP_PER_LEAPFROG = 1.0193e9             # SURVEY §8d "M": minimal-recompute schedule, B = 500
+
+
+def mlp_measure(X, lab, n_steps, rank, cpu_seconds):
+    """Secondary measurement, BASELINE config 3: MNIST MLP 784-256-256-10 SGHMC, batch 500, one
+    chain, float32 (Chainer's default dtype), device Philox noise and dropout masks, through the
+    fused hmcx_mlp_sghmc_run.  CPU baseline: the oracle's mlp.grad (NumPy float32) six times
+    per leapfrog — the reference's per-sub-step full gradient (sghmc.py:29-34)."""
+    import torch
+    from dropout_hamiltonian_montecarlo_amd.hamiltonian.models.gpu.mlp import mlp
+    from dropout_hamiltonian_montecarlo_amd.hamiltonian.inference.gpu.sghmc import sghmc
+    m = mlp({"alpha": ALPHA}, *MLP_SHAPE, dtype=torch.float32)
+    s = sghmc(m, m.init_params(1), path_length=5e-3, step_size=EPS, noise="philox", seed=11, chain=rank)
+    s.out = io.StringIO()
+    state = s._init_state()
+    Xd = torch.as_tensor(X).to(m.device, torch.float32).contiguous()
+    yd = torch.as_tensor(lab).to(m.device, torch.int32).contiguous()
+    nb = N_DATA // B
+    rows = [(i % nb) * B for i in range(n_steps)]
+    s.trace = []
+    s._run(state, (Xd, yd), rows[:2], [EPS] * 2, None, B)       # warm-up
+    torch.cuda.synchronize()
+    s.trace = []
+    m.ctx.set_timing(True)
+    t0 = time.perf_counter()
+    res = s._run(state, (Xd, yd), rows, [EPS] * n_steps, None, B)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    kms, _ = m.ctx.get_timing()
+    m.ctx.set_timing(False)
+    lf = float(sum(max(0.0, t["L"] - 1) for t in s.trace))
+    achieved = MLP_FLOP_PER_LEAPFROG * lf / (kms * 1e-3) / 1e12
+    out = {"workload": "MNIST MLP 784-256-256-10 SGHMC, batch 500, 1 chain (BASELINE config 3)",
+           "dtype": "f32", "param_dim": MLP_P, "steps": n_steps, "leapfrogs": lf,
+           "leapfrogs_per_s": lf / dt, "value": lf / dt * MLP_P, "unit": "leapfrog-steps/s x param-dim",
+           "accept_rate": float(np.mean(res.accepted)),
+           "roofline": {"bound": "mfma", "achieved": achieved, "peak": MFMA_PEAK_TFLOPS["f32"], "unit": "TFLOP/s",
+                        "frac": achieved / MFMA_PEAK_TFLOPS["f32"], "device_ms": kms,
+                        "kernel": "all kernels of one hmcx_mlp_sghmc_run call (k_mm GEMMs + step kernels)",
+                        "flop_per_leapfrog": MLP_FLOP_PER_LEAPFROG}}
+    if cpu_seconds > 0:
+        from oracle import models as om
+        rs = np.random.RandomState(0)
+        ref = om.mlp({"alpha": ALPHA}, *MLP_SHAPE)
+        par = {k: v.astype(np.float32) for k, v in m.init_params(1).items()}
+        Xb, yb = X[:B].astype(np.float32), lab[:B]
+        calls, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < cpu_seconds:
+            ref.grad(par, masks=om.dropout_masks(rs, B, MLP_SHAPE[1]), X_train=Xb, y_train=yb)
+            calls += 1
+        dtc = time.perf_counter() - t0
+        lfc = calls / 6.0 / dtc
+        import threadpoolctl
+        blas = [i for i in threadpoolctl.threadpool_info() if i.get("user_api") == "blas"]
+        out["cpu_baseline"] = {"value": lfc * MLP_P, "unit": "leapfrog-steps/s x param-dim",
+                               "cores": int(max((i.get("num_threads", 1) for i in blas), default=1)), "kind": "port",
+                               "sample": "%d oracle mlp.grad calls (NumPy f32, B=500, fresh dropout masks), "
+                                         "6 per leapfrog, %.1f s" % (calls, dtc),
+                               "leapfrogs_per_s": lfc}
+    return out
+
+
 def main():
     args = parse()
     import torch
@@ -228,6 +294,11 @@ def main():
         model.ctx.set_sghmc_path(0)
         batched = batched_chains(model, X, Y, data, args.batched_chains, 24, rank)
         parallel.barrier()
+    mlp_out = None
+    if args.mlp_steps > 0:
+        lab = np.argmax(Y, axis=1)
+        mlp_out = mlp_measure(X, lab, args.mlp_steps, rank, args.cpu_seconds / 2 if world == 1 and rank == 0 else 0)
+        parallel.barrier()
     if rank != 0:
         return
     path = "persistent" if (args.path != "kernels") else "kernels"
@@ -265,6 +336,7 @@ def main():
                         "gather": "torch.distributed all_gather (%s)" % (parallel.backend_name() if world > 1 else "local")},
         "cpu_baseline": None,
         "chain_batched": batched,
+        "mlp": mlp_out,
     }
     if world == 1 and args.cpu_seconds > 0:
         out["cpu_baseline"] = cpu_baseline(X, Y, args.cpu_seconds)
