@@ -26,8 +26,25 @@ constexpr int BKC = 10;           // classes (compiled for K = 10)
 constexpr int BNT = BCT * BKC;    // 160 columns per tile
 constexpr int BRW = 32;           // rows (k_bfwd) / features (k_bgrad) per tile
 constexpr int BCH = 32;           // depth of one staged k-chunk
-constexpr int BXP = BCH + 1;      // LDS pitch of the X chunk
-constexpr int BWP = BNT + 2;      // LDS pitch of the W / diff chunk
+// LDS pitches chosen for conflict-free operand reads (bank = dword address mod 64 for ds_read_b64,
+// mod 32 for ds_read_b32; lanes 0-15 and 16-31 of a half-wave must hit disjoint banks):
+//  * k_bfwd X chunk [row][k], read down a column (16 rows × 2 k): pitch ≡ 2 (mod 32) elements;
+//  * row-contiguous reads (W / diff chunk, k_bgrad X chunks; 16 elements × 2 rows): pitch ≡ 16 (mod 32).
+constexpr int BXP = BCH + 2;      // 34: k_bfwd X chunk
+constexpr int BXPG = 48;          // k_bgrad X chunk [row][32 features]
+constexpr int BWP = BNT + 16;     // 176: W / diff chunk [k][160 columns]
+
+// XCD-grouped tile order: the 1-D grid holds 8·nX·ceil(nCT/8) blocks; blocks b, b+8, b+16, ... share
+// one XCD (round-robin dispatch), so every x tile of chain tile ct lands on XCD ct mod 8 and the
+// chain tile's operand slice (W columns / diff columns) is fetched into that XCD's L2 once.
+// Placement is a speed assumption only; any placement gives the same results.
+__device__ inline bool xcd_tile(int nX, int nCT, int& bx, int& by) {
+  const int L = blockIdx.x, x = L & 7, s = L >> 3;
+  by = x + 8 * (s / nX);
+  bx = s - (s / nX) * nX;
+  return by < nCT;
+}
+inline unsigned xcd_grid(int nX, int nCT) { return 8u * (unsigned)nX * (unsigned)((nCT + 7) / 8); }
 
 template <typename T> struct BFwdArgs {
   const T* X; const T* Y;           // minibatch rows (offset to the step's first row)
@@ -37,6 +54,7 @@ template <typename T> struct BFwdArgs {
   const int32_t* n_iter;            // [C] of this step
   const int32_t* perm;              // [C] chain of each rank (path length descending)
   T* diff;                          // [B][N]
+  int nX, nCT;                      // row tiles × chain tiles (XCD-grouped 1-D grid, xcd_tile)
   T* colsum_part;                   // [nRB][N]
   double* ll_part;                  // [nRB][C]
 };
@@ -48,6 +66,8 @@ template <typename T> struct BGradArgs {
   const int32_t* n_iter; const int32_t* perm;
   T* W; T* b; T* pW; T* pb;
   double* kin_part;                 // [nDB][C]
+  int nDB_all;                      // k_bgrad2: kin_part rows past its grid are zero-filled up to here
+  int nX, nCT;                      // feature tiles × chain tiles (XCD-grouped 1-D grid, xcd_tile)
   double* kinb;                     // [C]
   int noise_mode; const double* noise; const int64_t* noff;
   uint64_t seed; uint32_t chain0, step, slot;
@@ -94,9 +114,32 @@ __device__ inline typename StageMap<T>::v2 ld2(const T* p, bool ok, int avail) {
 }
 template <typename T> __device__ inline void st2(T* p, typename StageMap<T>::v2 v) { p[0] = v[0]; p[1] = v[1]; }
 
+// Staging map of a chain-major [chain][row][10] operand chunk (32 rows × 16 chain slots × 10 classes =
+// 2560 two-element vectors, 10 per thread): 160 consecutive vectors walk one chain's 32 contiguous
+// rows, so a wave reads 1 KB contiguous.  Source element: base + wsrc + (r0 + wr)·10; LDS
+// destination: row wr, column wls (slot·10 + class).
+struct StageCM {
+  int wr[10], wls[10];
+  size_t wsrc[10];
+  bool wok[10];
+  __device__ StageCM(int tid, const int* chs, size_t stride) {
+#pragma unroll
+    for (int u = 0; u < 10; ++u) {
+      const int j = tid + 256 * u;
+      const int cs = j / 160, w = j - cs * 160, row = w / 5, k2 = (w - row * 5) * 2, ch = chs[cs];
+      wr[u] = row;
+      wok[u] = ch >= 0;
+      wsrc[u] = (size_t)(ch >= 0 ? ch : 0) * stride + k2;
+      wls[u] = cs * BKC + k2;
+    }
+  }
+};
+
 // MT = m-tiles per wave: the tile is 32·MT minibatch rows × 16 chains (MT = 2 halves the W
 // staging per MFMA; used when enough chains are active to fill the chip).
-template <typename T, int MT>
+// CM: W is the chain-major working copy [C][D][10] (else the caller's [D][C·10]); diff is written
+// chain-major [C][B][10].
+template <typename T, int MT, int CM>
 __global__ __launch_bounds__(256) void k_bfwd(BFwdArgs<T> a) {
   using M = mfma16<T>;
   constexpr int ROWS = 32 * MT;
@@ -105,7 +148,9 @@ __global__ __launch_bounds__(256) void k_bfwd(BFwdArgs<T> a) {
   __shared__ double Lt[ROWS][BCT];
   __shared__ int chs[BCT];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lg = lane >> 4;
-  const int m0 = blockIdx.x * ROWS, rank0 = blockIdx.y * BCT;
+  int bx, by;
+  if (!xcd_tile(a.nX, a.nCT, bx, by)) return;
+  const int m0 = bx * ROWS, rank0 = by * BCT;
   const int nrow = min(ROWS, a.B - m0);
   const int D = a.D, N = a.N;
   if (tid < BCT) chs[tid] = rank0 + tid < a.c_act ? a.perm[rank0 + tid] : -1;
@@ -114,6 +159,7 @@ __global__ __launch_bounds__(256) void k_bfwd(BFwdArgs<T> a) {
   // staging: 2-element vectors; X chunk [ROWS][32 d] (2·MT per thread), W chunk
   // [32 d][16 chains × 10] = 2560 vectors (10 per thread, consecutive lanes walk one chain's row)
   StageMap<T, MT> sm(tid, chs);
+  const StageCM scm(tid, chs, (size_t)a.D * BKC);
   const T* xsrc[2 * MT];
 #pragma unroll
   for (int u = 0; u < 2 * MT; ++u) xsrc[u] = a.X + (size_t)(m0 + min(sm.xr[u], nrow - 1)) * D + sm.xc[u];
@@ -123,15 +169,23 @@ __global__ __launch_bounds__(256) void k_bfwd(BFwdArgs<T> a) {
     for (int u = 0; u < 2 * MT; ++u) xv[u] = ld2<T>(xsrc[u] + k0, sm.xr[u] < nrow, D - k0 - sm.xc[u]);
 #pragma unroll
     for (int u = 0; u < 10; ++u) {
-      const int d = k0 + sm.wr[u];
-      wv[u] = ld2<T>(a.W + (size_t)min(d, D - 1) * N + sm.wcol[u], sm.wok[u] && d < D, 2);
+      if constexpr (CM) {
+        const int d = k0 + scm.wr[u];
+        wv[u] = ld2<T>(a.W + scm.wsrc[u] + (size_t)min(d, D - 1) * BKC, scm.wok[u] && d < D, 2);
+      } else {
+        const int d = k0 + sm.wr[u];
+        wv[u] = ld2<T>(a.W + (size_t)min(d, D - 1) * N + sm.wcol[u], sm.wok[u] && d < D, 2);
+      }
     }
   };
   auto stash = [&]() {
 #pragma unroll
     for (int u = 0; u < 2 * MT; ++u) st2<T>(Xs + sm.xr[u] * BXP + sm.xc[u], xv[u]);
 #pragma unroll
-    for (int u = 0; u < 10; ++u) st2<T>(Ws + sm.wr[u] * BWP + sm.wls[u], wv[u]);
+    for (int u = 0; u < 10; ++u) {
+      if constexpr (CM) st2<T>(Ws + scm.wr[u] * BWP + scm.wls[u], wv[u]);
+      else st2<T>(Ws + sm.wr[u] * BWP + sm.wls[u], wv[u]);
+    }
   };
 
   const int wm = wave & 1, nh = wave >> 1;            // rows [16·(wm·MT + i)], 5 n-tiles per wave
@@ -209,7 +263,7 @@ __global__ __launch_bounds__(256) void k_bfwd(BFwdArgs<T> a) {
         Lt[i][cs] = ll;
         continue;
       }
-      T* drow = a.diff + (size_t)(m0 + i) * N + ch * BKC;
+      T* drow = a.diff + ((size_t)ch * a.B + (m0 + i)) * BKC;
 #pragma unroll
       for (int k = 0; k < BKC; ++k) drow[k] = y[k] - e[k] / s;
       // variant 2: bias b' = b + ε·pb (bias sub-step, sghmc.py:32 on the bias)
@@ -240,14 +294,14 @@ __global__ __launch_bounds__(256) void k_bfwd(BFwdArgs<T> a) {
   }
   if (sghmc && tid < BNT) {                            // Σ_rows (y − ŷ') of this tile
     const int cs = tid / BKC, ch = chs[cs];
-    if (ch >= 0) a.colsum_part[(size_t)blockIdx.x * N + ch * BKC + (tid - cs * BKC)] = cs_acc;
+    if (ch >= 0) a.colsum_part[(size_t)bx * N + ch * BKC + (tid - cs * BKC)] = cs_acc;
   }
   if (tid < BCT) {
     const int ch = chs[tid];
     if (ch >= 0 && (!sghmc || a.iter == a.n_iter[ch] - 1)) {
       double v = 0.0;
       for (int i = 0; i < nrow; ++i) v += Lt[i][tid];
-      a.ll_part[(size_t)blockIdx.x * a.C + ch] = v;
+      a.ll_part[(size_t)bx * a.C + ch] = v;
     }
   }
 }
@@ -258,16 +312,61 @@ __device__ inline T bnoise(const BGradArgs<T>& a, int ch, uint32_t e, const floa
   return (T)z4[e & 3];
 }
 
+// Bias sub-step of one 16-chain tile (sghmc.py:32-34 on the bias), run by the feature-tile-0
+// workgroup of k_bgrad / k_bgrad2: gradient from the colsum partials, momentum, drift, p² at the end.
+template <typename T>
+__device__ inline void bias_substep(const BGradArgs<T>& a, const int* chs, T* pbs) {
+  const int tid = threadIdx.x, D = a.D, N = a.N;
+  if (tid < BNT) {
+    const int cs = tid / BKC, k = tid - cs * BKC, ch = chs[cs];
+    T pb_new = T(0);
+    if (ch >= 0) {
+      const int col = ch * BKC + k;
+      T c = T(0);
+      for (int rb = 0; rb < a.nRB; ++rb) c += a.colsum_part[(size_t)rb * N + col];
+      const T bb = a.b[col];
+      T p = a.pb[col];
+      const T bp = bb + a.eps * p;
+      const T gr = -(c - a.alpha * bp);
+      float z4[4] = {0.f, 0.f, 0.f, 0.f};
+      const uint32_t e = (uint32_t)(D * BKC + k);
+      if (a.noise_mode != HMCX_NOISE_BUFFER) philox_normal4(a.seed, a.chain0 + ch, a.step, a.slot, e >> 2, z4);
+      const T z = bnoise(a, ch, e, z4);
+      p = (a.one_minus_eps * p + a.eps * gr) + a.noise_scale * z;
+      a.pb[col] = p;
+      a.b[col] = bp;
+      pb_new = p;
+    }
+    pbs[tid] = pb_new;
+  }
+  {
+    __syncthreads();
+    if (tid < BCT) {
+      const int ch = chs[tid];
+      if (ch >= 0 && a.iter == a.n_iter[ch] - 1) {
+        double v = 0.0;
+        for (int k = 0; k < BKC; ++k) {
+          const double p = (double)pbs[tid * BKC + k];
+          v += p * p;
+        }
+        a.kinb[ch] = v;
+      }
+    }
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void k_bgrad(BGradArgs<T> a) {
   using M = mfma16<T>;
-  __shared__ T Xs[BCH * BXP];          // [row][feature]
+  __shared__ T Xs[BCH * BXPG];         // [row][feature]
   __shared__ T Ds[BCH * BWP];          // [row][column]; later the p² tile
   __shared__ float Nz[BRW * BNT];      // friction noise of the tile
   __shared__ int chs[BCT];
   __shared__ T pbs[BNT];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lg = lane >> 4;
-  const int d0 = blockIdx.x * BRW, rank0 = blockIdx.y * BCT;
+  int bx, by;
+  if (!xcd_tile(a.nX, a.nCT, bx, by)) return;
+  const int d0 = bx * BRW, rank0 = by * BCT;
   const int nfeat = min(BRW, a.D - d0);
   const int D = a.D, N = a.N, B = a.B;
   if (tid < BCT) chs[tid] = rank0 + tid < a.c_act ? a.perm[rank0 + tid] : -1;
@@ -290,7 +389,8 @@ __global__ __launch_bounds__(256) void k_bgrad(BGradArgs<T> a) {
     }
   }
 
-  StageMap<T> sm(tid, chs);                          // X chunk [32 rows][32 features], diff [32 rows][160]
+  StageMap<T> sm(tid, chs);                          // X chunk [32 rows][32 features]
+  const StageCM scm(tid, chs, (size_t)B * BKC);      // diff chunk [32 rows][16 chains × 10]
   typename StageMap<T>::v2 xv[2], dv[10];
   auto fetch = [&](int r0) {
 #pragma unroll
@@ -300,15 +400,15 @@ __global__ __launch_bounds__(256) void k_bgrad(BGradArgs<T> a) {
     }
 #pragma unroll
     for (int u = 0; u < 10; ++u) {
-      const int r = r0 + sm.wr[u];
-      dv[u] = ld2<T>(a.diff + (size_t)min(r, B - 1) * N + sm.wcol[u], sm.wok[u] && r < B, 2);
+      const int r = r0 + scm.wr[u];
+      dv[u] = ld2<T>(a.diff + scm.wsrc[u] + (size_t)min(r, B - 1) * BKC, scm.wok[u] && r < B, 2);
     }
   };
   auto stash = [&]() {
 #pragma unroll
-    for (int u = 0; u < 2; ++u) st2<T>(Xs + sm.xr[u] * BXP + sm.xc[u], xv[u]);
+    for (int u = 0; u < 2; ++u) st2<T>(Xs + sm.xr[u] * BXPG + sm.xc[u], xv[u]);
 #pragma unroll
-    for (int u = 0; u < 10; ++u) st2<T>(Ds + sm.wr[u] * BWP + sm.wls[u], dv[u]);
+    for (int u = 0; u < 10; ++u) st2<T>(Ds + scm.wr[u] * BWP + scm.wls[u], dv[u]);
   };
 
   const int mt = wave & 1, nh = wave >> 1;
@@ -324,7 +424,7 @@ __global__ __launch_bounds__(256) void k_bgrad(BGradArgs<T> a) {
     const int nks = min(BCH, B - r0 + 3) / 4;
 #pragma unroll 2
     for (int ks = 0; ks < nks; ++ks) {
-      const T av = Xs[(ks * 4 + lg) * BXP + mt * 16 + lr];          // A(feature, row) = X[row][feature]
+      const T av = Xs[(ks * 4 + lg) * BXPG + mt * 16 + lr];         // A(feature, row) = X[row][feature]
       T bv[5];
 #pragma unroll
       for (int j = 0; j < 5; ++j) bv[j] = Ds[(ks * 4 + lg) * BWP + (nh * 5 + j) * 16 + lr];
@@ -336,6 +436,20 @@ __global__ __launch_bounds__(256) void k_bgrad(BGradArgs<T> a) {
 
   // ---- epilogue on the accumulators: softmax.py:57-58 gradient, sghmc.py:31,34 momentum, :32 drift
   T* P2 = Ds;                                        // [BRW][BWP] p² of chains ending here
+  T* __restrict__ Wg = a.W;                          // all 20 W / pW loads first (no aliasing), then
+  T* __restrict__ Pg = a.pW;                         // the updates: one HBM round trip per thread
+  T wv[5][4], pv[5][4];
+#pragma unroll
+  for (int j = 0; j < 5; ++j)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int fi = mt * 16 + M::row(lane, q), col = (nh * 5 + j) * 16 + lr;
+      const int cs = col / BKC, k = col - cs * BKC, ch = chs[cs];
+      const bool ok = ch >= 0 && fi < nfeat;
+      const size_t idx = ok ? ((size_t)ch * D + (d0 + fi)) * BKC + k : 0;
+      wv[j][q] = ok ? Wg[idx] : T(0);
+      pv[j][q] = ok ? Pg[idx] : T(0);
+    }
 #pragma unroll
   for (int j = 0; j < 5; ++j)
 #pragma unroll
@@ -345,16 +459,16 @@ __global__ __launch_bounds__(256) void k_bgrad(BGradArgs<T> a) {
       T p2 = T(0);
       if (ch >= 0 && fi < nfeat) {
         const int d = d0 + fi;
-        const size_t idx = (size_t)d * N + ch * BKC + k;
-        const T w = a.W[idx];
+        const size_t idx = ((size_t)ch * D + d) * BKC + k;
+        const T w = wv[j][q];
         const T gr = -(acc[j][q] - a.alpha * w);
         const T z = a.noise_mode == HMCX_NOISE_BUFFER
                         ? (T)a.noise[a.noff[ch] + (int64_t)a.slot * a.P + (uint32_t)(d * BKC + k)]
                         : (T)Nz[fi * BNT + col];
-        const T p = (a.one_minus_eps * a.pW[idx] + a.eps * gr) + a.noise_scale * z;
-        a.pW[idx] = p;
+        const T p = (a.one_minus_eps * pv[j][q] + a.eps * gr) + a.noise_scale * z;
+        Pg[idx] = p;
         const int n = a.n_iter[ch];
-        if (a.iter < n - 1) a.W[idx] = w + a.eps * p;
+        if (a.iter < n - 1) Wg[idx] = w + a.eps * p;
         else p2 = p * p;
       }
       P2[fi * BWP + col] = p2;
@@ -366,45 +480,173 @@ __global__ __launch_bounds__(256) void k_bgrad(BGradArgs<T> a) {
       double v = 0.0;
       for (int fi = 0; fi < nfeat; ++fi)
         for (int k = 0; k < BKC; ++k) v += (double)P2[fi * BWP + tid * BKC + k];
-      a.kin_part[(size_t)blockIdx.x * a.C + ch] = v;
+      a.kin_part[(size_t)bx * a.C + ch] = v;
     }
   }
-  if (blockIdx.x == 0 && tid < BNT) {                // bias sub-step (sghmc.py:32-34 on the bias)
-    const int cs = tid / BKC, k = tid - cs * BKC, ch = chs[cs];
-    T pb_new = T(0);
-    if (ch >= 0) {
-      const int col = ch * BKC + k;
-      T c = T(0);
-      for (int rb = 0; rb < a.nRB; ++rb) c += a.colsum_part[(size_t)rb * N + col];
-      const T bb = a.b[col];
-      T p = a.pb[col];
-      const T bp = bb + a.eps * p;
-      const T gr = -(c - a.alpha * bp);
-      float z4[4] = {0.f, 0.f, 0.f, 0.f};
-      const uint32_t e = (uint32_t)(D * BKC + k);
-      if (a.noise_mode != HMCX_NOISE_BUFFER) philox_normal4(a.seed, a.chain0 + ch, a.step, a.slot, e >> 2, z4);
-      const T z = bnoise(a, ch, e, z4);
-      p = (a.one_minus_eps * p + a.eps * gr) + a.noise_scale * z;
-      a.pb[col] = p;
-      a.b[col] = bp;
-      pb_new = p;
-    }
-    pbs[tid] = pb_new;
+  if (bx == 0) bias_substep(a, chs, pbs);
+}
+
+// k_bgrad with 64-feature tiles (two m-tiles per wave: 10 MFMAs per 7 LDS operand reads instead of
+// 5 per 6), used when many chains are active.  LDS: X chunk [32 rows][64 features] and the diff
+// chunk as in k_bgrad; the friction noise is generated after the k loop into the diff chunk's
+// space and the kinetic partials use the X chunk's space, so two workgroups fit per CU.
+constexpr int BRW2 = 64;
+constexpr int BXP2 = BRW2 + 16;   // 80 ≡ 16 (mod 32)
+template <typename T>
+__global__ __launch_bounds__(256) void k_bgrad2(BGradArgs<T> a) {
+  using M = mfma16<T>;
+  typedef typename StageMap<T>::v2 v2;
+  constexpr int XSN = BCH * BXP2 > 8 * BNT * 8 / (int)sizeof(T) ? BCH * BXP2 : 8 * BNT * 8 / (int)sizeof(T);
+  __shared__ __attribute__((aligned(16))) T Xs[XSN];   // [row][feature]; later the per-lane-group p² sums
+  constexpr int DSN = BCH * BWP > BRW2 * BNT * 4 / (int)sizeof(T) ? BCH * BWP : BRW2 * BNT * 4 / (int)sizeof(T);
+  __shared__ __attribute__((aligned(16))) T Ds[DSN];   // [row][column]; later the friction noise (float)
+  __shared__ int chs[BCT];
+  __shared__ T pbs[BNT];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lg = lane >> 4;
+  int bx, by;
+  if (!xcd_tile(a.nX, a.nCT, bx, by)) return;
+  const int d0 = bx * BRW2, rank0 = by * BCT;
+  const int nfeat = min(BRW2, a.D - d0);
+  const int D = a.D, N = a.N, B = a.B;
+  if (tid < BCT) chs[tid] = rank0 + tid < a.c_act ? a.perm[rank0 + tid] : -1;
+  __syncthreads();
+
+  const StageCM scm(tid, chs, (size_t)B * BKC);      // diff chunk [32 rows][16 chains × 10]
+  int xr[4], xc[4];                                  // X part: [32 rows][64 features], 4 vectors each
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int j = tid + 256 * u;
+    xr[u] = j >> 5;
+    xc[u] = (j & 31) * 2;
   }
-  if (blockIdx.x == 0) {
+  v2 xv[4], dv[10];
+  auto fetch = [&](int r0) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int r = r0 + xr[u];
+      xv[u] = ld2<T>(a.X + (size_t)min(r, B - 1) * D + d0 + xc[u], r < B, nfeat - xc[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 10; ++u) {
+      const int r = r0 + scm.wr[u];
+      dv[u] = ld2<T>(a.diff + scm.wsrc[u] + (size_t)min(r, B - 1) * BKC, scm.wok[u] && r < B, 2);
+    }
+  };
+  auto stash = [&]() {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) st2<T>(Xs + xr[u] * BXP2 + xc[u], xv[u]);
+#pragma unroll
+    for (int u = 0; u < 10; ++u) st2<T>(Ds + scm.wr[u] * BWP + scm.wls[u], dv[u]);
+  };
+
+  const int mt = wave & 1, nh = wave >> 1;           // wave: features mt·32 .. +32, columns nh·80 .. +80
+  typename M::acc_t acc[2][5];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 5; ++j) acc[i][j] = M::zero();
+  fetch(0);
+  for (int r0 = 0; r0 < B; r0 += BCH) {
     __syncthreads();
-    if (tid < BCT) {
-      const int ch = chs[tid];
-      if (ch >= 0 && a.iter == a.n_iter[ch] - 1) {
-        double v = 0.0;
-        for (int k = 0; k < BKC; ++k) {
-          const double p = (double)pbs[tid * BKC + k];
-          v += p * p;
-        }
-        a.kinb[ch] = v;
+    stash();
+    __syncthreads();
+    if (r0 + BCH < B) fetch(r0 + BCH);
+    const int nks = min(BCH, B - r0 + 3) / 4;
+#pragma unroll 2
+    for (int ks = 0; ks < nks; ++ks) {
+      T av[2], bv[5];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) av[i] = Xs[(ks * 4 + lg) * BXP2 + mt * 32 + i * 16 + lr];
+#pragma unroll
+      for (int j = 0; j < 5; ++j) bv[j] = Ds[(ks * 4 + lg) * BWP + (nh * 5 + j) * 16 + lr];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 5; ++j) acc[i][j] = M::fma(av[i], bv[j], acc[i][j]);
+    }
+  }
+  __syncthreads();
+  // friction noise of the tile into the diff chunk's space: chain slot cs, elements e = d·K + k
+  float* Nz = reinterpret_cast<float*>(Ds);          // [64 features][160]
+  if (a.noise_mode != HMCX_NOISE_BUFFER) {
+    const int e0 = d0 * BKC, ne = nfeat * BKC;
+    const int g0 = e0 >> 2, ng = ((e0 + ne + 3) >> 2) - g0;
+    for (int t = tid; t < BCT * ng; t += 256) {
+      const int cs = t / ng, g = g0 + (t - cs * ng), ch = chs[cs];
+      if (ch < 0) continue;
+      float z4[4];
+      philox_normal4(a.seed, a.chain0 + ch, a.step, a.slot, (uint32_t)g, z4);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int e = 4 * g + q - e0;
+        if (e >= 0 && e < ne) Nz[(e / BKC) * BNT + cs * BKC + (e % BKC)] = z4[q];
       }
     }
+    __syncthreads();
   }
+
+  // ---- epilogue on the accumulators: softmax.py:57-58 gradient, sghmc.py:31,34 momentum, :32 drift
+  double* kp = reinterpret_cast<double*>(Xs);        // [mt·4 + lg][160] Σ p² over the lane's rows
+  // The 8 elements of one column (2 m-tiles × 4 rows) are loaded together (W and pW never alias):
+  // five HBM round trips per thread instead of one per element.
+  T* __restrict__ Wg = a.W;
+  T* __restrict__ Pg = a.pW;
+  T wv[1][8], pv[1][8];
+  auto ld_col = [&](int j, T (&w8)[8], T (&p8)[8]) {
+    const int col = (nh * 5 + j) * 16 + lr;
+    const int cs = col / BKC, k = col - cs * BKC, ch = chs[cs];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int fi = mt * 32 + i * 16 + M::row(lane, q);
+        const bool ok = ch >= 0 && fi < nfeat;
+        const size_t idx = ok ? ((size_t)ch * D + (d0 + fi)) * BKC + k : 0;
+        w8[i * 4 + q] = ok ? Wg[idx] : T(0);
+        p8[i * 4 + q] = ok ? Pg[idx] : T(0);
+      }
+  };
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    ld_col(j, wv[0], pv[0]);
+    const int col = (nh * 5 + j) * 16 + lr;
+    const int cs = col / BKC, k = col - cs * BKC, ch = chs[cs];
+    const bool last = ch >= 0 && a.iter >= a.n_iter[ch] - 1;
+    double p2s = 0.0;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int fi = mt * 32 + i * 16 + M::row(lane, q);
+        if (ch >= 0 && fi < nfeat) {
+          const int d = d0 + fi;
+          const size_t idx = ((size_t)ch * D + d) * BKC + k;
+          const T w = wv[0][i * 4 + q];
+          const T gr = -(acc[i][j][q] - a.alpha * w);
+          const T z = a.noise_mode == HMCX_NOISE_BUFFER
+                          ? (T)a.noise[a.noff[ch] + (int64_t)a.slot * a.P + (uint32_t)(d * BKC + k)]
+                          : (T)Nz[fi * BNT + col];
+          const T p = (a.one_minus_eps * pv[0][i * 4 + q] + a.eps * gr) + a.noise_scale * z;
+          Pg[idx] = p;
+          if (!last) Wg[idx] = w + a.eps * p;
+          else p2s += (double)(p * p);
+        }
+      }
+    kp[(mt * 4 + lg) * BNT + col] = p2s;
+  }
+  __syncthreads();
+  if (tid < BCT) {                                   // Σ pW² per chain ending at this iteration
+    const int ch = chs[tid];
+    if (ch >= 0 && a.iter == a.n_iter[ch] - 1) {
+      double v = 0.0;
+      for (int k = 0; k < BKC; ++k)
+        for (int g = 0; g < 8; ++g) v += kp[g * BNT + tid * BKC + k];
+      a.kin_part[(size_t)bx * a.C + ch] = v;
+      if (bx == 0)
+        for (int b2 = a.nX; b2 < a.nDB_all; ++b2) a.kin_part[(size_t)b2 * a.C + ch] = 0.0;
+    }
+  }
+  if (bx == 0) bias_substep(a, chs, pbs);
 }
 
 }  // namespace hmcx

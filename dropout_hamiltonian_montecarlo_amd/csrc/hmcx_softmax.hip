@@ -680,6 +680,78 @@ int softmax_predict_t(hmcx_ctx* ctx, const void* X, int B, int D, int K, int C, 
   return HMCX_OK;
 }
 
+// k_sghmc_init for the chain-batched path: same arithmetic, but the working copy Wwork and the
+// momentum pW are chain-major [C][D][K] (each chain's block contiguous, so every tile of the batched
+// kernels owns whole cache lines); W stays in the caller's [D][C·K] layout.
+template <typename T>
+__global__ __launch_bounds__(256) void k_binit(InitArgs<T> a) {
+  __shared__ double ksh[256];
+  const int c = blockIdx.y, tid = threadIdx.x;
+  const int K = a.K;
+  const int d0 = blockIdx.x * 16;
+  const bool take = a.prev_acc && a.prev_acc[c];
+  const bool drift = a.n_iter[c] >= 1;
+  double kin = 0.0;
+  for (int e = tid; e < 16 * K; e += 256) {
+    const int i = e / K, k = e - (e / K) * K, d = d0 + i;
+    if (d >= a.D) continue;
+    const size_t w = (size_t)d * a.N + c * K + k;
+    const size_t wc = ((size_t)c * a.D + d) * K + k;
+    double z;
+    if (a.noise_mode == HMCX_NOISE_BUFFER) z = a.noise[a.noff[c] + d * K + k];
+    else z = (double)philox_normal(a.seed, a.chain0 + c, a.step, 0u, (uint32_t)(d * K + k));
+    const T p = (T)z;                                                     // hmc.py:86 N(0,1)
+    T q = a.W[w];
+    if (take) { q = a.Wwork[wc]; a.W[w] = q; }                            // commit (sghmc.py:37)
+    a.pW[wc] = p;
+    a.Wwork[wc] = drift ? q + a.eps * p : q;                              // sghmc.py:32 (iteration 0)
+    kin += (double)p * (double)p;
+  }
+  ksh[tid] = kin;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (tid < s) ksh[tid] += ksh[tid + s];
+    __syncthreads();
+  }
+  if (tid == 0) a.kin0_part[(size_t)blockIdx.x * a.C + c] = ksh[0];
+  if (blockIdx.x == 0) {
+    __syncthreads();
+    double kb = 0.0;
+    if (tid < K) {
+      const int col = c * K + tid;
+      double z;
+      if (a.noise_mode == HMCX_NOISE_BUFFER) z = a.noise[a.noff[c] + a.D * K + tid];
+      else z = (double)philox_normal(a.seed, a.chain0 + c, a.step, 0u, (uint32_t)(a.D * K + tid));
+      const T p = (T)z;
+      T q = a.b[col];
+      if (take) { q = a.bwork[col]; a.b[col] = q; }
+      a.pb[col] = p;
+      a.bwork[col] = q;
+      kb = (double)p * (double)p;
+    }
+    ksh[tid] = kb;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+      if (tid < s) ksh[tid] += ksh[tid + s];
+      __syncthreads();
+    }
+    if (tid == 0) a.kin0b[c] = ksh[0];
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_bcommit(CommitArgs<T> a) {
+  const int c = blockIdx.y, tid = threadIdx.x;
+  if (!a.acc[c]) return;
+  const int K = a.K, d0 = blockIdx.x * 16;
+  for (int e = tid; e < 16 * K; e += 256) {
+    const int i = e / K, k = e - (e / K) * K, d = d0 + i;
+    if (d >= a.D) continue;
+    a.W[(size_t)d * a.N + c * K + k] = a.Wwork[((size_t)c * a.D + d) * K + k];
+  }
+  if (blockIdx.x == 0 && tid < K) a.b[c * K + tid] = a.bwork[c * K + tid];
+}
+
 // C chains, K = 10: per step k_sghmc_init, k_bfwd(LL) at q0, then per leapfrog iteration k_bfwd +
 // k_bgrad over the chains still moving (ranks < c_act(it), ranks = chains by path length
 // descending), k_sghmc_accept; the last step's proposal is committed by k_sghmc_commit.
@@ -691,6 +763,7 @@ int sghmc_batch_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
   const bool big = C >= 512;
   const int RT = big ? 64 : 32;
   const int nRB = (B + RT - 1) / RT, nDB = (D + BRW - 1) / BRW, nDB16 = (D + 15) / 16;
+  const int nDB2 = (D + BRW2 - 1) / BRW2;            // k_bgrad2 feature tiles
   const size_t nsc = (size_t)s->n_steps * C;
   // host: chain order per step (path length descending, stable) and active counts per iteration
   std::vector<int32_t> perm(nsc);
@@ -759,7 +832,7 @@ int sghmc_batch_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
     ia.W = (T*)s->W; ia.b = (T*)s->b;
     ia.Wwork = Wwork; ia.bwork = bwork; ia.pW = pW; ia.pb = pb;
     ia.kin0_part = k0p; ia.kin0b = k0b;
-    hipLaunchKernelGGL((k_sghmc_init<T>), dim3(nDB16, C), dim3(256), 0, st, ia);
+    hipLaunchKernelGGL((k_binit<T>), dim3(nDB16, C), dim3(256), 0, st, ia);
     HMCX_HIP(ctx, hipGetLastError());
 
     BFwdArgs<T> f{};
@@ -768,8 +841,9 @@ int sghmc_batch_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
     f.mode = FWD_LL; f.iter = -1; f.c_act = C;                      // E_current at q0 (all chains)
     f.W = (const T*)s->W; f.b = (const T*)s->b; f.pb = pb;
     f.ll_part = ll0;
-    if (big) hipLaunchKernelGGL((k_bfwd<T, 2>), dim3(nRB, (C + BCT - 1) / BCT), dim3(256), 0, st, f);
-    else hipLaunchKernelGGL((k_bfwd<T, 1>), dim3(nRB, (C + BCT - 1) / BCT), dim3(256), 0, st, f);
+    f.nX = nRB; f.nCT = (C + BCT - 1) / BCT;
+    if (big) hipLaunchKernelGGL((k_bfwd<T, 2, 0>), dim3(xcd_grid(f.nX, f.nCT)), dim3(256), 0, st, f);
+    else hipLaunchKernelGGL((k_bfwd<T, 1, 0>), dim3(xcd_grid(f.nX, f.nCT)), dim3(256), 0, st, f);
     HMCX_HIP(ctx, hipGetLastError());
 
     f.mode = FWD_SGHMC; f.W = Wwork; f.b = bwork;
@@ -780,18 +854,28 @@ int sghmc_batch_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
     g.alpha = (T)s->alpha; g.eps = (T)eps; g.one_minus_eps = (T)(1.0 - eps); g.noise_scale = (T)(2.0 * eps);
     g.n_iter = niter; g.perm = prm;
     g.W = Wwork; g.b = bwork; g.pW = pW; g.pb = pb;
-    g.kin_part = k1p; g.kinb = k1b;
+    g.kin_part = k1p; g.kinb = k1b; g.nDB_all = nDB;
     g.noise_mode = s->noise_mode; g.noise = s->noise; g.noff = noff;
     g.seed = s->seed; g.chain0 = s->chain0; g.step = step_id;
     for (int it = 0; it < maxit; ++it) {
       int c_act = 0;
       while (c_act < C && ni_h[perm[(size_t)st_i * C + c_act]] > it) ++c_act;
       f.iter = it; f.c_act = c_act;
-      if (big) hipLaunchKernelGGL((k_bfwd<T, 2>), dim3(nRB, (c_act + BCT - 1) / BCT), dim3(256), 0, st, f);
-      else hipLaunchKernelGGL((k_bfwd<T, 1>), dim3(nRB, (c_act + BCT - 1) / BCT), dim3(256), 0, st, f);
+      f.nX = nRB; f.nCT = (c_act + BCT - 1) / BCT;
+      if (big) hipLaunchKernelGGL((k_bfwd<T, 2, 1>), dim3(xcd_grid(f.nX, f.nCT)), dim3(256), 0, st, f);
+      else hipLaunchKernelGGL((k_bfwd<T, 1, 1>), dim3(xcd_grid(f.nX, f.nCT)), dim3(256), 0, st, f);
       HMCX_HIP(ctx, hipGetLastError());
       g.iter = it; g.c_act = c_act; g.slot = (uint32_t)(it + 1);
-      hipLaunchKernelGGL((k_bgrad<T>), dim3(nDB, (c_act + BCT - 1) / BCT), dim3(256), 0, st, g);
+      // 64-feature tiles while they fill the chip's 2 workgroups per CU, 32-feature tiles after
+      const int ctiles = (c_act + BCT - 1) / BCT;
+      g.nCT = ctiles;
+      if (nDB2 * ctiles >= 2 * ctx->num_cus) {
+        g.nX = nDB2;
+        hipLaunchKernelGGL((k_bgrad2<T>), dim3(xcd_grid(g.nX, g.nCT)), dim3(256), 0, st, g);
+      } else {
+        g.nX = nDB;
+        hipLaunchKernelGGL((k_bgrad<T>), dim3(xcd_grid(g.nX, g.nCT)), dim3(256), 0, st, g);
+      }
       HMCX_HIP(ctx, hipGetLastError());
     }
     AcceptArgs<T> aa{};
@@ -811,7 +895,7 @@ int sghmc_batch_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
   ca.D = D; ca.K = K; ca.C = C; ca.N = N;
   ca.acc = s->out_accepted + (size_t)(s->n_steps - 1) * C;
   ca.Wwork = Wwork; ca.bwork = bwork; ca.W = (T*)s->W; ca.b = (T*)s->b;
-  hipLaunchKernelGGL((k_sghmc_commit<T>), dim3(nDB16, C), dim3(256), 0, st, ca);
+  hipLaunchKernelGGL((k_bcommit<T>), dim3(nDB16, C), dim3(256), 0, st, ca);
   HMCX_HIP(ctx, hipGetLastError());
   hipLaunchKernelGGL(k_fix_acc, dim3((unsigned)((nsc + 255) / 256)), dim3(256), 0, st, d_niter, d_u,
                      s->out_accepted, (int)nsc);
