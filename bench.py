@@ -43,7 +43,7 @@ def parse():
     ap.add_argument("--dtype", choices=["f64", "f32"], default="f64")
     ap.add_argument("--path", choices=["auto", "kernels", "persistent"], default="auto")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline time budget (0 = skip)")
-    ap.add_argument("--batched-chains", type=int, default=1024,
+    ap.add_argument("--batched-chains", type=int, default=2048,
                     help="chains per GPU of the secondary chain-batched measurement (0 = skip)")
     ap.add_argument("--mlp-steps", type=int, default=40,
                     help="SGHMC steps of the secondary config-3 MLP measurement (0 = skip)")

@@ -115,8 +115,11 @@ __device__ inline typename StageMap<T>::v2 ld2(const T* p, bool ok, int avail) {
 template <typename T> __device__ inline void st2(T* p, typename StageMap<T>::v2 v) { p[0] = v[0]; p[1] = v[1]; }
 
 // Staging map of a chain-major [chain][row][10] operand chunk (32 rows × 16 chain slots × 10 classes =
-// 2560 two-element vectors, 10 per thread): 160 consecutive vectors walk one chain's 32 contiguous
-// rows, so a wave reads 1 KB contiguous.  Source element: base + wsrc + (r0 + wr)·10; LDS
+// 2560 two-element vectors, 10 per thread): vector j covers row j / 80, chain slot (j % 80) / 5,
+// classes 2·(j % 5) .. +1, so 5 lanes read one chain's 80-B row and consecutive lanes write
+// consecutive LDS addresses of one row (a lane order walking one chain's rows instead would put
+// 3-4 rows on the same banks of every ds_write: the LDS row pitch is ≡ 0 (mod 32) dwords for the
+// conflict-free MFMA operand reads).  Source element: base + wsrc + (r0 + wr)·10; LDS
 // destination: row wr, column wls (slot·10 + class).
 struct StageCM {
   int wr[10], wls[10];
@@ -126,7 +129,7 @@ struct StageCM {
 #pragma unroll
     for (int u = 0; u < 10; ++u) {
       const int j = tid + 256 * u;
-      const int cs = j / 160, w = j - cs * 160, row = w / 5, k2 = (w - row * 5) * 2, ch = chs[cs];
+      const int row = j / 80, rem = j - row * 80, cs = rem / 5, k2 = (rem - cs * 5) * 2, ch = chs[cs];
       wr[u] = row;
       wok[u] = ch >= 0;
       wsrc[u] = (size_t)(ch >= 0 ? ch : 0) * stride + k2;
