@@ -134,7 +134,7 @@ def batched_chains(model, X, Y, data, C, n_steps, rank):
     nb = N_DATA // B
     rows = [(i % nb) * B for i in range(n_steps)]
     s.trace = []
-    s._run(state, data, rows[:4], [EPS] * 4, None, B)          # warm-up (workspace, code objects)
+    s._run(state, data, rows, [EPS] * n_steps, None, B)      # warm-up: same call shape (workspace, code objects)
     torch.cuda.synchronize()
     s.trace = []
     model.ctx.set_timing(True)
@@ -176,7 +176,7 @@ def mlp_measure(X, lab, n_steps, rank, cpu_seconds):
     nb = N_DATA // B
     rows = [(i % nb) * B for i in range(n_steps)]
     s.trace = []
-    s._run(state, (Xd, yd), rows[:2], [EPS] * 2, None, B)       # warm-up
+    s._run(state, (Xd, yd), rows, [EPS] * n_steps, None, B)     # warm-up: same call shape
     torch.cuda.synchronize()
     s.trace = []
     m.ctx.set_timing(True)
