@@ -91,6 +91,10 @@ template <typename T> struct FwdArgs {
   int iter;
   const int32_t* n_iter;
   T* diff; T* colsum_part; double* ll_part; T* prob;
+  // split-K forward (few, deep tiles): slab_mode 1 = write the XW partial of D slice blockIdx.z to
+  // slab[z][B][N] and stop; 2 = skip the GEMM, XW = Σ_z slab[z] (fixed order), then the epilogue
+  int slab_mode, nslab;
+  T* slab;
 };
 
 template <typename T> struct GradArgs {

@@ -76,8 +76,14 @@ __global__ __launch_bounds__(NW * 64) void k_fwd(FwdArgs<T> a) {
   typename M::acc_t acc0[NBLK], acc1[NBLK];
 #pragma unroll
   for (int nb = 0; nb < NBLK; ++nb) { acc0[nb] = M::zero(); acc1[nb] = M::zero(); }
-  const int Dw = ((a.D + NW * 16 - 1) / (NW * 16)) * 16;
-  const int kbeg = wave * Dw, kend = min(a.D, kbeg + Dw);
+  int dlo = 0, dhi = a.D;
+  if (a.slab_mode == 1) {                                  // D slice blockIdx.z of gridDim.z
+    const int Dz = ((a.D + (int)gridDim.z * 16 - 1) / ((int)gridDim.z * 16)) * 16;
+    dlo = min(a.D, (int)blockIdx.z * Dz);
+    dhi = min(a.D, dlo + Dz);
+  }
+  const int Dw = ((dhi - dlo + NW * 16 - 1) / (NW * 16)) * 16;
+  const int kbeg = dlo + wave * Dw, kend = a.slab_mode == 2 ? kbeg : min(dhi, kbeg + Dw);
   const bool rok = r < nrow;
   const T* xrow = a.X + (size_t)(m0 + (rok ? r : 0)) * a.D;
   for (int kc = kbeg; kc < kend; kc += 64) {
@@ -129,6 +135,30 @@ __global__ __launch_bounds__(NW * 64) void k_fwd(FwdArgs<T> a) {
     if (e < 16 * NT) yt[e / NT][e - (e / NT) * NT] = yreg[q];
   }
   __syncthreads();
+  if (a.slab_mode == 1) {                                  // split-K partial: XW of this D slice
+    for (int e = tid; e < 16 * NT; e += NTH) {
+      const int i = e / NT, j = e - (e / NT) * NT;
+      if (i >= nrow || j >= ncols) continue;
+      T xw = red[0][i][j];
+#pragma unroll
+      for (int w = 1; w < NW; ++w) xw += red[w][i][j];
+      a.slab[((size_t)blockIdx.z * a.B + m0 + i) * a.N + n0 + j] = xw;
+    }
+    return;
+  }
+  if (a.slab_mode == 2) {                                  // XW = Σ_z slab[z]; the waves' partials are 0
+    for (int e = tid; e < 16 * NT; e += NTH) {
+      const int i = e / NT, j = e - (e / NT) * NT;
+      T xw = T(0);
+      if (i < nrow && j < ncols) {
+        const T* sp = a.slab + (size_t)(m0 + i) * a.N + n0 + j;
+        xw = sp[0];
+        for (int z = 1; z < a.nslab; ++z) xw += sp[(size_t)z * a.B * a.N];
+      }
+      red[0][i][j] = xw;
+    }
+    __syncthreads();
+  }
 
   // ---- pass 1 (element): XW (fixed wave order), z = clip(XW + b), z' = clip(XW + b')
   const T hi = a.clip_hi, lo = a.clip_lo;
@@ -568,16 +598,19 @@ __global__ void k_reduce_ll(const double* ll_part, int nRB, int C, double* out) 
 // ------------------------------------------------------------------ host-side launchers
 template <typename T>
 static hipError_t launch_fwd(const FwdArgs<T>& a, const Tiling& t, hipStream_t st) {
-  dim3 grid(t.nRB, t.nCT);
+  const int nz = a.slab_mode == 1 ? a.nslab : 1;
+  dim3 grid(t.nRB, t.nCT, nz);
   const bool vec = (a.D % 4) == 0;
 #define HMCX_FWD(NB, NW)                                                                          \
   if (vec) hipLaunchKernelGGL((k_fwd<T, NB, true, NW>), grid, dim3(NW * 64), 0, st, a);           \
   else hipLaunchKernelGGL((k_fwd<T, NB, false, NW>), grid, dim3(NW * 64), 0, st, a);
+  // few, deep tiles (one chain, large D: config 5) split D over 8 waves instead of 4
+  const bool deep = (size_t)t.nRB * t.nCT * nz <= 512 && a.D / nz >= 1024 && a.slab_mode != 2;
   switch (t.NBLK) {
     case 1: HMCX_FWD(1, 8) break;
     case 2: HMCX_FWD(2, 8) break;
-    case 3: HMCX_FWD(3, 4) break;
-    default: HMCX_FWD(4, 4) break;
+    case 3: if (deep) { HMCX_FWD(3, 8) } else { HMCX_FWD(3, 4) } break;
+    default: if (deep) { HMCX_FWD(4, 8) } else { HMCX_FWD(4, 4) } break;
   }
 #undef HMCX_FWD
   return hipGetLastError();
@@ -586,13 +619,33 @@ static hipError_t launch_fwd(const FwdArgs<T>& a, const Tiling& t, hipStream_t s
 template <typename T>
 static hipError_t launch_grad(const GradArgs<T>& a, const Tiling& t, hipStream_t st) {
   dim3 grid(t.nDB, t.nCT);
+  const bool deep = (size_t)t.nDB * t.nCT <= 512;
   switch (t.NBLK) {
     case 1: hipLaunchKernelGGL((k_grad<T, 1, 8>), grid, dim3(512), 0, st, a); break;
     case 2: hipLaunchKernelGGL((k_grad<T, 2, 8>), grid, dim3(512), 0, st, a); break;
-    case 3: hipLaunchKernelGGL((k_grad<T, 3, 4>), grid, dim3(256), 0, st, a); break;
-    default: hipLaunchKernelGGL((k_grad<T, 4, 4>), grid, dim3(256), 0, st, a); break;
+    case 3:
+      if (deep) hipLaunchKernelGGL((k_grad<T, 3, 8>), grid, dim3(512), 0, st, a);
+      else hipLaunchKernelGGL((k_grad<T, 3, 4>), grid, dim3(256), 0, st, a);
+      break;
+    default:
+      if (deep) hipLaunchKernelGGL((k_grad<T, 4, 8>), grid, dim3(512), 0, st, a);
+      else hipLaunchKernelGGL((k_grad<T, 4, 4>), grid, dim3(256), 0, st, a);
+      break;
   }
   return hipGetLastError();
+}
+
+// Forward with the D reduction split over S workgroups per tile (S > 1): one launch writes the
+// partial XW slabs, a second sums them in a fixed order and runs the epilogue.
+template <typename T>
+static hipError_t launch_fwd_split(FwdArgs<T> a, const Tiling& t, hipStream_t st, int S, T* slab) {
+  if (S <= 1) return launch_fwd<T>(a, t, st);
+  a.slab = slab; a.nslab = S;
+  a.slab_mode = 1;
+  hipError_t e = launch_fwd<T>(a, t, st);
+  if (e != hipSuccess) return e;
+  a.slab_mode = 2;
+  return launch_fwd<T>(a, t, st);
 }
 
 Tiling make_tiling(int B, int D, int K, int C) {
@@ -1034,8 +1087,12 @@ int sgld_run_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
   const int B = s->B, D = s->D, K = s->K, C = s->C, N = C * K;
   const Tiling t = make_tiling(B, D, K, C);
   const size_t nsc = (size_t)s->n_steps * C;
+  // few, deep forward tiles (one chain, large D: config 5): split D over S workgroups per tile
+  int S = 1;
+  if ((size_t)t.nRB * t.nCT < 128 && D >= 1024)
+    S = std::max(1, std::min(std::min(256 / (t.nRB * t.nCT), D / 256), 16));
   Workspace ws(ctx);
-  T *diff, *csp;
+  T *diff, *csp, *slab = nullptr;
   double* llp;
   int64_t* d_noff;
   do {
@@ -1044,6 +1101,7 @@ int sgld_run_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
     csp = ws.take<T>((size_t)t.nRB * N);
     llp = ws.take<double>((size_t)t.nRB * C);
     d_noff = ws.take<int64_t>(nsc);
+    if (S > 1) slab = ws.take<T>((size_t)S * B * N);
   } while (ws.retry());
   if (ws.failed) return HMCX_ENOMEM;
   begin_call(ctx);
@@ -1061,7 +1119,7 @@ int sgld_run_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
     const double eps = s->eps[st_i];
     FwdArgs<T> f = fwd_args<T>(Xs, Ys, s->W, s->b, B, D, K, C, t, FWD_GRAD);
     f.diff = diff; f.colsum_part = csp;
-    HMCX_HIP(ctx, launch_fwd<T>(f, t, st));
+    HMCX_HIP(ctx, launch_fwd_split<T>(f, t, st, S, slab));
     GradArgs<T> g = grad_args<T>(Xs, diff, csp, B, D, K, C, t, GRAD_SGLD, s->alpha);
     g.eps = (T)eps;
     g.noise_scale = (T)(2.0 * eps);                               // sgld.py:43
@@ -1073,7 +1131,7 @@ int sgld_run_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
     if (s->want_ll && s->want_ll[st_i] && s->out_ll) {
       FwdArgs<T> fl = fwd_args<T>(Xs, Ys, s->W, s->b, B, D, K, C, t, FWD_LL);
       fl.ll_part = llp;
-      HMCX_HIP(ctx, launch_fwd<T>(fl, t, st));
+      HMCX_HIP(ctx, launch_fwd_split<T>(fl, t, st, S, slab));
       hipLaunchKernelGGL(k_reduce_ll, dim3(C), dim3(64), 0, st, llp, t.nRB, C, s->out_ll + (size_t)st_i * C);
       HMCX_HIP(ctx, hipGetLastError());
     }

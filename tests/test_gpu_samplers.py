@@ -196,3 +196,15 @@ def test_full_size_mnist_shape_properties(path):
     assert np.all(np.isfinite(logp)) and post["weights"].shape == (2, 784, 10)
     np.testing.assert_array_equal(s.last_state["weights"].cpu().numpy(), post["weights"][-1])
     assert all(0.0 <= t["A"] <= 1.0 for t in s.trace)
+
+
+def test_sgld_wide_features_split_forward_vs_oracle():
+    """Config-5-like shape (D = 1536 features, K = 38 classes, one chain): the forward's D reduction
+    is split over several workgroups per tile (slab mode); trajectory within rel 1e-9 of the oracle."""
+    c = dict(kind="sgld", N=300, B=100, D=1536, K=38, alpha=0.01, step_size=1e-4, path_length=1.0,
+             burnin=1, epochs=2, data_seed=31, np_seed=8, rng_seed=9)
+    post_r, logp_r, _, _ = _run_oracle(c)
+    post_g, logp_g, _, _ = _run_gpu(c)
+    for v in ("weights", "bias"):
+        np.testing.assert_allclose(post_g[v], post_r[v], rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(logp_g, logp_r, rtol=1e-10)
