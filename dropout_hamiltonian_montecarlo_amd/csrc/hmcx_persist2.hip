@@ -48,6 +48,7 @@ constexpr int QNPM = 16;                 // largest team (producers per gather)
 constexpr unsigned long long QTIMEOUT = 400000000ull;   // s_memrealtime ticks (100 MHz): 4 s
 
 typedef unsigned int gran_t __attribute__((ext_vector_type(4)));
+__host__ __device__ inline int p2_pad(int n, int pad) { return pad ? (n + 7) & ~7 : n; }
 
 struct Q2Args {
   int B, D, K, P, n_steps;
@@ -61,6 +62,10 @@ struct Q2Args {
   char* arena;                              // granule arena (zeroed per call)
   int oXA, oXD, oXB, oXW, oXS;              // region offsets in granules
   int arena_bytes;
+  int pad;                                  // line-aligned producer blocks (HMCX_P2_PAD, default on)
+  int zoff;                                 // noise off the A-RS pollers (HMCX_P2_ZOFF, default on)
+  int spread;                               // rounds with spread gathers, bits A-RS, A-AG, B-RS, B-AG
+                                            // (HMCX_P2_SPREAD=<mask>; default A-AG, where it measured faster)
   int* abort_flag;                          // inside the arena
   double* out_A; int32_t* out_acc; double* out_ll; double* out_E;
   unsigned long long* prof;                 // HMCX_PERSIST_PROF=1: per-segment s_memtime totals (workgroup 0)
@@ -161,6 +166,59 @@ __device__ inline bool poll(__amdgpu_buffer_rsrc_t rs, int base0, int pstride, i
                             V* dst = nullptr, int dstride = 0) {
   return np <= 8 ? poll_nb<1, SUM, V>(rs, base0, pstride, np, pskip, off, valid, ep, sum, abort_flag, dst, dstride)
                  : poll_nb<2, SUM, V>(rs, base0, pstride, np, pskip, off, valid, ep, sum, abort_flag, dst, dstride);
+}
+
+// Spread gather: the (producer, item) pairs of a round are dealt over ALL threads of the workgroup
+// (at most 4 granules per thread, where the per-item polls above put up to 16 on a few lanes of
+// one wave) and land in LDS as stage[p·nitems + i]; the caller combines them in producer order
+// after the barrier, so sums are bit-identical to poll<true>.  Item i of producer p is granule
+// base0 + p·pstride + ioff(i); pairs with want(p, i) false are skipped.
+constexpr int QSTAGE = 4 * QTH;             // staged pairs per round (LDS doubles)
+template <int U, typename Off, typename Want>
+__device__ inline bool gather_u(__amdgpu_buffer_rsrc_t rs, int base0, int pstride, int np, int nitems, Off ioff,
+                                Want want, unsigned ep, int* abort_flag, double* stage) {
+  unsigned pend = 0;
+  int o[U], qi[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int q = threadIdx.x + u * QTH;
+    const int p = q / nitems, i = q - p * nitems;
+    const bool w = q < np * nitems && want(p, i);
+    pend |= w ? 1u << u : 0u;
+    o[u] = (base0 + (w ? p * pstride + ioff(i) : 0)) * 16;
+    qi[u] = q;
+  }
+  unsigned long long t0 = 0;
+  for (int spins = 0; pend; ++spins) {
+    gran_t v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, o[u], 0, 16 /* sc1 */);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (((pend >> u) & 1u) && v[u].y == ep && v[u].w == ep) {
+        stage[qi[u]] = decode(v[u]);
+        pend &= ~(1u << u);
+      }
+    if (!pend) break;
+    if (spins == 0) t0 = __builtin_amdgcn_s_memrealtime();
+    if ((spins & 63) == 63 &&
+        (__builtin_amdgcn_s_memrealtime() - t0 > QTIMEOUT ||
+         __hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+      __hip_atomic_store(abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    if (HMCX_P2_SLEEP) __builtin_amdgcn_s_sleep(1);
+  }
+  return true;
+}
+template <typename Off, typename Want>
+__device__ inline bool gather(__amdgpu_buffer_rsrc_t rs, int base0, int pstride, int np, int nitems, Off ioff,
+                              Want want, unsigned ep, int* abort_flag, double* stage) {
+  const int u = (np * nitems + QTH - 1) / QTH;
+  if (u <= 1) return gather_u<1>(rs, base0, pstride, np, nitems, ioff, want, ep, abort_flag, stage);
+  if (u == 2) return gather_u<2>(rs, base0, pstride, np, nitems, ioff, want, ep, abort_flag, stage);
+  if (u == 3) return gather_u<3>(rs, base0, pstride, np, nitems, ioff, want, ep, abort_flag, stage);
+  return gather_u<4>(rs, base0, pstride, np, nitems, ioff, want, ep, abort_flag, stage);
 }
 
 // Workgroup-uniform verdict after a gather (also the barrier that publishes dst).
@@ -313,8 +371,11 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
   const int MTA = Br / 16, WPA = max(1, QNW / MTA);
   const int MTB = BfP / 16, WPB = max(1, QNW / MTB);
   const int HA = KC + 1;                              // payload header: colsum[KC], ll
-  const int NXA = HA + Ro * KC;                       // A-AG payload per producer
-  const int NXB = HA + Bf * KC;                       // B-RS payload per producer
+  // payload blocks per producer, rounded to whole 128-byte lines (8 granules) when a.pad is set
+  const int NXA0 = HA + Ro * KC;                      // A-AG payload per producer
+  const int NXA = p2_pad(NXA0, a.pad);                // ... and its block stride
+  const int NXB = p2_pad(HA + Bf * KC, a.pad);        // B-RS payload per producer
+  const int NXS = a.pad ? 8 : 4;                      // accept partials per workgroup
 
   // ---- LDS carve-up (mirrored by p2_lds)
   T* Xs = reinterpret_cast<T*>(smem);                 // [Br][BFP]
@@ -337,6 +398,12 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
   double* dsh = hdr + 16;                                 // [16] reductions
   int* ish = reinterpret_cast<int*>(dsh + 16);            // [4] flags
   unsigned long long* profacc = reinterpret_cast<unsigned long long*>(ish + 4);   // [16]
+  double* stg = reinterpret_cast<double*>(profacc + 16);                             // [QSTAGE] spread gathers
+  T* zbuf = reinterpret_cast<T*>(stg + QSTAGE);                                      // [Fo·KC + 16] noise
+  // friction noise by the waves that do not poll A-RS (threads from NZ0 on), when they fit
+  const int NZ0 = ((nro * KC + 63) / 64) * 64;
+  const bool zoff = a.zoff && !(a.spread & 1) && NZ0 + Fo * KC + K <= QTH;
+  const auto all_items = [](int, int) { return true; };
 
   // owned weight of this thread: feature fo0 + od, class ok (thread t = od·KC + ok)
   const int od = tid / KC, okc = tid - (tid / KC) * KC;
@@ -371,7 +438,7 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
   auto roundA = [&]() -> bool {
     ++ep;
     const int reg = a.oXA + (((int)(uA & 1) * Gr + r) * Gf + f) * Br * KC;
-    const int nkp = (BfP / 4) / WPA;
+    const int nkp = WPA == 1 ? (nfeat + 3) / 4 : (BfP / 4) / WPA;   // zero-padded tail skipped
     for (int item = wave; item < MTA * WPA; item += QNW) {
       const int mt = item % MTA, part = item / MTA;
       const typename M::acc_t c = mfma_tile<T>(Xs + mt * 16 * BFP + part * nkp * 4, BFP, 1,
@@ -401,6 +468,19 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
   auto consumeA = [&]() -> bool {
     const int base0 = a.oXA + ((int)(uA & 1) * Gr + r) * Gf * Br * KC;
     ++uA;
+    if (a.spread & 1) {
+      const int ni = nro * KC;
+      const bool ok = gather(rs, base0, Br * KC, Gf, ni, [&](int i) { return ro0 * KC + i; }, all_items, ep,
+                             a.abort_flag, stg);
+      if (!all_ok(ok, ish)) return false;
+      if (tid < ni) {
+        double z = stg[tid];
+        for (int p = 1; p < Gf; ++p) z += stg[p * ni + tid];
+        Zo[(tid / KC) * 16 + (tid % KC)] = (T)z;
+      }
+      __syncthreads();
+      return true;
+    }
     double z = 0.0;
     const bool ok = poll<true>(rs, base0, Br * KC, Gf, -1, ro0 * KC + tid, tid < nro * KC, ep, nullptr, 0, &z,
                                a.abort_flag);
@@ -497,7 +577,24 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
       prof.stamp(2);
       // friction noise of this iteration (sghmc.py:31), generated while the partials travel
       T zb = T(0);
-      {
+      if (zoff) {
+        // by the waves that do not poll the A-RS round, into LDS; the owners pick it up below
+        const int zi = tid - NZ0;
+        if (zi >= 0 && zi < nfo * KC + K) {
+          float z4[4];
+          bool v = true;
+          uint32_t e;
+          if (zi < nfo * KC) {
+            const int od_ = zi / KC, ok_ = zi - (zi / KC) * KC;
+            v = ok_ < K;
+            e = (uint32_t)((feat0 + fo0 + od_) * K + ok_);
+          } else {
+            e = (uint32_t)(D * K + zi - nfo * KC);
+          }
+          if (v) philox4_if(a, s, (uint32_t)(it + 1), e >> 2, z4);
+          zbuf[zi] = v ? noise_at<T>(a, s, (uint32_t)(it + 1), e, z4) : T(0);
+        }
+      } else {
         float z4[4];
         if (own) philox4_if(a, s, (uint32_t)(it + 1), (uint32_t)(e_own >> 2), z4);
         zn = own ? noise_at<T>(a, s, (uint32_t)(it + 1), (uint32_t)e_own, z4) : T(0);
@@ -509,6 +606,10 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
       }
       prof.stamp(3);
       if (!consumeA()) return;
+      if (zoff) {                                       // consumeA ended in a barrier
+        zn = own ? zbuf[tid] : T(0);
+        zb = tid < K ? zbuf[nfo * KC + tid] : T(0);
+      }
       tstamp(s, it, 1);
       prof.stamp(4);
 
@@ -546,7 +647,7 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
       {
         ++ep;
         const int reg = a.oXD + (((int)(uD & 1) * Gr + r) * Gf + f) * NXA;
-        for (int t = tid; t < NXA; t += QTH) {
+        for (int t = tid; t < NXA0; t += QTH) {
           double v;
           if (t < KC) {
             T c = T(0);
@@ -565,14 +666,26 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
         const int base0 = a.oXD + ((int)(uD & 1) * Gr + r) * Gf * NXA;
         ++uD;
         bool ok;
-        if (tid < HA) {
+        if (a.spread & 2) {
+          ok = gather(rs, base0, NXA, Gf, NXA0, [](int i) { return i; }, all_items, ep, a.abort_flag, stg);
+          if (!all_ok(ok, ish)) return;
+          if (tid < HA) {
+            hv = stg[tid];
+            for (int p = 1; p < Gf; ++p) hv += stg[p * NXA0 + tid];
+          }
+          for (int q = tid; q < Gf * NXA0; q += QTH) {
+            const int p = q / NXA0, t = q - p * NXA0;
+            if (t >= HA) Ds[(p * Ro + (t - HA) / KC) * 16 + (t - HA) % KC] = (T)stg[q];
+          }
+          __syncthreads();
+        } else if (tid < HA) {
           ok = poll<true>(rs, base0, NXA, Gf, -1, tid, true, ep, nullptr, 0, &hv, a.abort_flag);
         } else {
           const int m = tid - HA;
-          ok = poll<false>(rs, base0, NXA, Gf, -1, tid, tid < NXA, ep, nullptr, 0, nullptr, a.abort_flag,
+          ok = poll<false>(rs, base0, NXA, Gf, -1, tid, tid < NXA0, ep, nullptr, 0, nullptr, a.abort_flag,
                            Ds + (m / KC) * 16 + (m % KC), Ro * 16);
         }
-        if (!all_ok(ok, ish)) return;
+        if (!(a.spread & 2) && !all_ok(ok, ish)) return;
         tstamp(s, it, 3);
       }
 
@@ -616,9 +729,22 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
         double sum = 0.0;
         const bool isg = tid < ng, ish_ = tid >= ng && tid < ng + HA;
         const int offB = isg ? HA + fo0 * KC + tid : tid - ng;
-        const bool ok = poll<true>(rs, base0, NXB, Gr, -1, offB, isg || ish_, ep, nullptr, 0, &sum, a.abort_flag);
-        if (ish_) hdr[tid - ng] = sum;
-        if (!all_ok(ok, ish)) return;
+        if (a.spread & 4) {
+          const int ni = ng + HA;
+          const bool ok = gather(rs, base0, NXB, Gr, ni, [&](int i) { return i < ng ? HA + fo0 * KC + i : i - ng; },
+                                 all_items, ep, a.abort_flag, stg);
+          if (!all_ok(ok, ish)) return;
+          if (tid < ni) {
+            sum = stg[tid];
+            for (int p = 1; p < Gr; ++p) sum += stg[p * ni + tid];
+          }
+          if (ish_) hdr[tid - ng] = sum;
+          __syncthreads();
+        } else {
+          const bool ok = poll<true>(rs, base0, NXB, Gr, -1, offB, isg || ish_, ep, nullptr, 0, &sum, a.abort_flag);
+          if (ish_) hdr[tid - ng] = sum;
+          if (!all_ok(ok, ish)) return;
+        }
         tstamp(s, it, 5);
         prof.stamp(8);
         // owned weight: gradient (softmax.py:57-58), momentum (sghmc.py:31,34), drift (:32)
@@ -641,16 +767,29 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
       prof.stamp(9);
       {
         ++ep;
-        const int per = Fo * KC;
+        const int per = p2_pad(Fo * KC, a.pad);
         const int reg = a.oXW + (((int)(uW & 1) * Gf + f) * Gr + r) * per;
         if (tid < nfo * KC) put(rs, reg + tid, own ? (double)wv : 0.0, ep);
         tstamp(s, it, 6);
         if (own) Wf[wl] = wv;
         const int base0 = a.oXW + ((int)(uW & 1) * Gf + f) * Gr * per;
         ++uW;
+        if (a.spread & 8) {
+          const int ni = Fo * KC;
+          const auto want = [&](int p, int i) { return p != r && p < min(Gr, (nfeat - i / KC + Fo - 1) / Fo); };
+          const bool ok = gather(rs, base0, per, Gr, ni, [](int i) { return i; }, want, ep, a.abort_flag, stg);
+          if (!all_ok(ok, ish)) return;
+          for (int q = tid; q < Gr * ni; q += QTH) {
+            const int p = q / ni, i = q - p * ni;
+            if (want(p, i)) Wf[(p * Fo + i / KC) * 16 + i % KC] = (T)stg[q];
+          }
+          __syncthreads();
+          tstamp(s, it, 7);
+          continue;
+        }
         const int dloc = tid / KC, kk = tid - (tid / KC) * KC;
-        const int npd = tid < per ? min(Gr, (nfeat - dloc + Fo - 1) / Fo) : 0;   // producers owning feature dloc
-        const bool ok = poll<false>(rs, base0, per, npd, r, tid, tid < per, ep, nullptr, 0, nullptr, a.abort_flag,
+        const int npd = tid < Fo * KC ? min(Gr, (nfeat - dloc + Fo - 1) / Fo) : 0;   // producers owning feature dloc
+        const bool ok = poll<false>(rs, base0, per, npd, r, tid, tid < Fo * KC, ep, nullptr, 0, nullptr, a.abort_flag,
                                     Wf + dloc * 16 + kk, Fo * 16);
         if (!all_ok(ok, ish)) return;
         tstamp(s, it, 7);
@@ -664,18 +803,18 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
     for (int k = 0; k < K; ++k) kb1 += (double)pbsh[k] * (double)pbsh[k];
     ++ep;
     {
-      const int reg = a.oXS + ((int)(uS & 1) * G + bid) * 4;
+      const int reg = a.oXS + ((int)(uS & 1) * G + bid) * NXS;
       if (tid == 0) put(rs, reg + 0, kin0, ep);
       if (tid == 1) put(rs, reg + 1, kin1w, ep);
       if (tid == 2) put(rs, reg + 2, ll0, ep);
     }
-    const int sbase = a.oXS + (int)(uS & 1) * G * 4;
+    const int sbase = a.oXS + (int)(uS & 1) * G * NXS;
     ++uS;
     double v3[3] = {0.0, 0.0, 0.0};
     bool ok = true;
 #pragma unroll
     for (int j = 0; j < 3; ++j)
-      ok = ok && poll<true>(rs, sbase + j, 4, 1, -1, tid * 4, tid < G, ep, nullptr, 0, &v3[j], a.abort_flag);
+      ok = ok && poll<true>(rs, sbase + j, NXS, 1, -1, tid * NXS, tid < G, ep, nullptr, 0, &v3[j], a.abort_flag);
     if (!all_ok(ok, ish)) return;
     const double S0 = wsum(v3[0], dsh), S1 = wsum(v3[1], dsh), L0 = wsum(v3[2], dsh);
     const double K0 = (0.0 + 0.5 * S0) + 0.5 * kb0;
@@ -722,7 +861,7 @@ static size_t p2_lds(const PersistPlan2& p, int K, size_t ts) {
   size_t t = ts * ((size_t)p.Br * p.BFP + 2 * (size_t)p.BfP * 16 + (size_t)p.Gf * p.Ro * 16 + ZPN +
                    4 * (size_t)p.Ro * 16 + 64);
   t = (t + 15) & ~(size_t)15;
-  t += 8 * ((size_t)p.Ro + 32) + 16 + 16 * 8;
+  t += 8 * ((size_t)p.Ro + 32) + 16 + 16 * 8 + 8 * (size_t)QSTAGE + ts * ((size_t)p.Fo * 16 + 16);
   (void)K;
   return t;
 }
@@ -774,8 +913,10 @@ int sghmc_p2_t(hmcx_ctx* ctx, const hmcx_sampler_args* s, const PersistPlan2& pl
   const int G = pl.Gr * pl.Gf, K = s->K, KC = kc_of(K);
   const size_t n = (size_t)s->n_steps;
   // granule arena: XA, XD, XB, XW, XS (double-buffered), then the abort word
-  const long nXA = 2L * G * pl.Br * KC, nXD = 2L * G * (KC + 1 + pl.Ro * KC), nXB = 2L * G * (KC + 1 + pl.Bf * KC),
-             nXW = 2L * G * pl.Fo * KC, nXS = 2L * G * 4;
+  static const int pad = !(getenv("HMCX_P2_PAD") && getenv("HMCX_P2_PAD")[0] == '0');
+  const long nXA = 2L * G * pl.Br * KC, nXD = 2L * G * p2_pad(KC + 1 + pl.Ro * KC, pad),
+             nXB = 2L * G * p2_pad(KC + 1 + pl.Bf * KC, pad), nXW = 2L * G * p2_pad(pl.Fo * KC, pad),
+             nXS = 2L * G * (pad ? 8 : 4);
   const long ngran = nXA + nXD + nXB + nXW + nXS + 1;
   if (ngran * 16 > 0x7fffffffL) return set_error(ctx, HMCX_EUNSUPPORTED, "persistent SGHMC: arena too large");
   Workspace ws(ctx);
@@ -815,6 +956,15 @@ int sghmc_p2_t(hmcx_ctx* ctx, const hmcx_sampler_args* s, const PersistPlan2& pl
   a.oXA = 0; a.oXD = (int)nXA; a.oXB = (int)(nXA + nXD); a.oXW = (int)(nXA + nXD + nXB);
   a.oXS = (int)(nXA + nXD + nXB + nXW);
   a.arena_bytes = (int)(ngran * 16);
+  a.pad = pad;
+  {
+    const int HA = KC + 1;
+    const bool fits = pl.Gf * pl.Ro * KC <= QSTAGE && pl.Gf * (HA + pl.Ro * KC) <= QSTAGE &&
+                      pl.Gr * (pl.Fo * KC + HA) <= QSTAGE && pl.Gr * pl.Fo * KC <= QSTAGE;
+    static const int spread_env = getenv("HMCX_P2_SPREAD") ? atoi(getenv("HMCX_P2_SPREAD")) : 2;
+    a.spread = fits ? spread_env : 0;
+    a.zoff = !(getenv("HMCX_P2_ZOFF") && getenv("HMCX_P2_ZOFF")[0] == '0');
+  }
   a.abort_flag = reinterpret_cast<int*>(arena + (ngran - 1) * 16);
   a.out_A = s->out_A; a.out_acc = s->out_accepted; a.out_ll = s->out_ll; a.out_E = s->out_E;
   static const bool prof_on = getenv("HMCX_PERSIST_PROF") && getenv("HMCX_PERSIST_PROF")[0] == '1';

@@ -2,7 +2,7 @@
 # Quick GPU iteration: GPU tests, then the SGHMC probe over several team grids.
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 300 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?
 tail -5 gpurun_out/pytest_gpu.log
 [ $rc -eq 0 ] || { grep -E "Error|error|assert" gpurun_out/pytest_gpu.log | head -20; exit $rc; }
 for g in ${GRIDS:-auto 4x4 8x4 4x8 8x8 16x8 8x16}; do

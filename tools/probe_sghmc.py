@@ -37,17 +37,22 @@ _lib_run = m.ctx.lib.hmcx_sghmc_run
 def timed_run(h, a):
     t0 = time.perf_counter(); rc = _lib_run(h, a); t_host.append(time.perf_counter() - t0); return rc
 class L: pass
-s.trace = []
-torch.cuda.synchronize()
-t0 = time.perf_counter()
+reps = int([a for a in sys.argv if a.startswith('reps=')][0][5:]) if any(a.startswith('reps=') for a in sys.argv) else 5
 m.ctx.lib.hmcx_sghmc_run = timed_run
+dts, lfs = [], []
 try:
-    res = s._run(state, data, rows, eps, None, 500)
+    for _ in range(reps):
+        s.trace = []
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        res = s._run(state, data, rows, eps, None, 500)
+        torch.cuda.synchronize()
+        dts.append(time.perf_counter() - t0)
+        lfs.append(sum(max(0, t['L'] - 1) for t in s.trace))
 finally:
     m.ctx.lib.hmcx_sghmc_run = _lib_run
-torch.cuda.synchronize()
-dt = time.perf_counter() - t0
-lf = sum(max(0, t['L'] - 1) for t in s.trace)
+us = sorted(d / l * 1e6 for d, l in zip(dts, lfs))
+dt, lf = dts[-1], lfs[-1]
 print('dtype', dtype, 'graph', graph, 'kern' in sys.argv, 'steps', len(s.trace), 'leapfrogs', lf, 'wall %.4f s' % dt,
-      'enqueue %.4f s' % t_host[0], 'lf/s %.1f' % (lf / dt), 'us/lf %.2f' % (dt / lf * 1e6),
-      'acc %.3f' % np.mean(res.accepted), flush=True)
+      'enqueue %.4f s' % t_host[0], 'lf/s %.1f' % (lf / dt), 'us/lf %.2f' % us[len(us) // 2],
+      'min %.2f max %.2f' % (us[0], us[-1]), 'acc %.3f' % np.mean(res.accepted), flush=True)
