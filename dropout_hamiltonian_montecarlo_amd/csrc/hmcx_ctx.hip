@@ -432,6 +432,8 @@ int hmcx_sgld_run(hmcx_ctx* ctx, const hmcx_sampler_args* a) {
   int rc = check_sampler(ctx, a, false);
   if (rc) return rc;
   if (a->n_steps == 0) return HMCX_OK;
+  if (sgld_wide_eligible(a))
+    return a->dtype == HMCX_F64 ? sgld_wide_t<double>(ctx, a) : sgld_wide_t<float>(ctx, a);
   return a->dtype == HMCX_F64 ? sgld_run_t<double>(ctx, a) : sgld_run_t<float>(ctx, a);
 }
 

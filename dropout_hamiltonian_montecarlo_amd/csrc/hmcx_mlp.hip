@@ -113,9 +113,19 @@ template <typename T>
 __device__ inline void run_pending(const Pending<T>& pd) {
   if (pd.mode == UPD_NONE) return;
   const int nthr = gridDim.x * gridDim.y * blockDim.x;
+  constexpr int PB = 16;                                       // partials loaded per batch
   for (int i = (blockIdx.y * gridDim.x + blockIdx.x) * blockDim.x + threadIdx.x; i < pd.n; i += nthr) {
-    T s = pd.part[i];
-    for (int b = 1; b < pd.nparts; ++b) s += pd.part[(size_t)b * pd.n + i];
+    // all loads of a batch go out before the (in-order) sum: one memory round trip per 16
+    // partials instead of one per partial
+    T s = T(0);
+    for (int b0 = 0; b0 < pd.nparts; b0 += PB) {
+      T v[PB];
+#pragma unroll
+      for (int q = 0; q < PB; ++q) v[q] = pd.part[(size_t)min(b0 + q, pd.nparts - 1) * pd.n + i];   // clamped, unconditional
+#pragma unroll
+      for (int q = 0; q < PB; ++q)
+        if (b0 + q < pd.nparts) s = (b0 + q == 0) ? v[q] : s + v[q];
+    }
     apply_upd(pd.u, pd.mode, i, s);
   }
 }
@@ -171,46 +181,41 @@ __device__ inline void load_chunk(T (&x)[4][2], const T* P, int ld, int r0, int 
     const int r = r0 + 16 * i + lr;
     const bool rok = r < R;
     if constexpr (VEC) {
+      // VEC also requires K % V == 0 (host), so a vector lies entirely inside [k0, ke) or entirely
+      // outside it.  Every load is unconditional (clamped address, zeroed afterwards): a load under
+      // a branch makes hipcc wait for it before the next one, which serialises the k chunks.
       constexpr int V = 16 / sizeof(T);
 #pragma unroll
       for (int h = 0; h < 4 / V; ++h) {                        // f32: one float4; f64: two double2
         const int kv = k0 + (sizeof(T) == 8 ? 8 * h + 2 * lg : 4 * lg);
-        const size_t base = (size_t)r * ld + kv;
-        if (rok && kv + V <= ke) {
-          T v[V], m[V], bb[V];
-          if constexpr (V == 4) {
-            const float4 w = *reinterpret_cast<const float4*>(P + base);
-            v[0] = w.x; v[1] = w.y; v[2] = w.z; v[3] = w.w;
-          } else {
-            const double2 w = *reinterpret_cast<const double2*>(P + base);
-            v[0] = w.x; v[1] = w.y;
-          }
-          if constexpr (OP == OP_H1) {
-            mvals<T, V>(ms, 0, base, m);
-#pragma unroll
-            for (int q = 0; q < V; ++q) bb[q] = b1[kv + q];
-          }
-#pragma unroll
-          for (int q = 0; q < V; ++q) x[h * V + q][i] = op_apply<T, OP>(v[q], m[q], bb[q]);
+        const bool ok = rok && kv < ke;
+        const size_t base = ok ? (size_t)r * ld + kv : 0;
+        T v[V], m[V], bb[V];
+        if constexpr (V == 4) {
+          const float4 w = *reinterpret_cast<const float4*>(P + base);
+          v[0] = w.x; v[1] = w.y; v[2] = w.z; v[3] = w.w;
         } else {
-#pragma unroll
-          for (int q = 0; q < V; ++q) {
-            const bool ok = rok && kv + q < ke;
-            x[h * V + q][i] = ok ? op_apply<T, OP>(P[base + q], OP == OP_H1 ? mval(ms, 0, base + q) : T(1),
-                                                   OP == OP_H1 ? b1[kv + q] : T(0))
-                                 : T(0);
-          }
+          const double2 w = *reinterpret_cast<const double2*>(P + base);
+          v[0] = w.x; v[1] = w.y;
         }
+        if constexpr (OP == OP_H1) {
+          mvals<T, V>(ms, 0, base, m);
+#pragma unroll
+          for (int q = 0; q < V; ++q) bb[q] = b1[ok ? kv + q : q];
+        }
+#pragma unroll
+        for (int q = 0; q < V; ++q) x[h * V + q][i] = ok ? op_apply<T, OP>(v[q], m[q], bb[q]) : T(0);
       }
     } else {
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int k = k0 + kmap<T>(u, lg);
-        const size_t idx = TR ? (size_t)k * ld + r : (size_t)r * ld + k;
         const bool ok = rok && k < ke;
-        x[u][i] = ok ? op_apply<T, OP>(P[idx], OP == OP_H1 ? mval(ms, 0, idx) : T(1),
-                                       OP == OP_H1 ? b1[TR ? r : k] : T(0))
-                     : T(0);
+        const size_t idx = ok ? (TR ? (size_t)k * ld + r : (size_t)r * ld + k) : 0;
+        const T pv = P[idx];
+        const T mv = OP == OP_H1 ? mval(ms, 0, idx) : T(1);
+        const T bv = OP == OP_H1 ? b1[ok ? (TR ? r : k) : 0] : T(0);
+        x[u][i] = ok ? op_apply<T, OP>(pv, mv, bv) : T(0);
       }
     }
   }
@@ -664,7 +669,9 @@ hipError_t mm(MlpNet<T>& net, MMArgs<T>& a) {
   net.pend.mode = UPD_NONE;
   dim3 grid((a.M + 31) / 32, (a.N + 31) / 32), blk(MM_NT);
   const bool h1ok = AOP != OP_H1 || net.vec_masks;
-  const bool av = !TA && h1ok && vec_ok(a.A, a.lda, sizeof(T)), bv = TB && vec_ok(a.B, a.ldb, sizeof(T));
+  const bool kvec = a.K % (int)(16 / sizeof(T)) == 0;       // vectors never straddle the K end
+  const bool av = !TA && h1ok && kvec && vec_ok(a.A, a.lda, sizeof(T));
+  const bool bv = TB && kvec && vec_ok(a.B, a.ldb, sizeof(T));
   hipStream_t st = net.st;
   if (av && bv) hipLaunchKernelGGL((k_mm<T, EPI, AOP, BOP, TA, TB, !TA, TB>), grid, blk, 0, st, a);
   else if (av) hipLaunchKernelGGL((k_mm<T, EPI, AOP, BOP, TA, TB, !TA, 0>), grid, blk, 0, st, a);

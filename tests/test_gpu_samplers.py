@@ -198,9 +198,11 @@ def test_full_size_mnist_shape_properties(path):
     assert all(0.0 <= t["A"] <= 1.0 for t in s.trace)
 
 
-def test_sgld_wide_features_split_forward_vs_oracle():
-    """Config-5-like shape (D = 1536 features, K = 38 classes, one chain): the forward's D reduction
-    is split over several workgroups per tile (slab mode); trajectory within rel 1e-9 of the oracle."""
+def test_sgld_wide_features_split_forward_vs_oracle(monkeypatch):
+    """Config-5-like shape (D = 1536 features, K = 38 classes, one chain) on the kernel-per-phase
+    path (HMCX_SGLD_WIDE=0): the forward's D reduction is split over several workgroups per tile
+    (slab mode); trajectory within rel 1e-9 of the oracle."""
+    monkeypatch.setenv("HMCX_SGLD_WIDE", "0")
     c = dict(kind="sgld", N=300, B=100, D=1536, K=38, alpha=0.01, step_size=1e-4, path_length=1.0,
              burnin=1, epochs=2, data_seed=31, np_seed=8, rng_seed=9)
     post_r, logp_r, _, _ = _run_oracle(c)
@@ -208,3 +210,38 @@ def test_sgld_wide_features_split_forward_vs_oracle():
     for v in ("weights", "bias"):
         np.testing.assert_allclose(post_g[v], post_r[v], rtol=1e-9, atol=1e-12)
     np.testing.assert_allclose(logp_g, logp_r, rtol=1e-10)
+
+
+@pytest.mark.parametrize("K,D,B", [(38, 2048, 500), (10, 131, 77), (64, 300, 40), (17, 8, 5)])
+def test_sgld_wide_path_vs_oracle(K, D, B, monkeypatch):
+    """hmcx_wide.hip (one chain; chosen for 16 < K ≤ 64, forced here for every shape): float64
+    trajectory within rel 1e-9 of the oracle.  Covers BASELINE config 5's shape (D=2048, K=38,
+    B=500), a ragged shape (D not a multiple of the vector width, partial row block), the largest
+    class count and a D smaller than one MFMA k-step group."""
+    monkeypatch.setenv("HMCX_SGLD_WIDE", "1")
+    c = dict(kind="sgld", N=2 * B, B=B, D=D, K=K, alpha=0.01, step_size=1e-4, path_length=1.0,
+             burnin=1, epochs=2, data_seed=41, np_seed=2, rng_seed=3)
+    post_r, logp_r, _, log_r = _run_oracle(c)
+    post_g, logp_g, _, log_g = _run_gpu(c)
+    for v in ("weights", "bias"):
+        np.testing.assert_allclose(post_g[v], post_r[v], rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(logp_g, logp_r, rtol=1e-10)
+    assert [l for l in log_g.splitlines() if "loss" in l] == [l for l in log_r.splitlines() if "loss" in l]
+
+
+@pytest.mark.parametrize("dtype", ["f64", "f32"])
+def test_sgld_wide_equals_kernel_path_philox(dtype, monkeypatch):
+    """Config 5 (D=2048, K=38, B=500): the wide path and the kernel-per-phase path consume the same
+    Philox noise, so they produce the same trajectory up to summation order (f64: rel 1e-9;
+    f32: rel 1e-4 + 1e-7 absolute)."""
+    c = dict(kind="sgld", N=1500, B=500, D=2048, K=38, alpha=0.01, step_size=1e-4, path_length=1.0,
+             burnin=0, epochs=2, data_seed=43, np_seed=0, rng_seed=0)
+    dt = torch.float64 if dtype == "f64" else torch.float32
+    monkeypatch.setenv("HMCX_SGLD_WIDE", "1")
+    pw, lw, _, _ = _run_gpu(c, dtype=dt, noise="philox", seed=9)
+    monkeypatch.setenv("HMCX_SGLD_WIDE", "0")
+    ps, ls, _, _ = _run_gpu(c, dtype=dt, noise="philox", seed=9)
+    tol = dict(rtol=1e-9, atol=1e-12) if dtype == "f64" else dict(rtol=1e-4, atol=1e-7)
+    for v in ("weights", "bias"):
+        np.testing.assert_allclose(pw[v], ps[v], **tol)
+    np.testing.assert_allclose(lw, ls, rtol=1e-9 if dtype == "f64" else 1e-4)
