@@ -61,6 +61,16 @@ class MlpSghmcArgs(ctypes.Structure):
                 ("out_loss", c_void_p), ("out_nlp", c_void_p), ("out_E", c_void_p)]
 
 
+class SgdArgs(ctypes.Structure):
+    _fields_ = [("dtype", c_int), ("model", c_int), ("B", c_int), ("D", c_int), ("K", c_int), ("n_steps", c_int),
+                ("alpha", c_double), ("step_size", c_double), ("gamma", c_double),
+                ("X", c_void_p), ("Y", c_void_p), ("row0", c_i64p),
+                ("dropout", c_int), ("keep_p", c_double), ("mask_mode", c_int), ("keep", c_void_p),
+                ("keep_off", c_i64p), ("seed", ctypes.c_uint64), ("step_base", ctypes.c_uint32),
+                ("W", c_void_p), ("b", c_void_p), ("mW", c_void_p), ("mb", c_void_p)]
+
+
+MODEL_SOFTMAX, MODEL_LOGISTIC = 0, 1
 MLP_MASK_SLOT0 = 0x80000000
 
 
@@ -70,7 +80,8 @@ EXPORTS = ("hmcx_version", "hmcx_create", "hmcx_destroy", "hmcx_last_error", "hm
            "hmcx_philox_uniforms", "hmcx_philox_normals",
            "hmcx_softmax_grad", "hmcx_softmax_loglik", "hmcx_softmax_predict", "hmcx_sghmc_run",
            "hmcx_sgld_run", "hmcx_hmc_mvn_run", "hmcx_mlp_masks", "hmcx_mlp_grad", "hmcx_mlp_loss",
-           "hmcx_mlp_sghmc_run")
+           "hmcx_mlp_sghmc_run", "hmcx_logistic_grad", "hmcx_logistic_loglik", "hmcx_logistic_predict",
+           "hmcx_sumsq", "hmcx_sgd_run")
 
 _lib = None
 _lock = threading.Lock()
@@ -124,6 +135,14 @@ def load_library():
         lib.hmcx_mlp_loss.argtypes = [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                                       ctypes.POINTER(MlpParams), c_void_p, c_void_p, c_void_p]
         lib.hmcx_mlp_sghmc_run.argtypes = [c_void_p, ctypes.POINTER(MlpSghmcArgs)]
+        lib.hmcx_logistic_grad.argtypes = [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
+                                           c_void_p, c_void_p, c_double, c_void_p, c_void_p]
+        lib.hmcx_logistic_loglik.argtypes = [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
+                                             c_void_p, c_void_p, c_void_p]
+        lib.hmcx_logistic_predict.argtypes = [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,
+                                              c_void_p]
+        lib.hmcx_sumsq.argtypes = [c_void_p, c_int, c_void_p, ctypes.c_int64, c_void_p]
+        lib.hmcx_sgd_run.argtypes = [c_void_p, ctypes.POINTER(SgdArgs)]
         _lib = lib
         return lib
 

@@ -403,6 +403,64 @@ int hmcx_softmax_predict(hmcx_ctx* ctx, int dtype, const void* X, int B, int D, 
                            : softmax_predict_t<float>(ctx, X, B, D, K, C, W, b, prob);
 }
 
+int hmcx_logistic_grad(hmcx_ctx* ctx, int dtype, const void* X, const void* y, int B, int D, int C,
+                       const void* W, const void* b, double alpha, void* gW, void* gb) {
+  HMCX_GUARD_CTX(ctx);
+  int rc = check_dims(ctx, dtype, B, D, 1, C);
+  if (rc) return rc;
+  if (!X || !y || !W || !b || !gW || !gb) return set_error(ctx, HMCX_EINVAL, "null pointer");
+  return dtype == HMCX_F64 ? softmax_grad_t<double>(ctx, X, y, B, D, 1, C, W, b, alpha, gW, gb, LINK_SIGMOID)
+                           : softmax_grad_t<float>(ctx, X, y, B, D, 1, C, W, b, alpha, gW, gb, LINK_SIGMOID);
+}
+
+int hmcx_logistic_loglik(hmcx_ctx* ctx, int dtype, const void* X, const void* y, int B, int D, int C,
+                         const void* W, const void* b, double* ll) {
+  HMCX_GUARD_CTX(ctx);
+  int rc = check_dims(ctx, dtype, B, D, 1, C);
+  if (rc) return rc;
+  if (!X || !y || !W || !b || !ll) return set_error(ctx, HMCX_EINVAL, "null pointer");
+  return dtype == HMCX_F64 ? softmax_loglik_t<double>(ctx, X, y, B, D, 1, C, W, b, ll, LINK_SIGMOID)
+                           : softmax_loglik_t<float>(ctx, X, y, B, D, 1, C, W, b, ll, LINK_SIGMOID);
+}
+
+int hmcx_logistic_predict(hmcx_ctx* ctx, int dtype, const void* X, int B, int D, int C, const void* W,
+                          const void* b, void* prob) {
+  HMCX_GUARD_CTX(ctx);
+  int rc = check_dims(ctx, dtype, B, D, 1, C);
+  if (rc) return rc;
+  if (!X || !W || !b || !prob) return set_error(ctx, HMCX_EINVAL, "null pointer");
+  return dtype == HMCX_F64 ? softmax_predict_t<double>(ctx, X, B, D, 1, C, W, b, prob, LINK_SIGMOID)
+                           : softmax_predict_t<float>(ctx, X, B, D, 1, C, W, b, prob, LINK_SIGMOID);
+}
+
+int hmcx_sumsq(hmcx_ctx* ctx, int dtype, const void* x, int64_t n, double* out) {
+  HMCX_GUARD_CTX(ctx);
+  if (dtype != HMCX_F32 && dtype != HMCX_F64) return set_error(ctx, HMCX_EINVAL, "dtype must be HMCX_F32/HMCX_F64");
+  if (n < 0 || (n > 0 && !x) || !out) return set_error(ctx, HMCX_EINVAL, "hmcx_sumsq: bad arguments");
+  return dtype == HMCX_F64 ? sumsq_t<double>(ctx, x, n, out) : sumsq_t<float>(ctx, x, n, out);
+}
+
+int hmcx_sgd_run(hmcx_ctx* ctx, const hmcx_sgd_args* a) {
+  HMCX_GUARD_CTX(ctx);
+  if (!a) return set_error(ctx, HMCX_EINVAL, "null args");
+  if (a->model != HMCX_MODEL_SOFTMAX && a->model != HMCX_MODEL_LOGISTIC)
+    return set_error(ctx, HMCX_EINVAL, "sgd: model must be HMCX_MODEL_SOFTMAX or HMCX_MODEL_LOGISTIC");
+  if (a->model == HMCX_MODEL_LOGISTIC && a->K != 1) return set_error(ctx, HMCX_EINVAL, "sgd: logistic needs K = 1");
+  int rc = check_dims(ctx, a->dtype, a->B, a->D, a->K, 1);
+  if (rc) return rc;
+  if (a->n_steps < 0) return set_error(ctx, HMCX_EINVAL, "n_steps < 0");
+  if (!a->X || !a->Y || !a->row0 || !a->W || !a->b || !a->mW || !a->mb)
+    return set_error(ctx, HMCX_EINVAL, "null pointer");
+  if (a->dropout) {
+    if (a->mask_mode == HMCX_NOISE_BUFFER && (!a->keep || !a->keep_off))
+      return set_error(ctx, HMCX_EINVAL, "sgd: BUFFER dropout needs keep and keep_off");
+    if (a->mask_mode != HMCX_NOISE_BUFFER && a->mask_mode != HMCX_NOISE_PHILOX)
+      return set_error(ctx, HMCX_EINVAL, "bad mask_mode");
+  }
+  if (a->n_steps == 0) return HMCX_OK;
+  return a->dtype == HMCX_F64 ? sgd_run_t<double>(ctx, a) : sgd_run_t<float>(ctx, a);
+}
+
 static int check_sampler(hmcx_ctx* ctx, const hmcx_sampler_args* a, bool sghmc) {
   if (!a) return set_error(ctx, HMCX_EINVAL, "null args");
   int rc = check_dims(ctx, a->dtype, a->B, a->D, a->K, a->C);

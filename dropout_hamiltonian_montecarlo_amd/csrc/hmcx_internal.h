@@ -81,12 +81,18 @@ struct Tiling {
 Tiling make_tiling(int B, int D, int K, int C);
 
 enum FwdMode { FWD_GRAD = 0, FWD_SGHMC = 1, FWD_LL = 2, FWD_PRED = 3 };
-enum GradMode { GRAD_OUT = 0, GRAD_SGHMC = 1, GRAD_SGLD = 2 };
+enum GradMode { GRAD_OUT = 0, GRAD_SGHMC = 1, GRAD_SGLD = 2, GRAD_SGD = 3 };
+// Output link of the linear model: softmax over K classes (models/cpu/softmax.py) or the
+// sigmoid of K = 1 logistic regression (models/cpu/logistic.py:43-55).
+enum Link { LINK_SOFTMAX = 0, LINK_SIGMOID = 1 };
+// Philox slot of the input-dropout masks of sgd.fit_dropout (below the SGHMC path/accept slots).
+constexpr uint32_t SLOT_DROPX = 0xFFFFFFFCu;
 
 template <typename T> struct FwdArgs {
   const T* X; const T* Y; const T* W; const T* b; const T* pb;
   int B, D, K, C, N, CB;
   int mode;
+  int link;                  // Link (FWD_SGHMC: softmax only)
   T eps, clip_hi, clip_lo;
   int iter;
   const int32_t* n_iter;
@@ -102,6 +108,7 @@ template <typename T> struct GradArgs {
   int B, D, K, C, N, CB, nRB, nDB, P;
   int mode;
   T alpha, eps, one_minus_eps, noise_scale, m_half_eps;
+  T gamma, lr;               // GRAD_SGD: momentum decay and step size (sgd.py:40)
   int iter;
   const int32_t* n_iter;
   const T* Wsrc; const T* bsrc;
@@ -156,11 +163,13 @@ struct GraphScope {
 };
 
 template <typename T> int softmax_grad_t(hmcx_ctx*, const void*, const void*, int, int, int, int, const void*,
-                                         const void*, double, void*, void*);
+                                         const void*, double, void*, void*, int link = LINK_SOFTMAX);
 template <typename T> int softmax_loglik_t(hmcx_ctx*, const void*, const void*, int, int, int, int, const void*,
-                                           const void*, double*);
+                                           const void*, double*, int link = LINK_SOFTMAX);
 template <typename T> int softmax_predict_t(hmcx_ctx*, const void*, int, int, int, int, const void*, const void*,
-                                            void*);
+                                            void*, int link = LINK_SOFTMAX);
+template <typename T> int sgd_run_t(hmcx_ctx*, const hmcx_sgd_args*);
+template <typename T> int sumsq_t(hmcx_ctx*, const void*, int64_t, double*);
 template <typename T> int sghmc_run_t(hmcx_ctx*, const hmcx_sampler_args*);
 template <typename T> int sgld_run_t(hmcx_ctx*, const hmcx_sampler_args*);
 bool sgld_wide_eligible(const hmcx_sampler_args*);       // hmcx_wide.hip: one chain, 16 < K ≤ 64

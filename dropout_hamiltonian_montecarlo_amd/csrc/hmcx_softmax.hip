@@ -54,6 +54,7 @@ __global__ __launch_bounds__(NW * 64) void k_fwd(FwdArgs<T> a) {
   const int K = a.K;
   const int mode = a.mode;
   const bool sghmc = mode == FWD_SGHMC;
+  const bool sig = a.link == LINK_SIGMOID;                 // logistic.py:43-55 (K = 1)
   const int nrow = min(16, a.B - m0);
 
   // ---- prefetch epilogue operands into registers (their latency overlaps the GEMM)
@@ -171,8 +172,8 @@ __global__ __launch_bounds__(NW * 64) void k_fwd(FwdArgs<T> a) {
     if (sghmc) zB[i][j] = clipz(xw + bpt[j], hi, lo);
   }
   __syncthreads();
-  // ---- pass 2 (row, chain): row max (np.max semantics: NaN propagates)
-  for (int p = tid; p < 16 * ncb; p += NTH) {
+  // ---- pass 2 (row, chain): row max (np.max semantics: NaN propagates); softmax link only
+  for (int p = tid; p < (sig ? 0 : 16 * ncb); p += NTH) {
     const int i = p & 15, cb = (p >> 4) * K;
     T m = zA[i][cb];
     for (int k = 1; k < K; ++k) m = max_nan(m, zA[i][cb + k]);
@@ -189,12 +190,16 @@ __global__ __launch_bounds__(NW * 64) void k_fwd(FwdArgs<T> a) {
     const int i = e / NT, j = e - (e / NT) * NT;
     if (j >= ncols) continue;
     const int cc = j / K;
+    if (sig) {
+      eA[i][j] = T(1) / (T(1) + exp(-zA[i][j]));                          // logistic.py:54-55
+      continue;
+    }
     eA[i][j] = exp(zA[i][j] - mA[i][cc]);                                 // softmax.py:34
     if (sghmc) eB[i][j] = exp(zB[i][j] - mB[i][cc]);
   }
   __syncthreads();
-  // ---- pass 4 (row, chain): normalisers
-  for (int p = tid; p < 16 * ncb; p += NTH) {
+  // ---- pass 4 (row, chain): normalisers (softmax link)
+  for (int p = tid; p < (sig ? 0 : 16 * ncb); p += NTH) {
     const int i = p & 15, cc = p >> 4, cb = cc * K;
     T s = T(0);
     for (int k = 0; k < K; ++k) s += eA[i][cb + k];
@@ -212,7 +217,7 @@ __global__ __launch_bounds__(NW * 64) void k_fwd(FwdArgs<T> a) {
     if (j >= ncols || i >= nrow) continue;
     const int cc = j / K;
     const size_t gidx = (size_t)(m0 + i) * a.N + n0 + j;
-    const T yh = eA[i][j] / sA[i][cc];                                    // softmax.py:35-36
+    const T yh = sig ? eA[i][j] : eA[i][j] / sA[i][cc];                   // softmax.py:35-36
     if (mode == FWD_PRED) { a.prob[gidx] = yh; continue; }
     const T y = yt[i][j];
     if (mode == FWD_GRAD || sghmc) {
@@ -226,8 +231,12 @@ __global__ __launch_bounds__(NW * 64) void k_fwd(FwdArgs<T> a) {
       zA[i][j] = y - yb;                                                  // bias sub-step colsum term
       eB[i][j] = y * (zB[i][j] - lse);                                    // softmax.py:19-20
     } else if (mode == FWD_LL) {
-      const T lse = log(sA[i][cc]) + mA[i][cc];
-      eA[i][j] = y * (zA[i][j] - lse);
+      if (sig) {
+        eA[i][j] = y * log(yh) + (T(1) - y) * log(T(1) - yh);             // logistic.py:71
+      } else {
+        const T lse = log(sA[i][cc]) + mA[i][cc];
+        eA[i][j] = y * (zA[i][j] - lse);
+      }
     }
   }
   __syncthreads();
@@ -304,8 +313,8 @@ __global__ __launch_bounds__(NW * 64) void k_grad(GradArgs<T> a) {
         wreg[q] = a.Wsrc[idx];
       } else {
         wreg[q] = a.W[idx];
-        if (mode == GRAD_SGHMC) preg[q] = a.pW[idx];
-        zreg[q] = (T)noise_at(a, c0 + cc, (uint32_t)(d * K + k));
+        if (mode == GRAD_SGHMC || mode == GRAD_SGD) preg[q] = a.pW[idx];
+        if (mode != GRAD_SGD) zreg[q] = (T)noise_at(a, c0 + cc, (uint32_t)(d * K + k));
       }
     }
   }
@@ -369,6 +378,10 @@ __global__ __launch_bounds__(NW * 64) void k_grad(GradArgs<T> a) {
       a.pW[idx] = p;
       pnew[q] = p;
       if (a.iter < a.n_iter[c0 + j / K] - 1) a.W[idx] = wreg[q] + a.eps * p;   // next drift
+    } else if (mode == GRAD_SGD) {
+      const T m = a.gamma * preg[q] - a.lr * gr;                          // sgd.py:40
+      a.pW[idx] = m;
+      a.W[idx] = wreg[q] + m;                                             // sgd.py:41
     } else {
       T p = a.noise_scale * zreg[q];
       p = p + a.m_half_eps * gr;
@@ -433,6 +446,12 @@ __global__ __launch_bounds__(NW * 64) void k_grad(GradArgs<T> a) {
           a.pb[col] = p;
           a.b[col] = bp;
           pb_new = p;
+        } else if (mode == GRAD_SGD) {
+          const T bb = a.b[col];
+          const T gr = -(cs - a.alpha * bb);
+          const T m = a.gamma * a.pb[col] - a.lr * gr;                      // sgd.py:40-41
+          a.pb[col] = m;
+          a.b[col] = bb + m;
         } else {
           const T bb = a.b[col];
           const T gr = -(cs - a.alpha * bb);
@@ -684,7 +703,7 @@ static GradArgs<T> grad_args(const T* X, const T* diff, const T* csp, int B, int
 // ------------------------------------------------------------------ entry points (typed)
 template <typename T>
 int softmax_grad_t(hmcx_ctx* ctx, const void* X, const void* Y, int B, int D, int K, int C, const void* W,
-                   const void* b, double alpha, void* gW, void* gb) {
+                   const void* b, double alpha, void* gW, void* gb, int link) {
   const Tiling t = make_tiling(B, D, K, C);
   const int N = C * K;
   Workspace ws(ctx);
@@ -696,6 +715,7 @@ int softmax_grad_t(hmcx_ctx* ctx, const void* X, const void* Y, int B, int D, in
   } while (ws.retry());
   if (ws.failed) return HMCX_ENOMEM;
   FwdArgs<T> f = fwd_args<T>(X, Y, W, b, B, D, K, C, t, FWD_GRAD);
+  f.link = link;
   f.diff = diff; f.colsum_part = csp;
   HMCX_HIP(ctx, launch_fwd<T>(f, t, ctx->stream));
   GradArgs<T> g = grad_args<T>((const T*)X, diff, csp, B, D, K, C, t, GRAD_OUT, alpha);
@@ -706,7 +726,7 @@ int softmax_grad_t(hmcx_ctx* ctx, const void* X, const void* Y, int B, int D, in
 
 template <typename T>
 int softmax_loglik_t(hmcx_ctx* ctx, const void* X, const void* Y, int B, int D, int K, int C, const void* W,
-                     const void* b, double* ll) {
+                     const void* b, double* ll, int link) {
   const Tiling t = make_tiling(B, D, K, C);
   Workspace ws(ctx);
   double* llp;
@@ -716,6 +736,7 @@ int softmax_loglik_t(hmcx_ctx* ctx, const void* X, const void* Y, int B, int D, 
   } while (ws.retry());
   if (ws.failed) return HMCX_ENOMEM;
   FwdArgs<T> f = fwd_args<T>(X, Y, W, b, B, D, K, C, t, FWD_LL);
+  f.link = link;
   f.ll_part = llp;
   HMCX_HIP(ctx, launch_fwd<T>(f, t, ctx->stream));
   hipLaunchKernelGGL(k_reduce_ll, dim3(C), dim3(64), 0, ctx->stream, llp, t.nRB, C, ll);
@@ -725,11 +746,92 @@ int softmax_loglik_t(hmcx_ctx* ctx, const void* X, const void* Y, int B, int D, 
 
 template <typename T>
 int softmax_predict_t(hmcx_ctx* ctx, const void* X, int B, int D, int K, int C, const void* W, const void* b,
-                      void* prob) {
+                      void* prob, int link) {
   const Tiling t = make_tiling(B, D, K, C);
   FwdArgs<T> f = fwd_args<T>(X, nullptr, W, b, B, D, K, C, t, FWD_PRED);
+  f.link = link;
   f.prob = (T*)prob;
   HMCX_HIP(ctx, launch_fwd<T>(f, t, ctx->stream));
+  return HMCX_OK;
+}
+
+// ------------------------------------------------------------------ momentum SGD (sgd.py:25-70)
+// X_s ⊙ Z for sgd.fit_dropout (sgd.py:61-62): Z from the host's binomial draws or from Philox.
+template <typename T>
+__global__ void k_xdrop(const T* X, T* Xd, int64_t n, const uint8_t* keep, int mode, double p, uint64_t seed,
+                        uint32_t step) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const bool z = mode == HMCX_NOISE_BUFFER ? keep[i] != 0 : philox_uniform(seed, 0u, step, SLOT_DROPX, (uint32_t)i) < p;
+  Xd[i] = X[i] * (z ? T(1) : T(0));                                      // np.multiply(X_batch, Z)
+}
+
+// One k_fwd (gradient mode, softmax or sigmoid link) + one k_grad (GRAD_SGD epilogue) per minibatch.
+template <typename T>
+int sgd_run_t(hmcx_ctx* ctx, const hmcx_sgd_args* s) {
+  const int B = s->B, D = s->D, K = s->K;
+  const Tiling t = make_tiling(B, D, K, 1);
+  const int link = s->model == HMCX_MODEL_LOGISTIC ? LINK_SIGMOID : LINK_SOFTMAX;
+  Workspace ws(ctx);
+  T *diff, *csp, *xd = nullptr;
+  do {
+    ws.reset();
+    diff = ws.take<T>((size_t)B * K);
+    csp = ws.take<T>((size_t)t.nRB * K);
+    if (s->dropout) xd = ws.take<T>((size_t)B * D);
+  } while (ws.retry());
+  if (ws.failed) return HMCX_ENOMEM;
+  begin_call(ctx);
+  int rc;
+  if ((rc = timing_begin(ctx, ctx->stream))) return rc;
+  GraphScope gs(ctx);
+  hipStream_t st = ctx->stream;
+  for (int i = 0; i < s->n_steps; ++i) {
+    const T* Xs = (const T*)s->X + (size_t)s->row0[i] * D;
+    const T* Ys = (const T*)s->Y + (size_t)s->row0[i] * K;
+    if (s->dropout) {
+      const int64_t n = (int64_t)B * D;
+      const uint8_t* kp = s->mask_mode == HMCX_NOISE_BUFFER ? s->keep + s->keep_off[i] : nullptr;
+      hipLaunchKernelGGL(k_xdrop<T>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, Xs, xd, n, kp,
+                         s->mask_mode, s->keep_p, s->seed, s->step_base + (uint32_t)i);
+      HMCX_HIP(ctx, hipGetLastError());
+      Xs = xd;
+    }
+    FwdArgs<T> f = fwd_args<T>(Xs, Ys, s->W, s->b, B, D, K, 1, t, FWD_GRAD);
+    f.link = link;
+    f.diff = diff; f.colsum_part = csp;
+    HMCX_HIP(ctx, launch_fwd<T>(f, t, st));
+    GradArgs<T> g = grad_args<T>(Xs, diff, csp, B, D, K, 1, t, GRAD_SGD, s->alpha);
+    g.gamma = (T)s->gamma; g.lr = (T)s->step_size;
+    g.W = (T*)s->W; g.b = (T*)s->b; g.pW = (T*)s->mW; g.pb = (T*)s->mb;
+    HMCX_HIP(ctx, launch_grad<T>(g, t, st));
+  }
+  if ((rc = gs.finish())) return rc;
+  return timing_end(ctx, ctx->stream);
+}
+
+// Σ x² in float64, one workgroup, fixed order (logistic.py:20's np.sum(np.square(θ))).
+template <typename T>
+__global__ __launch_bounds__(256) void k_sumsq(const T* x, int64_t n, double* out) {
+  __shared__ double sh[256];
+  double acc = 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += 256) {
+    const double v = (double)x[i];
+    acc += v * v;
+  }
+  sh[threadIdx.x] = acc;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) sh[threadIdx.x] += sh[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *out = sh[0];
+}
+
+template <typename T>
+int sumsq_t(hmcx_ctx* ctx, const void* x, int64_t n, double* out) {
+  hipLaunchKernelGGL(k_sumsq<T>, dim3(1), dim3(256), 0, ctx->stream, (const T*)x, n, out);
+  HMCX_HIP(ctx, hipGetLastError());
   return HMCX_OK;
 }
 
@@ -1141,15 +1243,21 @@ int sgld_run_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
 }
 
 template int softmax_grad_t<float>(hmcx_ctx*, const void*, const void*, int, int, int, int, const void*,
-                                   const void*, double, void*, void*);
+                                   const void*, double, void*, void*, int);
 template int softmax_grad_t<double>(hmcx_ctx*, const void*, const void*, int, int, int, int, const void*,
-                                    const void*, double, void*, void*);
+                                    const void*, double, void*, void*, int);
 template int softmax_loglik_t<float>(hmcx_ctx*, const void*, const void*, int, int, int, int, const void*,
-                                     const void*, double*);
+                                     const void*, double*, int);
 template int softmax_loglik_t<double>(hmcx_ctx*, const void*, const void*, int, int, int, int, const void*,
-                                      const void*, double*);
-template int softmax_predict_t<float>(hmcx_ctx*, const void*, int, int, int, int, const void*, const void*, void*);
-template int softmax_predict_t<double>(hmcx_ctx*, const void*, int, int, int, int, const void*, const void*, void*);
+                                      const void*, double*, int);
+template int softmax_predict_t<float>(hmcx_ctx*, const void*, int, int, int, int, const void*, const void*, void*,
+                                      int);
+template int softmax_predict_t<double>(hmcx_ctx*, const void*, int, int, int, int, const void*, const void*, void*,
+                                       int);
+template int sgd_run_t<float>(hmcx_ctx*, const hmcx_sgd_args*);
+template int sgd_run_t<double>(hmcx_ctx*, const hmcx_sgd_args*);
+template int sumsq_t<float>(hmcx_ctx*, const void*, int64_t, double*);
+template int sumsq_t<double>(hmcx_ctx*, const void*, int64_t, double*);
 template int sghmc_run_t<float>(hmcx_ctx*, const hmcx_sampler_args*);
 template int sghmc_run_t<double>(hmcx_ctx*, const hmcx_sampler_args*);
 template int sgld_run_t<float>(hmcx_ctx*, const hmcx_sampler_args*);

@@ -82,6 +82,53 @@ int hmcx_softmax_loglik(hmcx_ctx* ctx, int dtype, const void* X, const void* Y, 
 int hmcx_softmax_predict(hmcx_ctx* ctx, int dtype, const void* X, int B, int D, int K, int C,
                          const void* W, const void* b, void* prob);
 
+/* ------------------------------------------------------------------ logistic model
+ * Replaces hamiltonian/models/cpu/logistic.py:24-72 (K = 1; the GPU file models/gpu/logistic.py is
+ * its CuPy twin).  X [B][D], y [B] (dtype, 0/1), W [D][C], b [C] (C independent parameter sets, C = 1
+ * is the reference's {'weights': [D,1], 'bias': [1]}).
+ * net = sigmoid(clip(XW + b)) = 1/(1 + exp(−z)) (:43-55);  grad = −(Xᵀ(y − net) − alpha·θ) (:24-41). */
+int hmcx_logistic_grad(hmcx_ctx* ctx, int dtype, const void* X, const void* y, int B, int D, int C,
+                       const void* W, const void* b, double alpha, void* gW, void* gb);
+/* ll[c] = Σ_rows y·log(net) + (1 − y)·log(1 − net)  (:64-72), device double[C]. */
+int hmcx_logistic_loglik(hmcx_ctx* ctx, int dtype, const void* X, const void* y, int B, int D, int C,
+                         const void* W, const void* b, double* ll);
+/* prob [B][C] = net (predict(prob=True) of :75-87, before batching). */
+int hmcx_logistic_predict(hmcx_ctx* ctx, int dtype, const void* X, int B, int D, int C, const void* W,
+                          const void* b, void* prob);
+/* out[0] = Σ x² (float64 accumulation, fixed order): the θ-dependent part of logistic.log_prior
+ * (:15-21).  x device [n] (dtype), out device double[1]. */
+int hmcx_sumsq(hmcx_ctx* ctx, int dtype, const void* x, int64_t n, double* out);
+
+/* ------------------------------------------------------------------ momentum SGD (sgd.fit)
+ * Replaces hamiltonian/inference/cpu/sgd.py:25-45 (fit) and :47-70 (fit_dropout) for the softmax
+ * and logistic models: per minibatch s (rows row0[s] .. +B of X / Y)
+ *   g = model.grad(θ, X_s, Y_s);  m = gamma·m − step_size·g;  θ += m      (sgd.py:38-41)
+ * with X_s replaced by X_s ⊙ Z (Z ∈ {0,1}^{B×D}) when dropout is set (sgd.py:61-63).  Z comes from
+ * keep (device uint8, B·D per step from keep_off[s]; BUFFER: the host's np.random.binomial draws)
+ * or from Philox (PHILOX: Z = u < keep_p, u = Philox(seed, 0, step_base + s, 0xFFFFFFFC, element)). */
+enum hmcx_model { HMCX_MODEL_SOFTMAX = 0, HMCX_MODEL_LOGISTIC = 1 };
+typedef struct hmcx_sgd_args {
+  int dtype;
+  int model;               /* hmcx_model                                                  */
+  int B, D, K, n_steps;    /* K = 1 for the logistic model                                */
+  double alpha;            /* prior precision (hyper['alpha'])                            */
+  double step_size;        /* sgd.py:14                                                   */
+  double gamma;            /* momentum decay, sgd.py:25                                   */
+  const void* X;           /* device [N][D]                                               */
+  const void* Y;           /* device [N][K] (softmax one-hot) or [N] (logistic)           */
+  const int64_t* row0;     /* host [n_steps]                                              */
+  int dropout;             /* 0: fit, 1: fit_dropout                                      */
+  double keep_p;           /* fit_dropout's p (PHILOX mode)                               */
+  int mask_mode;           /* HMCX_NOISE_BUFFER or HMCX_NOISE_PHILOX                      */
+  const uint8_t* keep;     /* device, BUFFER                                              */
+  const int64_t* keep_off; /* host [n_steps], BUFFER                                      */
+  uint64_t seed;           /* PHILOX                                                      */
+  uint32_t step_base;      /* PHILOX                                                      */
+  void* W; void* b;        /* device state [D][K], [K], updated in place                  */
+  void* mW; void* mb;      /* device momentum (zero at fit start, sgd.py:35)              */
+} hmcx_sgd_args;
+int hmcx_sgd_run(hmcx_ctx* ctx, const hmcx_sgd_args* a);
+
 /* ------------------------------------------------------------------ samplers
  * One call enqueues n_steps consecutive sampler steps for C chains that share each
  * minibatch; the minibatch of step s is rows [row0[s], row0[s]+B) of X / Y.

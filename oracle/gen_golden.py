@@ -2,7 +2,8 @@
 """ORACLE (test infrastructure only) — generate tests/golden/*.npz by running the
 REFERENCE's own NumPy code (/root/reference, read-only) in a child process.
 
-Run once in the build container:  ``python oracle/gen_golden.py``
+Run once in the build container:  ``python oracle/gen_golden.py`` (``--logistic``: only the
+logistic-model / momentum-SGD fixtures of section 4)
 (the reference does not exist on the GPU box; the committed .npz files travel instead).
 
 The reference needs a four-line import shim on Python 3.10 / NumPy 2:
@@ -167,10 +168,72 @@ np.savez_compressed(OUT + '/hmc_softmax.npz', post_weights=post['weights'], post
 print('ok')
 '''
 
+# ---- (4) logistic model and momentum SGD (SURVEY §8f rank 4): models/cpu/logistic.py,
+# inference/cpu/sgd.py.  Separate child so the earlier fixtures are not rewritten.
+CHILD_LOGISTIC = r'''
+import sys, types, collections, collections.abc, io, contextlib, importlib.util, json
+sys.dont_write_bytecode = True
+sys.path.insert(0, '/root/reference')
+collections.Iterable = collections.abc.Iterable
+sys.modules['h5py'] = types.ModuleType('h5py')
+import numpy as np
+np.int = int
+np.float = float
+spec = importlib.util.spec_from_file_location('golden_inputs', sys.argv[1])
+gi = importlib.util.module_from_spec(spec); spec.loader.exec_module(gi)
+OUT = sys.argv[2]
+from hamiltonian.models.cpu.logistic import logistic as ref_logistic
+from hamiltonian.models.cpu.softmax import softmax as ref_softmax
+from hamiltonian.inference.cpu.sgd import sgd as ref_sgd
+
+out = {}
+for i, (seed, B, D, ws) in enumerate(gi.LOGISTIC_CASES):
+    X, y, W, b = gi.logistic_inputs(seed, B, D, wscale=ws)
+    m = ref_logistic({'alpha': 0.25})
+    par = {'weights': W, 'bias': b}
+    g = m.grad(par, X_train=X, y_train=y)
+    out['c%d_gW' % i] = g['weights']
+    out['c%d_gb' % i] = g['bias']
+    out['c%d_net' % i] = m.net(par, X_train=X)
+    out['c%d_scalars' % i] = np.array([m.log_likelihood(par, X_train=X, y_train=y),
+                                       m.negative_log_posterior(par, X_train=X, y_train=y),
+                                       m.log_prior(par)])
+    bs = max(1, B // 3)
+    out['c%d_pred' % i] = m.predict(par, X, prob=False, batchsize=bs)
+    out['c%d_predp' % i] = m.predict(par, X, prob=True, batchsize=bs)
+np.savez_compressed(OUT + '/logistic.npz', **out)
+
+for name, c in gi.SGD_CONFIGS.items():
+    X, Y, start = gi.sgd_problem(c)
+    model = ref_logistic({'alpha': c['alpha']}) if c['model'] == 'logistic' else ref_softmax({'alpha': c['alpha']})
+    opt = ref_sgd(model, {k: v.copy() for k, v in start.items()}, step_size=c['step_size'])
+    np.random.seed(c['np_seed'])
+    with contextlib.redirect_stdout(io.StringIO()), contextlib.redirect_stderr(io.StringIO()):
+        if c['dropout']:
+            par, loss = opt.fit_dropout(epochs=c['epochs'], batch_size=c['B'], gamma=c['gamma'], p=c['p'],
+                                        X_train=X, y_train=Y)
+        else:
+            par, loss = opt.fit(epochs=c['epochs'], batch_size=c['B'], gamma=c['gamma'], X_train=X, y_train=Y)
+    np.savez_compressed(OUT + '/sgd_%s.npz' % name, weights=par['weights'], bias=par['bias'], loss=loss)
+print('ok')
+'''
+
+
+def _run_child(code, env):
+    r = subprocess.run([sys.executable, '-c', code, os.path.join(REPO, 'oracle', 'inputs.py'), OUT],
+                       env=env, capture_output=True, text=True)
+    sys.stdout.write(r.stdout[-2000:])
+    sys.stderr.write(r.stderr[-4000:])
+    if r.returncode != 0:
+        raise SystemExit(r.returncode)
+
 
 def main():
     os.makedirs(OUT, exist_ok=True)
     env = dict(os.environ, PYTHONDONTWRITEBYTECODE='1', OPENBLAS_NUM_THREADS='1')
+    if '--logistic' in sys.argv:            # only the logistic / sgd fixtures (4)
+        _run_child(CHILD_LOGISTIC, env)
+        return
     r = subprocess.run([sys.executable, '-c', CHILD, os.path.join(REPO, 'oracle', 'inputs.py'), OUT],
                        env=env, capture_output=True, text=True)
     sys.stdout.write(r.stdout[-2000:])

@@ -53,3 +53,42 @@ HMC_SOFTMAX_CONFIG = dict(N=50, D=16, K=10, alpha=0.01, step_size=1e-2, path_len
 
 GRAD_CASES = [(seed, B, ws) for seed in (0, 1, 2) for B in (32, 500) for ws in (0.01,)] + \
              [(3, 64, 5.0), (4, 64, 50.0), (5, 1, 0.01)]
+
+
+def logistic_inputs(seed, B, D, wscale=0.5):
+    """Two Gaussian clusters like benchmarks/1.-Simulated_data.ipynb (make_blobs, D=2 there):
+    X = N(±1.5, 1)^{B×D} by label, y ∈ {0,1} (float), W~N(0,wscale²)[D,1], b~N(0,wscale²)[1]."""
+    rs = np.random.RandomState(seed)
+    y = rs.randint(0, 2, B).astype(np.float64)
+    X = rs.normal(0, 1, (B, D)) + 1.5 * (2 * y[:, None] - 1)
+    W = rs.normal(0, wscale, (D, 1))
+    b = rs.normal(0, wscale, 1)
+    return X, y, W, b
+
+
+LOGISTIC_CASES = [(0, 50, 2, 0.5), (1, 500, 784, 0.05), (2, 1, 3, 0.5), (3, 77, 33, 2.0), (4, 64, 16, 40.0)]
+
+# sgd.fit / fit_dropout runs (sgd.py:25-70): (name, model, N, B, D, K, alpha, eta, gamma, epochs, p, seeds)
+SGD_CONFIGS = {
+    'fit_logistic':  dict(model='logistic', N=750, B=50, D=2, K=1, alpha=0.25, step_size=1e-3, gamma=0.9,
+                          epochs=4, data_seed=40, start_seed=41, dropout=False, p=0.5, np_seed=0),
+    'fit_softmax':   dict(model='softmax', N=600, B=100, D=64, K=10, alpha=0.01, step_size=1e-4, gamma=0.9,
+                          epochs=3, data_seed=42, start_seed=43, dropout=False, p=0.5, np_seed=0),
+    'drop_softmax':  dict(model='softmax', N=400, B=100, D=32, K=10, alpha=0.01, step_size=1e-4, gamma=0.9,
+                          epochs=2, data_seed=44, start_seed=45, dropout=True, p=0.8, np_seed=5),
+    'drop_logistic': dict(model='logistic', N=300, B=50, D=8, K=1, alpha=0.25, step_size=1e-3, gamma=0.5,
+                          epochs=2, data_seed=46, start_seed=47, dropout=True, p=0.5, np_seed=6),
+}
+
+
+def sgd_problem(c):
+    """Dataset and start point of an SGD_CONFIGS entry."""
+    if c['model'] == 'logistic':
+        X, y, _, _ = logistic_inputs(c['data_seed'], c['N'], c['D'])
+        rs = np.random.RandomState(c['start_seed'])
+        start = {'weights': 2 * rs.random_sample((c['D'], 1)), 'bias': 2 * rs.random_sample(1)}   # notebook :269
+        return X, y, start
+    X, Y = dataset(c['data_seed'], c['N'], c['D'], c['K'])
+    rs = np.random.RandomState(c['start_seed'])
+    start = {'weights': rs.normal(0, 0.01, (c['D'], c['K'])), 'bias': rs.normal(0, 0.01, c['K'])}
+    return X, Y, start

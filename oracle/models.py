@@ -2,6 +2,7 @@
 
 softmax        ← /root/reference/hamiltonian/models/cpu/softmax.py
 mvn_gaussian   ← /root/reference/hamiltonian/models/cpu/mvn_gaussian.py
+logistic       ← /root/reference/hamiltonian/models/cpu/logistic.py
 mlp            ← /root/reference/hamiltonian/models/gpu/mlp.py (Chainer; restated with
                  injected dropout masks — parity UNPINNED, cross-checked vs torch autograd)
 one_hot        ← /root/reference/hamiltonian/utils.py:4-8
@@ -101,6 +102,67 @@ class softmax:
             Z = np.random.binomial(1, p, size=X.shape)
         yhat = self.net(par, np.multiply(X, Z))
         return yhat if prob else yhat.argmax(axis=1)
+
+
+class logistic:
+    """models/cpu/logistic.py:10-87 — logistic regression (K = 1, sigmoid link), float64."""
+
+    def __init__(self, _hyper):
+        self.hyper = {var: np.asarray(_hyper[var]) for var in _hyper.keys()}     # :12-13
+
+    def log_prior(self, par, **args):                                    # :15-21
+        K = 0
+        for var in par.keys():
+            dim = (np.asarray(par[var])).size
+            K += dim * 0.5 * np.log(self.hyper['alpha'] / (2 * np.pi))
+            K -= 0.5 * self.hyper['alpha'] * np.sum(np.square(par[var]))
+        return K
+
+    def grad(self, par, **args):                                         # :24-41
+        X, y = _batch(args)
+        X = np.asarray(X)
+        y = np.asarray(y)
+        yhat = self.net(par, **args)
+        diff = y.reshape(-1, 1) - yhat
+        grad_w = np.dot(X.T, diff)
+        grad_b = np.sum(diff, axis=0)
+        grad = {}
+        grad['weights'] = grad_w - self.hyper['alpha'] * par['weights']
+        grad['weights'] = -1.0 * grad['weights']
+        grad['bias'] = grad_b - self.hyper['alpha'] * par['bias']
+        grad['bias'] = -1.0 * grad['bias']
+        return grad
+
+    def net(self, par, **args):                                          # :43-51
+        X, _ = _batch(args)
+        y_linear = np.dot(np.asarray(X), par['weights']) + par['bias']
+        y_linear = np.minimum(y_linear, CLIP_HI)
+        y_linear = np.maximum(y_linear, CLIP_LO)
+        return self.sigmoid(y_linear)
+
+    def sigmoid(self, y_linear):                                         # :53-55
+        norms = (1.0 + np.exp(-y_linear))
+        return 1.0 / norms
+
+    def negative_log_posterior(self, par, **args):                       # :57-62
+        n_data = np.asarray(args['X_train']).shape[0]
+        return (-1.0 / n_data) * (self.log_likelihood(par, **args) + self.log_prior(par, **args))
+
+    def log_likelihood(self, par, **args):                               # :64-72
+        X, y = _batch(args)
+        y = np.asarray(y)
+        y_pred = np.squeeze(self.net(par, **args), axis=1)
+        return np.sum(np.multiply(y, np.log(y_pred)) + np.multiply((1.0 - y), np.log(1.0 - y_pred)))
+
+    def loss(self, par, **args):
+        return self.negative_log_posterior(par, **args)
+
+    def predict(self, par, X, prob=False, batchsize=32):                 # :75-87
+        results = []
+        for start_idx in range(0, X.shape[0] - batchsize + 1, batchsize):
+            yhat = self.net(par, X_train=X[start_idx:start_idx + batchsize])
+            results.append(yhat if prob else (yhat > 0.5).astype(int).flatten())
+        return np.asarray(results).flatten()
 
 
 class mvn_gaussian:

@@ -6,6 +6,7 @@ sghmc   ← /root/reference/hamiltonian/inference/cpu/sghmc.py:16-39  + the A1 c
           ``sample`` consuming the first two entries of step()'s 3-tuple.
 sgld    ← /root/reference/hamiltonian/inference/cpu/sgld.py:13-46
 hmc     ← /root/reference/hamiltonian/inference/cpu/hmc.py:11-176
+sgd     ← /root/reference/hamiltonian/inference/cpu/sgd.py:11-70
 
 Random streams are used exactly as in the reference: the sampler's ``rng``
 (RandomState) for momenta/noise and the GLOBAL ``np.random`` for the path
@@ -252,3 +253,56 @@ class DualAveragingStepSize:                                              # hmc.
         self.log_averaged_step = eta * log_step + (1 - eta) * self.log_averaged_step
         self.t += 1
         return np.exp(log_step), np.exp(self.log_averaged_step)
+
+
+class sgd:
+    """cpu/sgd.py:11-70 — momentum SGD (fit) and input-dropout SGD (fit_dropout).  The tqdm
+    progress bar of the reference (:36,58) is omitted (display only)."""
+
+    def __init__(self, model, start_p, step_size=0.1):                  # :13-16
+        self.start = start_p
+        self.step_size = step_size
+        self.model = model
+        self.out = sys.stdout
+
+    iterate_minibatches = sgmcmc.iterate_minibatches                    # :19-23
+
+    def fit(self, epochs=1, batch_size=1, gamma=0.9, **args):           # :25-45
+        X = args['X_train']
+        y = args['y_train']
+        verbose = args.get('verbose', None)
+        epochs = int(epochs)
+        loss_val = np.zeros(epochs)
+        par = deepcopy(self.start)
+        momentum = {var: np.zeros_like(par[var]) for var in par.keys()}
+        for i in range(epochs):
+            for X_batch, y_batch in self.iterate_minibatches(X, y, batch_size):
+                grad_p = self.model.grad(par, X_train=X_batch, y_train=y_batch)
+                for var in par.keys():
+                    momentum[var] = gamma * momentum[var] - self.step_size * grad_p[var]
+                    par[var] += momentum[var]
+            loss_val[i] = self.model.negative_log_posterior(par, X_train=X_batch, y_train=y_batch)
+            if verbose and (i % (epochs / 10) == 0):
+                print('loss: {0:.4f}'.format(loss_val[i]), file=self.out)
+        return par, loss_val
+
+    def fit_dropout(self, epochs=1, batch_size=1, gamma=0.9, p=0.5, **args):   # :47-70
+        X = args['X_train']
+        y = args['y_train']
+        verbose = args.get('verbose', None)
+        epochs = int(epochs)
+        loss_val = np.zeros(epochs)
+        par = deepcopy(self.start)
+        momentum = {var: np.zeros_like(par[var]) for var in par.keys()}
+        for i in range(epochs):
+            for X_batch, y_batch in self.iterate_minibatches(X, y, batch_size):
+                Z = np.random.binomial(1, p, size=X_batch.shape)
+                X_batch_dropout = np.multiply(X_batch, Z)
+                grad_p = self.model.grad(par, X_train=X_batch_dropout, y_train=y_batch)
+                for var in par.keys():
+                    momentum[var] = gamma * momentum[var] - self.step_size * grad_p[var]
+                    par[var] += momentum[var]
+            loss_val[i] = -1. * self.model.log_likelihood(par, X_train=X_batch, y_train=y_batch)
+            if verbose and (i % (epochs / 10) == 0):
+                print('loss: {0:.4f}'.format(loss_val[i]), file=self.out)
+        return par, loss_val

@@ -41,6 +41,9 @@ def test_struct_layout_matches_header(nat):
     a = nat.SamplerArgs
     assert a.alpha.offset == 24 and a.X.offset == 40
     assert ctypes.sizeof(a) == a.out_E.offset + 8
+    s = nat.SgdArgs                           # 6 ints, 3 doubles, 3 pointers, int, double, int, ...
+    assert s.alpha.offset == 24 and s.X.offset == 48 and s.dropout.offset == 72 and s.keep_p.offset == 80
+    assert s.seed.offset == 112 and s.W.offset == 128 and ctypes.sizeof(s) == 160
 
 
 def test_philox_host_generator(nat):
@@ -70,9 +73,12 @@ def test_python_surface_imports():
     import hamiltonian.inference.gpu.hmc as m3
     import hamiltonian.models.gpu.softmax as m4
     import hamiltonian.models.gpu.mvn_gaussian as m5
+    import hamiltonian.models.gpu.logistic as m6
+    import hamiltonian.inference.gpu.sgd as m7
     import hamiltonian.utils as u
     assert hasattr(m1, "sghmc") and hasattr(m2, "sgld") and hasattr(m3, "hmc")
     assert hasattr(m4, "softmax") and hasattr(m5, "mvn_gaussian")
+    assert hasattr(m6, "logistic") and hasattr(m7, "sgd")
     np.testing.assert_array_equal(u.one_hot([2, 0], 3), [[0, 0, 1], [1, 0, 0]])
 
 
