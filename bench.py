@@ -47,6 +47,8 @@ def parse():
                     help="chains per GPU of the secondary chain-batched measurement (0 = skip)")
     ap.add_argument("--mlp-steps", type=int, default=40,
                     help="SGHMC steps of the secondary config-3 MLP measurement (0 = skip)")
+    ap.add_argument("--sgld-steps", type=int, default=400,
+                    help="SGLD steps of the secondary config-5 (D=2048, K=38) measurement (0 = skip)")
     return ap.parse_args()
 
 
@@ -218,6 +220,69 @@ def mlp_measure(X, lab, n_steps, rank, cpu_seconds):
     return out
 
 
+V_D, V_K, V_N = 2048, 38, 20000               # BASELINE config 5 (PlantVillage-like features; SURVEY §8 "V")
+V_P = V_D * V_K + V_K
+V_FLOP_PER_STEP = 4.0 * B * V_D * V_K         # 155.6 MFLOP per SGLD step
+
+
+def plantvillage_measure(n_steps, rank, cpu_seconds):
+    """Secondary measurement, BASELINE config 5: softmax SGLD on conv-feature-like inputs (D=2048,
+    K=38, batch 500), one chain per GPU, float64, device Philox noise, through hmcx_sgld_run (the
+    wide path, hmcx_wide.hip).  Logging cadence of the reference (log-likelihood every 10
+    minibatches) included.  CPU baseline: the oracle's SGLD on the same shape."""
+    import torch
+    from dropout_hamiltonian_montecarlo_amd.hamiltonian.models.gpu.softmax import softmax
+    from dropout_hamiltonian_montecarlo_amd.hamiltonian.inference.gpu.sgld import sgld
+    Xv = np.random.RandomState(5).rand(V_N, V_D)
+    Yv = np.eye(V_K)[np.random.RandomState(6).randint(0, V_K, V_N)]
+    m = softmax({"alpha": ALPHA}, dtype=torch.float64)
+    s = sgld(m, {"weights": np.zeros((V_D, V_K)), "bias": np.zeros(V_K)}, step_size=1e-4, noise="philox",
+             seed=17, chain=rank)
+    s.out = io.StringIO()
+    data = s._upload_data(Xv, Yv)
+    state = s._init_state()
+    nb = V_N // B
+    rows = [(i % nb) * B for i in range(n_steps)]
+    s._run(state, data, rows, [1e-4] * n_steps, None, B)       # warm-up: same call shape
+    torch.cuda.synchronize()
+    m.ctx.set_timing(True)
+    t0 = time.perf_counter()
+    s._run(state, data, rows, [1e-4] * n_steps, None, B)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    kms, _ = m.ctx.get_timing()
+    m.ctx.set_timing(False)
+    tf = V_FLOP_PER_STEP * n_steps / (kms * 1e-3) / 1e12
+    xbytes = 2.0 * B * V_D * 8                    # X tile read by the forward and by the gradient GEMM
+    out = {"workload": "PlantVillage-like softmax SGLD, D=2048 features, K=38, batch 500, 1 chain (BASELINE config 5)",
+           "dtype": "f64", "param_dim": V_P, "steps": n_steps, "us_per_step": kms * 1e3 / n_steps,
+           "leapfrogs_per_s": n_steps / dt, "value": n_steps / dt * V_P, "unit": "leapfrog-steps/s x param-dim",
+           "roofline": {"bound": "mfma", "achieved": tf, "peak": MFMA_PEAK_TFLOPS["f64"], "unit": "TFLOP/s",
+                        "frac": tf / MFMA_PEAK_TFLOPS["f64"], "device_ms": kms,
+                        "hbm_GBps_X": xbytes * n_steps / (kms * 1e-3) / 1e9,
+                        "kernel": "k_wfwd + k_wsoft + k_wgrad per step (+ logging forward every 10th)"}}
+    if cpu_seconds > 0:
+        from oracle import models as om, samplers as osm
+        import threadpoolctl
+        n_cpu = 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < cpu_seconds:
+            o = osm.sgld(om.softmax({"alpha": ALPHA}), {"weights": np.zeros((V_D, V_K)), "bias": np.zeros(V_K)},
+                         step_size=1e-4, verbose=False)
+            o.out = io.StringIO()
+            np.random.seed(n_cpu)
+            o.sample(epochs=1, burnin=0, batch_size=B, rng=np.random.RandomState(n_cpu),
+                     X_train=Xv[:10 * B], y_train=Yv[:10 * B])
+            n_cpu += 10
+        dtc = time.perf_counter() - t0
+        blas = [i for i in threadpoolctl.threadpool_info() if i.get("user_api") == "blas"]
+        out["cpu_baseline"] = {"value": n_cpu / dtc * V_P, "unit": "leapfrog-steps/s x param-dim",
+                               "cores": int(max((i.get("num_threads", 1) for i in blas), default=1)), "kind": "port",
+                               "sample": "%d oracle SGLD steps (NumPy f64, B=500, D=2048, K=38, logging every 10), %.1f s"
+                                         % (n_cpu, dtc), "leapfrogs_per_s": n_cpu / dtc}
+    return out
+
+
 def main():
     args = parse()
     import torch
@@ -299,6 +364,10 @@ def main():
         lab = np.argmax(Y, axis=1)
         mlp_out = mlp_measure(X, lab, args.mlp_steps, rank, args.cpu_seconds / 2 if world == 1 and rank == 0 else 0)
         parallel.barrier()
+    v_out = None
+    if args.sgld_steps > 0:
+        v_out = plantvillage_measure(args.sgld_steps, rank, args.cpu_seconds / 2 if world == 1 and rank == 0 else 0)
+        parallel.barrier()
     if rank != 0:
         return
     path = "persistent" if (args.path != "kernels") else "kernels"
@@ -337,6 +406,7 @@ def main():
         "cpu_baseline": None,
         "chain_batched": batched,
         "mlp": mlp_out,
+        "plantvillage_sgld": v_out,
     }
     if world == 1 and args.cpu_seconds > 0:
         out["cpu_baseline"] = cpu_baseline(X, Y, args.cpu_seconds)
