@@ -13,7 +13,7 @@ import threading
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libhmcx.so")
+LIB_PATH = os.path.join(_HERE, "lib", os.environ.get("HMCX_LIB", "libhmcx.so"))   # HMCX_LIB: A/B builds
 
 HMCX_F32, HMCX_F64 = 0, 1
 NOISE_BUFFER, NOISE_PHILOX = 0, 1

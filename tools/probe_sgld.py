@@ -18,6 +18,8 @@ dev = torch.device('cuda', 0)
 X = torch.from_numpy(np.random.RandomState(0).rand(N, D)).to(dev, dtype)
 Y = torch.from_numpy(np.eye(K)[np.random.RandomState(1).randint(0, K, N)]).to(dev, dtype)
 ctx = nat.context(0)
+if 'graph' in sys.argv:
+    ctx.set_graph_mode(True)
 W = torch.zeros(D, C * K, dtype=dtype, device=dev)
 b = torch.zeros(C * K, dtype=dtype, device=dev)
 row0 = (np.arange(steps) % (N // B) * B).astype(np.int64)
