@@ -48,32 +48,37 @@ template <typename T> struct MaskSrc {
   T scale;
   int mn;
 };
+// Mask reads: both candidate sources are loaded unconditionally (an absent source reads a zero
+// dummy) and pinned by an empty asm, so hipcc cannot sink the loads into the (wave-uniform) source
+// branches — a load inside a branch is waited for on the spot (s_waitcnt vmcnt(0) per mask value),
+// which serialised the 48 mask/activation loads of the layer-3 backward.
+__device__ __align__(16) unsigned char g_mask_dummy[32];
 template <typename T> __device__ inline T mval(const MaskSrc<T>& s, int which, size_t i) {
   const size_t e = (size_t)which * s.mn + i;
-  if (s.vals) return s.vals[e];
-  if (s.keep) return s.keep[e] ? s.scale : T(0);
-  return T(1);
+  const T* vp = s.vals ? s.vals + e : reinterpret_cast<const T*>(g_mask_dummy);
+  const uint8_t* kp = s.keep ? s.keep + e : g_mask_dummy;
+  T v = *vp;
+  uint32_t k = *kp;
+  asm volatile("" : "+v"(v), "+v"(k));
+  return s.vals ? v : (s.keep ? (k ? s.scale : T(0)) : T(1));
 }
 // V consecutive mask values from an element index that is a multiple of V (V = 16 / sizeof T)
 template <typename T, int V> __device__ inline void mvals(const MaskSrc<T>& s, int which, size_t i, T (&m)[V]) {
   const size_t e = (size_t)which * s.mn + i;
-  if (s.vals) {
+  const T* vp = s.vals ? s.vals + e : reinterpret_cast<const T*>(g_mask_dummy);
+  const uint8_t* kp = s.keep ? s.keep + e : g_mask_dummy;
+  T v[V];
 #pragma unroll
-    for (int q = 0; q < V; ++q) m[q] = s.vals[e + q];
-  } else if (s.keep) {
-    if constexpr (V == 4) {
-      const uint32_t k = *reinterpret_cast<const uint32_t*>(s.keep + e);
+  for (int q = 0; q < V; ++q) v[q] = vp[q];
+  uint32_t k;
+  if constexpr (V == 4) k = *reinterpret_cast<const uint32_t*>(kp);
+  else k = *reinterpret_cast<const uint16_t*>(kp);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) m[q] = ((k >> (8 * q)) & 0xFF) ? s.scale : T(0);
-    } else {
-      const uint16_t k = *reinterpret_cast<const uint16_t*>(s.keep + e);
-      m[0] = (k & 0xFF) ? s.scale : T(0);
-      m[1] = (k >> 8) ? s.scale : T(0);
-    }
-  } else {
+  for (int q = 0; q < V; ++q) asm volatile("" : "+v"(v[q]));
+  asm volatile("" : "+v"(k));
 #pragma unroll
-    for (int q = 0; q < V; ++q) m[q] = T(1);
-  }
+  for (int q = 0; q < V; ++q)
+    m[q] = s.vals ? v[q] : (s.keep ? (((k >> (8 * q)) & 0xFF) ? s.scale : T(0)) : T(1));
 }
 
 __device__ inline bool keep_flag(uint32_t w) {                // Chainer dropout: keep iff u >= ratio
@@ -271,11 +276,20 @@ __device__ inline void l3_backward(const MMArgs<T>& a, const T* zt, int zs, int 
   if (a.ga2) {
     const bool wl = N * nm + nt <= scr_n;                      // W3 in LDS (+ nt values for the combine)
     T* w3 = scr + nt;
-    if (wl) {
-      for (int e = tid; e < N * nm; e += nt) w3[e] = a.W3[e];
+    if (wl) {                                                  // 8 loads in flight per thread
+      const int nw = N * nm;
+      for (int e0 = tid; e0 < nw; e0 += 8 * nt) {
+        T v[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = a.W3[min(e0 + q * nt, nw - 1)];
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          if (e0 + q * nt < nw) w3[e0 + q * nt] = v[q];
+      }
       __syncthreads();
     }
     const int R = max(1, nt / nm), cols = nt / R;
+    constexpr int RB = 16;                                     // rows per pass (one pass at R = 2)
 #pragma unroll 1
     for (int jb = 0; jb < nm; jb += cols) {
       const int j = jb + tid % cols, g = tid / cols;
@@ -283,11 +297,11 @@ __device__ inline void l3_backward(const MMArgs<T>& a, const T* zt, int zs, int 
       T cs = T(0);
       if (act) {
 #pragma unroll 1
-        for (int r0 = g; r0 < rows; r0 += 8 * R) {
-          // 8 rows per pass: their h2 / mask loads go out first, then 8 independent dot products
-          T hv[8], m1v[8], m2v[8], acc8[8];
+        for (int r0 = g; r0 < rows; r0 += RB * R) {
+          // RB rows per pass: their h2 / mask loads go out first, then RB independent dot products
+          T hv[RB], m1v[RB], m2v[RB], acc8[RB];
 #pragma unroll
-          for (int c = 0; c < 8; ++c) {
+          for (int c = 0; c < RB; ++c) {
             const int r = min(r0 + c * R, rows - 1);
             const size_t i = (size_t)(m0 + r) * nm + j;
             hv[c] = a.h2[i];
@@ -299,10 +313,10 @@ __device__ inline void l3_backward(const MMArgs<T>& a, const T* zt, int zs, int 
           for (int o = 0; o < N; ++o) {
             const T w = wl ? w3[o * nm + j] : a.W3[(size_t)o * nm + j];
 #pragma unroll
-            for (int c = 0; c < 8; ++c) acc8[c] += zt[min(r0 + c * R, 31) * zs + o] * w;
+            for (int c = 0; c < RB; ++c) acc8[c] += zt[min(r0 + c * R, 31) * zs + o] * w;
           }
 #pragma unroll
-          for (int c = 0; c < 8; ++c) {
+          for (int c = 0; c < RB; ++c) {
             const int r = r0 + c * R;
             T t = acc8[c] * m2v[c];
             t = t * (hv[c] > T(0) ? T(1) : T(0));
