@@ -172,7 +172,7 @@ template <typename T> int sgd_run_t(hmcx_ctx*, const hmcx_sgd_args*);
 template <typename T> int sumsq_t(hmcx_ctx*, const void*, int64_t, double*);
 template <typename T> int sghmc_run_t(hmcx_ctx*, const hmcx_sampler_args*);
 template <typename T> int sgld_run_t(hmcx_ctx*, const hmcx_sampler_args*);
-bool sgld_wide_eligible(const hmcx_sampler_args*);       // hmcx_wide.hip: one chain, 16 < K ≤ 64
+bool sgld_wide_eligible(const hmcx_sampler_args*);       // hmcx_wide.hip: one chain, K ≤ 64
 template <typename T> int sgld_wide_t(hmcx_ctx*, const hmcx_sampler_args*);
 int hmc_mvn_run(hmcx_ctx*, const hmcx_hmc_mvn_args*);
 template <typename T> int mlp_grad_t(hmcx_ctx*, const void*, const int32_t*, int, int, int, int,

@@ -1,4 +1,4 @@
-// hmcx_wide.hip — single-chain SGLD for wide softmax models (BASELINE config 5: PlantVillage-like
+// hmcx_wide.hip — single-chain SGLD (any K ≤ 64; designed for BASELINE config 5: PlantVillage-like
 // conv features, D = 2048, K = 38, batch 500), three launches per step.
 //
 // Mathematics and op order: cpu/sgld.py:31-46 (p = N(0,(2ε)²) then p += −½ε·g, q += p) with the
@@ -318,8 +318,9 @@ bool sgld_wide_eligible(const hmcx_sampler_args* s) {
   const char* env = getenv("HMCX_SGLD_WIDE");
   if (env && env[0] == '0') return false;
   if (s->C != 1 || s->K > 64 || s->K < 1 || s->B < 1 || s->D < 1) return false;
-  if (env && env[0] == '1') return true;
-  return s->K > 16;
+  // faster than the kernel-per-phase path for every single-chain shape measured (MNIST D=784,
+  // K=10: 18.0 vs 20.5 µs per f64 step; config 5 D=2048, K=38: 26.4 vs 35.1 µs)
+  return true;
 }
 
 template <typename T, int KB>

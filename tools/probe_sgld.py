@@ -13,7 +13,7 @@ dtype = torch.float32 if 'f32' in sys.argv else torch.float64
 nums = [int(a) for a in sys.argv[1:] if a.isdigit()]
 steps = nums[0] if nums else 200
 C = nums[1] if len(nums) > 1 else 1
-N, B, D, K = 20000, 500, 2048, 38
+N, B, D, K = (60000, 500, 784, 10) if 'mnist' in sys.argv else (20000, 500, 2048, 38)
 dev = torch.device('cuda', 0)
 X = torch.from_numpy(np.random.RandomState(0).rand(N, D)).to(dev, dtype)
 Y = torch.from_numpy(np.eye(K)[np.random.RandomState(1).randint(0, K, N)]).to(dev, dtype)
