@@ -31,30 +31,82 @@ bool Workspace::retry() {
   return true;
 }
 
+static int ev_take(hmcx_ctx* ctx, hipEvent_t* ev) {
+  if (!ctx->ev_pool.empty()) {
+    *ev = ctx->ev_pool.back();
+    ctx->ev_pool.pop_back();
+    return HMCX_OK;
+  }
+  HMCX_HIP(ctx, hipEventCreate(ev));
+  return HMCX_OK;
+}
+
 int timing_collect(hmcx_ctx* ctx) {
-  if (!ctx->t_pending) return HMCX_OK;
-  ctx->t_pending = false;
-  HMCX_HIP(ctx, hipEventSynchronize(ctx->tev1));
-  float ms = 0.f;
-  HMCX_HIP(ctx, hipEventElapsedTime(&ms, ctx->tev0, ctx->tev1));
-  ctx->t_ms += ms;
-  ctx->t_n += 1;
+  for (auto& pr : ctx->t_pend) {
+    HMCX_HIP(ctx, hipEventSynchronize(pr.second));
+    float ms = 0.f;
+    HMCX_HIP(ctx, hipEventElapsedTime(&ms, pr.first, pr.second));
+    ctx->t_ms += ms;
+    ctx->t_n += 1;
+    ctx->ev_pool.push_back(pr.first);
+    ctx->ev_pool.push_back(pr.second);
+  }
+  ctx->t_pend.clear();
   return HMCX_OK;
 }
 
 int timing_begin(hmcx_ctx* ctx, hipStream_t st) {
   if (!ctx->timing) return HMCX_OK;
-  int rc = timing_collect(ctx);
+  int rc = ev_take(ctx, &ctx->t_open);
   if (rc) return rc;
-  HMCX_HIP(ctx, hipEventRecord(ctx->tev0, st));
+  HMCX_HIP(ctx, hipEventRecord(ctx->t_open, st));
   return HMCX_OK;
 }
 
 int timing_end(hmcx_ctx* ctx, hipStream_t st) {
-  if (!ctx->timing) return HMCX_OK;
-  HMCX_HIP(ctx, hipEventRecord(ctx->tev1, st));
-  ctx->t_pending = true;
+  if (!ctx->timing || !ctx->t_open) return HMCX_OK;
+  hipEvent_t e1 = nullptr;
+  int rc = ev_take(ctx, &e1);
+  if (rc) return rc;
+  HMCX_HIP(ctx, hipEventRecord(e1, st));
+  ctx->t_pend.emplace_back(ctx->t_open, e1);
+  ctx->t_open = nullptr;
   return HMCX_OK;
+}
+
+int abort_poll(hmcx_ctx* ctx, bool block) {
+  bool aborted = false;
+  size_t keep = 0;
+  for (size_t i = 0; i < ctx->abort_pend.size(); ++i) {
+    auto pr = ctx->abort_pend[i];
+    hipError_t e = block ? hipEventSynchronize(pr.first) : hipEventQuery(pr.first);
+    if (e == hipErrorNotReady) {
+      ctx->abort_pend[keep++] = pr;
+      continue;
+    }
+    if (e != hipSuccess) return set_error(ctx, HMCX_EHIP, std::string("abort check: ") + hipGetErrorString(e));
+    if (ctx->abort_host[pr.second]) aborted = true;
+    ctx->ev_pool.push_back(pr.first);
+  }
+  ctx->abort_pend.resize(keep);
+  if (aborted) return set_error(ctx, HMCX_EHIP, "persistent SGHMC: hand-off timed out (workgroups not co-resident?)");
+  return HMCX_OK;
+}
+
+int abort_defer(hmcx_ctx* ctx, const int* dev_flag, hipStream_t st) {
+  if (!ctx->abort_host) HMCX_HIP(ctx, hipHostMalloc((void**)&ctx->abort_host, ABORT_SLOTS * sizeof(int), hipHostMallocDefault));
+  if (ctx->abort_pend.size() >= (size_t)ABORT_SLOTS / 2) {     // bound the in-flight checks
+    int rc = abort_poll(ctx, true);
+    if (rc) return rc;
+  }
+  const int slot = (int)(ctx->abort_next++ % ABORT_SLOTS);
+  hipEvent_t ev = nullptr;
+  int rc = ev_take(ctx, &ev);
+  if (rc) return rc;
+  HMCX_HIP(ctx, hipMemcpyAsync(ctx->abort_host + slot, dev_flag, sizeof(int), hipMemcpyDeviceToHost, st));
+  HMCX_HIP(ctx, hipEventRecord(ev, st));
+  ctx->abort_pend.emplace_back(ev, slot);
+  return abort_poll(ctx, false);                                 // earlier launches that have finished
 }
 
 void begin_call(hmcx_ctx* ctx) {
@@ -276,8 +328,7 @@ int hmcx_create(int device, hmcx_ctx** out) {
   c->device = device;
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->stage_ev, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreate(&c->tev0) != hipSuccess || hipEventCreate(&c->tev1) != hipSuccess) {
+      hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming) != hipSuccess) {
     delete c;
     return HMCX_EHIP;
   }
@@ -299,8 +350,11 @@ int hmcx_destroy(hmcx_ctx* ctx) {
   if (ctx->stage) (void)hipHostFree(ctx->stage);
   if (ctx->stage_ev) (void)hipEventDestroy(ctx->stage_ev);
   if (ctx->ev_in) (void)hipEventDestroy(ctx->ev_in);
-  if (ctx->tev0) (void)hipEventDestroy(ctx->tev0);
-  if (ctx->tev1) (void)hipEventDestroy(ctx->tev1);
+  for (auto& pr : ctx->t_pend) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
+  if (ctx->t_open) (void)hipEventDestroy(ctx->t_open);
+  for (auto& pr : ctx->abort_pend) (void)hipEventDestroy(pr.first);
+  for (auto e : ctx->ev_pool) (void)hipEventDestroy(e);
+  if (ctx->abort_host) (void)hipHostFree(ctx->abort_host);
   for (auto& g : ctx->graveyard) {
     (void)hipGraphExecDestroy(g.first);
     (void)hipEventDestroy(g.second);
@@ -321,7 +375,7 @@ int hmcx_set_stream(hmcx_ctx* ctx, void* stream) {
 int hmcx_synchronize(hmcx_ctx* ctx) {
   HMCX_GUARD_CTX(ctx);
   HMCX_HIP(ctx, hipStreamSynchronize(ctx->stream));
-  return HMCX_OK;
+  return abort_poll(ctx, true);                    // reports an aborted persistent launch
 }
 
 int hmcx_set_sghmc_path(hmcx_ctx* ctx, int path) {
@@ -339,9 +393,9 @@ int hmcx_set_graph_mode(hmcx_ctx* ctx, int enabled) {
 
 int hmcx_set_timing(hmcx_ctx* ctx, int enabled) {
   HMCX_GUARD_CTX(ctx);
-  if (ctx->t_pending) (void)hipEventSynchronize(ctx->tev1);
+  int rc = timing_collect(ctx);                    // drain (and discard) pending intervals
+  if (rc) return rc;
   ctx->timing = enabled ? 1 : 0;
-  ctx->t_pending = false;
   ctx->t_ms = 0.0;
   ctx->t_n = 0;
   return HMCX_OK;

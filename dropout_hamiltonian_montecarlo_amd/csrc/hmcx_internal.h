@@ -28,13 +28,21 @@ struct hmcx_ctx {
   // hipGraph mode: capture happens on own_stream (the legacy default stream cannot be captured)
   hipEvent_t ev_in = nullptr, ev_out = nullptr;
   std::vector<std::pair<hipGraphExec_t, hipEvent_t>> graveyard;   // executed graphs awaiting release
-  // device timing of sampler launches (hmcx_set_timing): events bracket the kernels of each run
+  // device timing of sampler launches (hmcx_set_timing): an event pair brackets the kernels of each
+  // run; pairs are collected lazily (hmcx_get_timing), so timing never serialises consecutive calls
   int timing = 0;
-  hipEvent_t tev0 = nullptr, tev1 = nullptr;
-  bool t_pending = false;
+  hipEvent_t t_open = nullptr;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> t_pend;
   double t_ms = 0.0;
   long long t_n = 0;
+  std::vector<hipEvent_t> ev_pool;     // recycled timing-capable events
+  // deferred abort checks of persistent launches: the abort word is copied into a pinned slot and
+  // checked once the launch's event has completed (next call, hmcx_synchronize), not by a per-call sync
+  int* abort_host = nullptr;           // pinned [ABORT_SLOTS]
+  std::vector<std::pair<hipEvent_t, int>> abort_pend;
+  unsigned abort_next = 0;
 };
+constexpr int ABORT_SLOTS = 64;
 
 namespace hmcx {
 
@@ -49,6 +57,11 @@ int set_error(hmcx_ctx* ctx, int code, const std::string& msg);
 int timing_begin(hmcx_ctx* ctx, hipStream_t st);
 int timing_end(hmcx_ctx* ctx, hipStream_t st);
 int timing_collect(hmcx_ctx* ctx);
+// Deferred abort check of a persistent launch: copy the device abort word into a pinned slot after
+// the launch (stream-ordered) and remember it; abort_poll folds completed checks (block: wait for all)
+// and returns an error if any launch had aborted.
+int abort_defer(hmcx_ctx* ctx, const int* dev_flag, hipStream_t st);
+int abort_poll(hmcx_ctx* ctx, bool block);
 
 #define HMCX_HIP(ctx, expr)                                                                  \
   do {                                                                                       \

@@ -994,10 +994,11 @@ int sghmc_p2_t(hmcx_ctx* ctx, const hmcx_sampler_args* s, const PersistPlan2& pl
     return set_error(ctx, HMCX_EUNSUPPORTED, "persistent SGHMC: workgroups cannot be co-resident");
   HMCX_HIP(ctx, hipLaunchKernel(kfn, dim3(G), dim3(QTH), kargs, (unsigned)pl.lds, ctx->stream));
   if ((rc = timing_end(ctx, ctx->stream))) return rc;
+  if (!dprof && !dtrace)                         // no per-call sync: checked once the launch is done
+    return abort_defer(ctx, a.abort_flag, ctx->stream);
   int flag = 0;
   HMCX_HIP(ctx, hipMemcpyAsync(&flag, a.abort_flag, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
   HMCX_HIP(ctx, hipStreamSynchronize(ctx->stream));
-  if ((rc = timing_collect(ctx))) return rc;
   if (dprof) {
     unsigned long long h[16];
     HMCX_HIP(ctx, hipMemcpy(h, dprof, sizeof(h), hipMemcpyDeviceToHost));

@@ -87,20 +87,27 @@ class sghmc(sgmcmc):
     def _run(self, state, data, rows, eps, rng, batch_size):
         if self.model._hmcx_model == 'mlp':
             return self._run_mlp(state, data, rows, eps, rng, batch_size)
+        return self._collect(self._enqueue(state, data, rows, eps, rng, batch_size))
+
+    def _enqueue(self, state, data, rows, eps, rng, batch_size):
+        """Prepare the schedule of len(rows) steps and enqueue them (one hmcx_sghmc_run call) without
+        waiting: the returned handle is read back by _collect.  A caller may enqueue the next call
+        before collecting this one — the state stays on the device and stream order keeps the calls
+        in sequence — so the host work of one call overlaps the device work of the previous one."""
         Xd, Yd = data
         W, b = state['weights'], state['bias']
         C = self.chains
         D, K = W.shape[0], W.shape[1] // C
         P = D * K + K
         n_steps = len(rows)
+        t0 = len(self.trace) if self.trace is not None else 0
         n_iter, u, noise, noise_off = self._schedule(n_steps, eps, rng, P)
         n_iter, u, noise_off = (np.ascontiguousarray(x.reshape(-1)) for x in (n_iter, u, noise_off))
         dev = self.model.device
         noise_d = torch.from_numpy(noise).to(dev) if noise is not None else None
-        out_A = torch.empty(n_steps * C, dtype=torch.float64, device=dev)
+        out_f = torch.empty(4 * n_steps * C, dtype=torch.float64, device=dev)     # A, ll, E (2)
         out_acc = torch.empty(n_steps * C, dtype=torch.int32, device=dev)
-        out_ll = torch.empty(n_steps * C, dtype=torch.float64, device=dev)
-        out_E = torch.empty(2 * n_steps * C, dtype=torch.float64, device=dev)
+        out_A, out_ll, out_E = out_f[:n_steps * C], out_f[n_steps * C:2 * n_steps * C], out_f[2 * n_steps * C:]
         row0 = np.asarray(rows, dtype=np.int64)
         eps_a = np.asarray(eps, dtype=np.float64)
         a = nat.SamplerArgs()
@@ -123,17 +130,25 @@ class sghmc(sgmcmc):
         ctx = nat.context(dev)
         ctx.check(ctx.lib.hmcx_sghmc_run(ctx.h, a), "hmcx_sghmc_run")
         self.global_step += n_steps
+        return dict(out_f=out_f, out_acc=out_acc, noise_d=noise_d, n_steps=n_steps, C=C, t0=t0, ctx=ctx)
+
+    def _collect(self, h):
+        """Read back one enqueued call (waits for it) and fill the trace entries of its steps."""
+        n_steps, C = h['n_steps'], h['C']
+        f = h['out_f'].cpu().numpy()
+        acc = h['out_acc'].cpu().numpy().astype(bool)
+        ctx = h['ctx']
+        ctx.check(ctx.lib.hmcx_synchronize(ctx.h), "hmcx_sghmc_run")        # deferred abort check
+        nsc = n_steps * C
+        A, ll, E = f[:nsc], f[nsc:2 * nsc], f[2 * nsc:]
         if C == 1:
-            res = RunResult(out_A.cpu().numpy(), out_acc.cpu().numpy().astype(bool), out_ll.cpu().numpy(),
-                            out_E.cpu().numpy().reshape(n_steps, 2))
+            res = RunResult(A, acc, ll, E.reshape(n_steps, 2))
         else:
-            res = RunResult(out_A.cpu().numpy().reshape(n_steps, C),
-                            out_acc.cpu().numpy().astype(bool).reshape(n_steps, C),
-                            out_ll.cpu().numpy().reshape(n_steps, C), out_E.cpu().numpy().reshape(n_steps, C, 2))
-        del noise_d
+            res = RunResult(A.reshape(n_steps, C), acc.reshape(n_steps, C), ll.reshape(n_steps, C),
+                            E.reshape(n_steps, C, 2))
         if self.trace is not None:
             for s in range(n_steps):
-                t = self.trace[len(self.trace) - n_steps + s]
+                t = self.trace[h['t0'] + s]
                 t['A'] = float(res.A[s]) if C == 1 else res.A[s].copy()
                 t['accepted'] = bool(res.accepted[s]) if C == 1 else res.accepted[s].copy()
         return res
