@@ -127,24 +127,41 @@ class sgmcmc:
             raise ValueError("batch_size larger than the dataset: no minibatch (sgmcmc.py:36)")
         data = self._upload_data(X, y)
         state = self._init_state()
+        # Epoch calls are pipelined where the sampler supports it (_enqueue/_collect): epoch i+1 is
+        # enqueued before epoch i is read back, and a device copy of the state taken right after
+        # epoch i stands in for the state itself.  Printed lines and results are unchanged.
+        pipelined = hasattr(self, '_enqueue') and self.model._hmcx_model != 'mlp'
+
+        def launch(eps):
+            if not pipelined:
+                return self._run(state, data, rows, eps, rng, batch_size)
+            return self._enqueue(state, data, rows, eps, rng, batch_size)
+
+        def finish(h):
+            return self._collect(h) if pipelined else h
+
         print('start burnin', file=self.out)
-        for i in range(int(burnin)):
-            eps = [self.step_size] * len(rows)
-            res = self._run(state, data, rows, eps, rng, batch_size)
+
+        def burnin_log(i, res):
             for j in range(len(rows)):
                 if (j % self.log_every) == 0:
                     ll = -1.0 * np.ravel(res.ll[j])[0]
                     print('burnin {0}, loss: {1:.4f}, mini-batch update : {2}'.format(i, ll, j), file=self.out)
+
+        pend = None
+        for i in range(int(burnin)):
+            h = launch([self.step_size] * len(rows))
+            if pend is not None:
+                burnin_log(i - 1, finish(pend))
+            pend = h
+        if pend is not None:
+            burnin_log(int(burnin) - 1, finish(pend))
         logp_samples = np.zeros(epochs) if self.chains == 1 else np.zeros((epochs, self.chains))
         posterior = {var: [] for var in self.start.keys()}
         print('start sampling', file=self.out)
         initial_step_size = self.step_size
-        for i in range(epochs):
-            eps = []
-            for j in range(len(rows)):
-                eps.append(self.step_size)
-                self.step_size = self.lr_schedule(initial_step_size, j, decay_factor, num_batches)
-            res = self._run(state, data, rows, eps, rng, batch_size)
+
+        def epoch_done(i, res, snap):
             for j in range(len(rows)):
                 if (j % self.log_every) == 0:
                     ll = -1.0 * np.ravel(res.ll[j])[0]
@@ -154,11 +171,28 @@ class sgmcmc:
                 logp_samples[i] = res.nlp[-1]
             else:
                 logp_samples[i] = (-1.0 / batch_size) * (res.ll[-1] + self._log_prior())
-            host = self._state_to_host(state)
+            host = self._state_to_host(snap)
             for var in self.start.keys():
                 posterior[var].append(host[var])
             if self.verbose and (i % (epochs / 10) == 0):
                 print('loss: {0:.4f}'.format(np.ravel(logp_samples[i])[0]), file=self.out)
+
+        pend = None
+        for i in range(epochs):
+            eps = []
+            for j in range(len(rows)):
+                eps.append(self.step_size)
+                self.step_size = self.lr_schedule(initial_step_size, j, decay_factor, num_batches)
+            h = launch(eps)
+            if not pipelined:                       # _run has already completed the epoch
+                epoch_done(i, h, state)
+                continue
+            snap = {var: state[var].clone() for var in state}   # stream-ordered copy of the epoch's state
+            if pend is not None:
+                epoch_done(i - 1, finish(pend[0]), pend[1])
+            pend = (h, snap)
+        if pend is not None:
+            epoch_done(epochs - 1, finish(pend[0]), pend[1])
         for var in self.start.keys():
             posterior[var] = np.array(posterior[var])
             if self.chains > 1:
