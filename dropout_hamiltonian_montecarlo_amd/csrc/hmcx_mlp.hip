@@ -53,14 +53,23 @@ template <typename T> struct MaskSrc {
 // branches — a load inside a branch is waited for on the spot (s_waitcnt vmcnt(0) per mask value),
 // which serialised the 48 mask/activation loads of the layer-3 backward.
 __device__ __align__(16) unsigned char g_mask_dummy[32];
-template <typename T> __device__ inline T mval(const MaskSrc<T>& s, int which, size_t i) {
+template <typename T> struct MRaw { T v; uint32_t k; };
+// unconditional raw loads of element i of mask `which` from both sources (see above)
+template <typename T> __device__ inline MRaw<T> mraw(const MaskSrc<T>& s, int which, size_t i) {
   const size_t e = (size_t)which * s.mn + i;
   const T* vp = s.vals ? s.vals + e : reinterpret_cast<const T*>(g_mask_dummy);
   const uint8_t* kp = s.keep ? s.keep + e : g_mask_dummy;
-  T v = *vp;
-  uint32_t k = *kp;
-  asm volatile("" : "+v"(v), "+v"(k));
-  return s.vals ? v : (s.keep ? (k ? s.scale : T(0)) : T(1));
+  return MRaw<T>{*vp, (uint32_t)*kp};
+}
+// pin after a whole batch of mraw loads has been issued (the pin waits for its own load only)
+template <typename T> __device__ inline void mpin(MRaw<T>& r) { asm volatile("" : "+v"(r.v), "+v"(r.k)); }
+template <typename T> __device__ inline T mfin(const MaskSrc<T>& s, const MRaw<T>& r) {
+  return s.vals ? r.v : (s.keep ? (r.k ? s.scale : T(0)) : T(1));
+}
+template <typename T> __device__ inline T mval(const MaskSrc<T>& s, int which, size_t i) {
+  MRaw<T> r = mraw(s, which, i);
+  mpin(r);
+  return mfin(s, r);
 }
 // V consecutive mask values from an element index that is a multiple of V (V = 16 / sizeof T)
 template <typename T, int V> __device__ inline void mvals(const MaskSrc<T>& s, int which, size_t i, T (&m)[V]) {
@@ -181,6 +190,38 @@ template <> __device__ inline int kmap<double>(int u, int lg) { return ((u >> 1)
 template <typename T, int OP, int TR, int VEC>
 __device__ inline void load_chunk(T (&x)[4][2], const T* P, int ld, int r0, int R, int k0, int ke, int lr, int lg,
                                   const MaskSrc<T>& ms, const T* b1) {
+  if constexpr (!VEC) {
+    // scalar path: all 8 operand loads (+ masks and b1 for OP_H1) of the chunk go out first
+    T pv[2][4], bv[2][4];
+    MRaw<T> mr[2][4];
+    bool okv[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = r0 + 16 * i + lr;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int k = k0 + kmap<T>(u, lg);
+        const bool ok = r < R && k < ke;
+        const size_t idx = ok ? (TR ? (size_t)k * ld + r : (size_t)r * ld + k) : 0;
+        okv[i][u] = ok;
+        pv[i][u] = P[idx];
+        if constexpr (OP == OP_H1) {
+          mr[i][u] = mraw(ms, 0, idx);
+          bv[i][u] = b1[ok ? (TR ? r : k) : 0];
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if constexpr (OP == OP_H1) mpin(mr[i][u]);
+        const T mv = OP == OP_H1 ? mfin(ms, mr[i][u]) : T(1);
+        const T bb = OP == OP_H1 ? bv[i][u] : T(0);
+        x[u][i] = okv[i][u] ? op_apply<T, OP>(pv[i][u], mv, bb) : T(0);
+      }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int r = r0 + 16 * i + lr;
@@ -210,17 +251,6 @@ __device__ inline void load_chunk(T (&x)[4][2], const T* P, int ld, int r0, int 
         }
 #pragma unroll
         for (int q = 0; q < V; ++q) x[h * V + q][i] = ok ? op_apply<T, OP>(v[q], m[q], bb[q]) : T(0);
-      }
-    } else {
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int k = k0 + kmap<T>(u, lg);
-        const bool ok = rok && k < ke;
-        const size_t idx = ok ? (TR ? (size_t)k * ld + r : (size_t)r * ld + k) : 0;
-        const T pv = P[idx];
-        const T mv = OP == OP_H1 ? mval(ms, 0, idx) : T(1);
-        const T bv = OP == OP_H1 ? b1[ok ? (TR ? r : k) : 0] : T(0);
-        x[u][i] = ok ? op_apply<T, OP>(pv, mv, bv) : T(0);
       }
     }
   }
