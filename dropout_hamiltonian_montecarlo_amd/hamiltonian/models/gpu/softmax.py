@@ -136,16 +136,51 @@ class softmax:
         return prob
 
     def predict(self, par, X, prob=False, batchsize=None):                # softmax.py:82-89
+        """CPU semantics (cpu/softmax.py:82-89) by default; with ``batchsize`` the GPU file's
+        batching (gpu/softmax.py:90-102): whole batches only, and prob=True returns the
+        probabilities flattened to 1-D (its ``results.reshape(-1,)``)."""
+        if batchsize:
+            n = (X.shape[0] // batchsize) * batchsize
+            yhat = self.net(par, X[:n])
+            out = yhat if prob else yhat.argmax(dim=1)
+            return out.cpu().numpy().reshape(-1)
         yhat = self.net(par, X)
         out = yhat if prob else yhat.argmax(dim=1)
         return out.cpu().numpy()
 
-    def predict_stochastic(self, par, X, prob=False, p=0.5, Z=None):      # softmax.py:91-100
+    def predict_stochastic(self, par, X, prob=False, p=0.5, Z=None, batchsize=None):   # softmax.py:91-100
+        """Input dropout X ⊙ Z, Z ~ Bernoulli(p) (``Z`` may be given).  With ``batchsize`` the GPU
+        file's batching (gpu/softmax.py:105-121): whole batches, output reshaped to
+        (-1, last dimension) as there."""
         X = self._dev(X)
+        if batchsize:
+            n = (X.shape[0] // batchsize) * batchsize
+            X = X[:n]
+            Z = Z[:n] if Z is not None else None
         if Z is None:
             Z = torch.bernoulli(torch.full_like(X, p))
         else:
             Z = self._dev(Z)
         yhat = self.net(par, X * Z)
-        out = yhat if prob else yhat.argmax(dim=1)
-        return out.cpu().numpy()
+        out = (yhat if prob else yhat.argmax(dim=1)).cpu().numpy()
+        if batchsize:
+            out = out.reshape(-1, out.shape[-1]) if prob else out.reshape(-1, batchsize)
+        return out
+
+    def predict_posterior(self, posterior, X, prob=False):
+        """Posterior predictive over S samples (extension): mean over s of softmax(X·W_s + b_s), all
+        S parameter sets in ONE launch (the chain-interleaved layout W[D][S][K] of hmcx_softmax_predict).
+        ``posterior``: {'weights': [S, D, K], 'bias': [S, K]} as returned by ``sample``."""
+        Ws = np.asarray(posterior['weights'])
+        bs = np.asarray(posterior['bias'])
+        S, D, K = Ws.shape
+        Xd = self._dev(X)
+        B = Xd.shape[0]
+        W = self._dev(np.ascontiguousarray(Ws.transpose(1, 0, 2)).reshape(D, S * K))
+        b = self._dev(bs.reshape(S * K))
+        prob_all = torch.empty((B, S * K), dtype=self.dtype, device=self.device)
+        ctx = context(self.device)
+        ctx.check(ctx.lib.hmcx_softmax_predict(ctx.h, self.code, ptr(Xd), B, D, K, S, ptr(W), ptr(b),
+                                               ptr(prob_all)), "hmcx_softmax_predict")
+        mean = prob_all.cpu().numpy().reshape(B, S, K).mean(axis=1)
+        return mean if prob else mean.argmax(axis=1)

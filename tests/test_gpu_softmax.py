@@ -136,3 +136,24 @@ def test_bad_shapes_raise(model64):
         model64.grad({"weights": W[:5], "bias": b}, X_train=X, y_train=Y)
     with pytest.raises(HmcxError):
         model64.grad({"weights": np.zeros((16, 70)), "bias": np.zeros(70)}, X_train=X, y_train=np.zeros((8, 70)))
+
+
+def test_predict_gpu_batching_and_posterior(model64):
+    """predict / predict_stochastic with the GPU file's batching (gpu/softmax.py:90-121) and the
+    posterior predictive over S samples in one launch (mean of per-sample softmax, rel 1e-12)."""
+    X, Y, W, b = gi.softmax_inputs(6, 250, D=40, K=7)
+    par = {"weights": W, "bias": b}
+    m = om.softmax({"alpha": 0.01})
+    ref = m.predict(par, X, prob=True)
+    np.testing.assert_allclose(model64.predict(par, X, prob=True, batchsize=100), ref[:200].reshape(-1), rtol=1e-11)
+    np.testing.assert_array_equal(model64.predict(par, X, batchsize=100), ref[:200].argmax(axis=1))
+    Z = (np.random.RandomState(3).rand(*X.shape) < 0.5).astype(np.float64)
+    ps = model64.predict_stochastic(par, X, prob=True, Z=Z, batchsize=100)
+    np.testing.assert_allclose(ps, m.predict_stochastic(par, X[:200], prob=True, Z=Z[:200]), rtol=1e-11)
+    assert model64.predict_stochastic(par, X, Z=Z, batchsize=100).shape == (2, 100)
+    rs = np.random.RandomState(9)
+    post = {"weights": rs.normal(0, 0.3, (5, 40, 7)), "bias": rs.normal(0, 0.3, (5, 7))}
+    want = np.mean([m.predict({"weights": post["weights"][s], "bias": post["bias"][s]}, X, prob=True)
+                    for s in range(5)], axis=0)
+    np.testing.assert_allclose(model64.predict_posterior(post, X, prob=True), want, rtol=1e-12)
+    np.testing.assert_array_equal(model64.predict_posterior(post, X), want.argmax(axis=1))
