@@ -535,6 +535,7 @@ int hmcx_sghmc_run(hmcx_ctx* ctx, const hmcx_sampler_args* a) {
   HMCX_GUARD_CTX(ctx);
   int rc = check_sampler(ctx, a, true);
   if (rc) return rc;
+  if (a->pW || a->pb) return set_error(ctx, HMCX_EINVAL, "sghmc: pW/pb are SGLD-only fields");
   if (a->n_steps == 0) return HMCX_OK;
   return a->dtype == HMCX_F64 ? sghmc_run_t<double>(ctx, a) : sghmc_run_t<float>(ctx, a);
 }
@@ -543,6 +544,7 @@ int hmcx_sgld_run(hmcx_ctx* ctx, const hmcx_sampler_args* a) {
   HMCX_GUARD_CTX(ctx);
   int rc = check_sampler(ctx, a, false);
   if (rc) return rc;
+  if (!a->pW != !a->pb) return set_error(ctx, HMCX_EINVAL, "sgld: pW and pb must both be set or both NULL");
   if (a->n_steps == 0) return HMCX_OK;
   if (sgld_wide_eligible(a))
     return a->dtype == HMCX_F64 ? sgld_wide_t<double>(ctx, a) : sgld_wide_t<float>(ctx, a);

@@ -94,7 +94,8 @@ struct Tiling {
 Tiling make_tiling(int B, int D, int K, int C);
 
 enum FwdMode { FWD_GRAD = 0, FWD_SGHMC = 1, FWD_LL = 2, FWD_PRED = 3 };
-enum GradMode { GRAD_OUT = 0, GRAD_SGHMC = 1, GRAD_SGLD = 2, GRAD_SGD = 3 };
+// GRAD_SGLD_GPU: the CuPy file's SGLD update p = ν⊙p_prev − ½ε∇U, q += p (gpu/sgld.py:11-20, A2g)
+enum GradMode { GRAD_OUT = 0, GRAD_SGHMC = 1, GRAD_SGLD = 2, GRAD_SGD = 3, GRAD_SGLD_GPU = 4 };
 // Output link of the linear model: softmax over K classes (models/cpu/softmax.py) or the
 // sigmoid of K = 1 logistic regression (models/cpu/logistic.py:43-55).
 enum Link { LINK_SOFTMAX = 0, LINK_SIGMOID = 1 };

@@ -313,7 +313,7 @@ __global__ __launch_bounds__(NW * 64) void k_grad(GradArgs<T> a) {
         wreg[q] = a.Wsrc[idx];
       } else {
         wreg[q] = a.W[idx];
-        if (mode == GRAD_SGHMC || mode == GRAD_SGD) preg[q] = a.pW[idx];
+        if (mode == GRAD_SGHMC || mode == GRAD_SGD || mode == GRAD_SGLD_GPU) preg[q] = a.pW[idx];
         if (mode != GRAD_SGD) zreg[q] = (T)noise_at(a, c0 + cc, (uint32_t)(d * K + k));
       }
     }
@@ -382,6 +382,11 @@ __global__ __launch_bounds__(NW * 64) void k_grad(GradArgs<T> a) {
       const T m = a.gamma * preg[q] - a.lr * gr;                          // sgd.py:40
       a.pW[idx] = m;
       a.W[idx] = wreg[q] + m;                                             // sgd.py:41
+    } else if (mode == GRAD_SGLD_GPU) {
+      T p = (a.noise_scale * zreg[q]) * preg[q];                          // gpu/sgld.py:18 ν⊙p
+      p = p + a.m_half_eps * gr;
+      a.pW[idx] = p;
+      a.W[idx] = wreg[q] + p;                                             // gpu/sgld.py:19
     } else {
       T p = a.noise_scale * zreg[q];
       p = p + a.m_half_eps * gr;
@@ -457,7 +462,9 @@ __global__ __launch_bounds__(NW * 64) void k_grad(GradArgs<T> a) {
           const T gr = -(cs - a.alpha * bb);
           const T z = (T)noise_at(a, c, (uint32_t)(DK + k));
           T p = a.noise_scale * z;
+          if (mode == GRAD_SGLD_GPU) p = p * a.pb[col];                     // gpu/sgld.py:18
           p = p + a.m_half_eps * gr;
+          if (mode == GRAD_SGLD_GPU) a.pb[col] = p;
           a.b[col] = bb + p;
         }
       }
@@ -1222,11 +1229,11 @@ int sgld_run_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
     FwdArgs<T> f = fwd_args<T>(Xs, Ys, s->W, s->b, B, D, K, C, t, FWD_GRAD);
     f.diff = diff; f.colsum_part = csp;
     HMCX_HIP(ctx, launch_fwd_split<T>(f, t, st, S, slab));
-    GradArgs<T> g = grad_args<T>(Xs, diff, csp, B, D, K, C, t, GRAD_SGLD, s->alpha);
+    GradArgs<T> g = grad_args<T>(Xs, diff, csp, B, D, K, C, t, s->pW ? GRAD_SGLD_GPU : GRAD_SGLD, s->alpha);
     g.eps = (T)eps;
     g.noise_scale = (T)(2.0 * eps);                               // sgld.py:43
     g.m_half_eps = (T)(-0.5 * eps);                               // sgld.py:37
-    g.W = (T*)s->W; g.b = (T*)s->b;
+    g.W = (T*)s->W; g.b = (T*)s->b; g.pW = (T*)s->pW; g.pb = (T*)s->pb;
     g.noise_mode = s->noise_mode; g.noise = s->noise; g.noff = d_noff + (size_t)st_i * C;
     g.seed = s->seed; g.chain0 = s->chain0; g.step = s->step_base + (uint32_t)st_i; g.slot = 0;
     HMCX_HIP(ctx, launch_grad<T>(g, t, st));

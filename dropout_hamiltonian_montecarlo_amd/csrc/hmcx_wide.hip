@@ -32,6 +32,7 @@ constexpr int GTH = GNW * 64;
 
 template <typename T> struct WideArgs {
   const T* X; const T* Y; T* W; T* b;
+  T* pW; T* pb;                          // non-null: GPU-file momentum update (gpu/sgld.py:11-20)
   int B, D, K, KP, S, Dz, nSB;           // nSB: k_wsoft blocks
   T* slab; T* diff; T* csp; double* llp;
   T alpha, noise_scale, m_half_eps, clip_hi, clip_lo;
@@ -210,15 +211,18 @@ __global__ __launch_bounds__(GTH) void k_wgrad(WideArgs<T> a) {
   const bool dok = d0 + lr < a.D;
 
   // epilogue operands and noise first: their latency overlaps the GEMM
-  T wreg[EPT], zreg[EPT];
+  T wreg[EPT], zreg[EPT], preg[EPT];
+  const bool gpu_var = a.pW != nullptr;
+  const T* psrc = gpu_var ? a.pW : a.W;                      // pointer-selected: no load under a branch
 #pragma unroll
   for (int q = 0; q < EPT; ++q) {
     const int e = tid + q * GTH, i = e / KP, k = e - (e / KP) * KP;
     const bool ok = e < 16 * KP && d0 + i < a.D && k < K;
     const uint32_t el = ok ? (uint32_t)((d0 + i) * K + k) : 0u;
     wreg[q] = a.W[el];                                       // unconditional (clamped) load
+    preg[q] = psrc[el];
     zreg[q] = (T)wide_noise(a, el);
-    if (!ok) wreg[q] = zreg[q] = T(0);
+    if (!ok) wreg[q] = zreg[q] = preg[q] = T(0);
   }
 
   // rows [w·Bw, (w+1)·Bw) of the minibatch on wave w, 16 k-steps of operands in flight; loads are
@@ -270,7 +274,9 @@ __global__ __launch_bounds__(GTH) void k_wgrad(WideArgs<T> a) {
     for (int w = 1; w < GNW; ++w) dot += red[w][i][k];
     const T gr = -(dot - a.alpha * wreg[q]);                                  // softmax.py:57-58
     T p = a.noise_scale * zreg[q];                                            // sgld.py:43-46
+    if (gpu_var) p = p * preg[q];                                             // gpu/sgld.py:18
     p = p + a.m_half_eps * gr;                                                // sgld.py:37
+    if (gpu_var) a.pW[(size_t)(d0 + i) * K + k] = p;
     a.W[(size_t)(d0 + i) * K + k] = wreg[q] + p;                              // sgld.py:38
   }
 
@@ -294,7 +300,9 @@ __global__ __launch_bounds__(GTH) void k_wgrad(WideArgs<T> a) {
       const T bb = a.b[tid];
       const T gr = -(cs - a.alpha * bb);
       T p = a.noise_scale * (T)wide_noise(a, (uint32_t)(a.D * K + tid));
+      if (gpu_var) p = p * a.pb[tid];                                         // gpu/sgld.py:18
       p = p + a.m_half_eps * gr;
+      if (gpu_var) a.pb[tid] = p;
       a.b[tid] = bb + p;
     }
   }
@@ -357,7 +365,7 @@ int sgld_wide_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
   begin_call(ctx);
   int rc;
   WideArgs<T> a{};
-  a.W = (T*)s->W; a.b = (T*)s->b;
+  a.W = (T*)s->W; a.b = (T*)s->b; a.pW = (T*)s->pW; a.pb = (T*)s->pb;
   a.B = B; a.D = D; a.K = K; a.KP = KP; a.S = S; a.Dz = Dz; a.nSB = nSB;
   a.slab = slab; a.diff = diff; a.csp = csp; a.llp = llp;
   a.alpha = (T)s->alpha;

@@ -2,8 +2,11 @@
 
 Reference step: /root/reference/hamiltonian/inference/cpu/sgld.py:31-46:
     p = N(0, (2ε)²)  (draw_momentum, noise_scale = 2ε);  p += −½ε·∇U(q);  q += p.
-The CuPy file's variant p = ν⊙p_prev − ½ε∇U (gpu/sgld.py:11-20) is NOT the
-default; the NumPy semantics are the parity target.
+The CuPy file's variant (gpu/sgld.py:11-20) is the named mode ``variant='gpu'``:
+p = ν⊙p_prev − ½ε∇U(q) with ν ~ N(0, (2ε)²) and p carried from step to step (zeros at the start
+of ``sample``, gpu/sgmcmc.py:48), q += p.  The momentum lives on the device next to the state
+(hmcx_sampler_args.pW/pb); the kernels fuse the extra multiply and store.  Default
+``variant='cpu'``: the NumPy semantics, the parity target.
 
 One SGLD step = one k_fwd + one k_grad launch (hmcx_sgld_run); the log-likelihood the
 reference prints every 10 minibatches costs one extra forward launch on those steps only.
@@ -18,6 +21,24 @@ from .sgmcmc import RunResult, sgmcmc
 
 
 class sgld(sgmcmc):
+
+    def __init__(self, model, start_p, path_length=1.0, step_size=0.1, verbose=True,
+                 noise='numpy', seed=0, chain=0, chains=1, variant='cpu'):
+        if variant not in ('cpu', 'gpu'):
+            raise ValueError("variant must be 'cpu' (cpu/sgld.py) or 'gpu' (gpu/sgld.py)")
+        self.variant = variant
+        self._mom = None
+        super().__init__(model, start_p, path_length=path_length, step_size=step_size, verbose=verbose,
+                         noise=noise, seed=seed, chain=chain, chains=chains)
+
+    def sample(self, epochs=1, burnin=1, batch_size=1, rng=None, **args):
+        self._mom = None                       # p = zeros (gpu/sgmcmc.py:48)
+        return super().sample(epochs=epochs, burnin=burnin, batch_size=batch_size, rng=rng, **args)
+
+    def _momentum(self, state):
+        if self._mom is None or any(self._mom[v].shape != state[v].shape for v in state):
+            self._mom = {v: torch.zeros_like(state[v]) for v in state}
+        return self._mom
 
     def _check_vars(self):
         if self.model._hmcx_model != 'softmax' or list(self.start.keys()) != ['weights', 'bias']:
@@ -58,6 +79,9 @@ class sgld(sgmcmc):
         a.noise_off = noise_off.ctypes.data_as(nat.c_i64p)
         a.seed, a.chain0, a.step_base = self.seed, self.chain, self.global_step & 0xFFFFFFFF
         a.W, a.b = ptr(W), ptr(b)
+        if self.variant == 'gpu':
+            mom = self._momentum(state)
+            a.pW, a.pb = ptr(mom['weights']), ptr(mom['bias'])
         a.out_ll = ptr(out_ll)
         ctx = nat.context(dev)
         ctx.check(ctx.lib.hmcx_sgld_run(ctx.h, a), "hmcx_sgld_run")
@@ -70,12 +94,22 @@ class sgld(sgmcmc):
         return RunResult(np.ones(n_steps), np.ones(n_steps, dtype=bool), ll)
 
     def step(self, state, momentum, rng, **args):                         # sgld.py:31-39
+        """variant='cpu': returns (q, None) — the drawn momentum is not part of the result the
+        reference's loop uses.  variant='gpu' (gpu/sgld.py:11-20): ``momentum`` is p_prev (None =
+        zeros) and (q, p) is returned."""
         if self.chains != 1:
             raise HmcxError("step() is the reference's single-chain API; use sample() for chains > 1")
         X, y = args['X_train'], args['y_train']
         data = self._upload_data(X, y)
-        st = {var: torch.as_tensor(np.asarray(state[var]) if not isinstance(state[var], torch.Tensor)
-                                   else state[var]).to(self.model.device, self.model.dtype).contiguous().clone()
-              for var in self.start}
+        dev, dt = self.model.device, self.model.dtype
+
+        def dev_copy(v):
+            return torch.as_tensor(np.asarray(v) if not isinstance(v, torch.Tensor) else v) \
+                .to(dev, dt).contiguous().clone()
+
+        st = {var: dev_copy(state[var]) for var in self.start}
+        if self.variant == 'gpu':
+            self._mom = {var: (dev_copy(momentum[var]).reshape(st[var].shape) if momentum is not None
+                               else torch.zeros_like(st[var])) for var in self.start}
         self._run(st, data, [0], [self.step_size], rng, data[0].shape[0])
-        return st, None
+        return st, (self._mom if self.variant == 'gpu' else None)

@@ -162,13 +162,17 @@ typedef struct hmcx_sampler_args {
   int32_t* out_accepted;   /* device [n_steps*C]                                       */
   double* out_ll;          /* device [n_steps*C] log_likelihood(q_after, batch)        */
   double* out_E;           /* device [n_steps*C*2] (E_current, E_new) or NULL          */
+  void* pW;                /* SGLD only, or NULL: device [D][C*K] momentum carried     */
+  void* pb;                /*   across steps; selects the CuPy file's update (A2g)     */
 } hmcx_sampler_args;
 
 /* Replaces hamiltonian/inference/{cpu,gpu}/sghmc.py:19-39 (step, with the A1 completion:
  * momentum ~ N(0,1), MH accept min(1, exp(E_cur - E_new)) from cpu/hmc.py:67-87). */
 int hmcx_sghmc_run(hmcx_ctx* ctx, const hmcx_sampler_args* a);
 
-/* Replaces hamiltonian/inference/cpu/sgld.py:31-46 (step): p = N(0,(2ε)²) − ½ε∇U; q += p. */
+/* Replaces hamiltonian/inference/cpu/sgld.py:31-46 (step): p = N(0,(2ε)²) − ½ε∇U; q += p.
+ * With pW/pb set: hamiltonian/inference/gpu/sgld.py:11-20, p = ν⊙p_prev − ½ε∇U with
+ * ν ~ N(0,(2ε)²), q += p, p written back to pW/pb. */
 int hmcx_sgld_run(hmcx_ctx* ctx, const hmcx_sampler_args* a);
 
 /* ------------------------------------------------------------------ full-batch HMC, MVN model

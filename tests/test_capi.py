@@ -36,14 +36,40 @@ def test_argument_validation_without_device(nat):
     assert lib.hmcx_last_error(None) == b"null context"
 
 
-def test_struct_layout_matches_header(nat):
-    # 5 ints + n_steps, 2 doubles, then pointers: offsets follow the C layout on x86-64
-    a = nat.SamplerArgs
-    assert a.alpha.offset == 24 and a.X.offset == 40
-    assert ctypes.sizeof(a) == a.out_E.offset + 8
-    s = nat.SgdArgs                           # 6 ints, 3 doubles, 3 pointers, int, double, int, ...
-    assert s.alpha.offset == 24 and s.X.offset == 48 and s.dropout.offset == 72 and s.keep_p.offset == 80
-    assert s.seed.offset == 112 and s.W.offset == 128 and ctypes.sizeof(s) == 160
+_MIRRORS = [("SamplerArgs", "hmcx_sampler_args"), ("SgdArgs", "hmcx_sgd_args"), ("MvnArgs", "hmcx_hmc_mvn_args"),
+            ("MlpParams", "hmcx_mlp_params"), ("MlpSghmcArgs", "hmcx_mlp_sghmc_args")]
+
+
+def test_struct_layout_matches_header(nat, tmp_path):
+    """Every field offset and the size of each ctypes mirror equal what gcc computes from
+    include/hmcx.h (a layout drift would silently corrupt arguments)."""
+    import shutil
+    import subprocess
+    cc = shutil.which("gcc") or shutil.which("cc")
+    if cc is None:
+        pytest.skip("no C compiler")
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "hmcx.h"', "int main(void) {"]
+    for py, c in _MIRRORS:
+        st = getattr(nat, py)
+        lines.append('printf("%s sizeof %%zu\\n", sizeof(%s));' % (py, c))
+        for f in st._fields_:
+            lines.append('printf("%s %s %%zu\\n", offsetof(%s, %s));' % (py, f[0], c, f[0]))
+    lines += ["return 0;", "}"]
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run([cc, "-I", os.path.join(REPO, "include"), str(src), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
+    got = {}
+    for line in out:
+        if line:
+            py, name, val = line.split()
+            got[(py, name)] = int(val)
+    for py, _ in _MIRRORS:
+        st = getattr(nat, py)
+        assert ctypes.sizeof(st) == got[(py, "sizeof")], py
+        for f in st._fields_:
+            assert getattr(st, f[0]).offset == got[(py, f[0])], (py, f[0])
 
 
 def test_philox_host_generator(nat):

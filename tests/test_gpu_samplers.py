@@ -245,3 +245,61 @@ def test_sgld_wide_equals_kernel_path_philox(dtype, monkeypatch):
     for v in ("weights", "bias"):
         np.testing.assert_allclose(pw[v], ps[v], **tol)
     np.testing.assert_allclose(lw, ls, rtol=1e-9 if dtype == "f64" else 1e-4)
+
+
+def _run_variant_oracle(c):
+    X, Y = gi.dataset(c["data_seed"], c["N"], c["D"], c["K"])
+    s = osm.sgld_gpu_variant(om.softmax({"alpha": c["alpha"]}),
+                             {"weights": np.zeros((c["D"], c["K"])), "bias": np.zeros(c["K"])},
+                             path_length=1.0, step_size=c["step_size"], verbose=True)
+    s.out = io.StringIO()
+    post, logp = s.sample(epochs=c["epochs"], burnin=c["burnin"], batch_size=c["B"],
+                          rng=np.random.RandomState(c["rng_seed"]), X_train=X, y_train=Y)
+    return post, logp, s.out.getvalue()
+
+
+@pytest.mark.parametrize("wide", ["0", "1"])
+@pytest.mark.parametrize("K,D,B", [(10, 40, 100), (38, 300, 64), (3, 7, 5)])
+def test_sgld_gpu_variant_vs_oracle(K, D, B, wide, monkeypatch):
+    """variant='gpu' (gpu/sgld.py:11-20): p = ν⊙p_prev − ½ε∇U carried across steps,
+    on both SGLD paths (wide single-workgroup-row kernels and kernel-per-phase).  float64
+    trajectory within rel 1e-9 of the oracle's sgld_gpu_variant; the printed loss lines match.
+    Parity is against the oracle restatement only: the CuPy reference is not importable here."""
+    monkeypatch.setenv("HMCX_SGLD_WIDE", wide)
+    softmax, _, sgld = _gpu_classes()
+    c = dict(N=3 * B, B=B, D=D, K=K, alpha=0.01, step_size=0.05, burnin=1, epochs=3, data_seed=51, rng_seed=4)
+    post_r, logp_r, log_r = _run_variant_oracle(c)
+    X, Y = gi.dataset(c["data_seed"], c["N"], c["D"], c["K"])
+    s = sgld(softmax({"alpha": c["alpha"]}, dtype=torch.float64, device="cuda:0"),
+             {"weights": np.zeros((D, K)), "bias": np.zeros(K)}, step_size=c["step_size"], verbose=True,
+             variant="gpu")
+    s.out = io.StringIO()
+    post_g, logp_g = s.sample(epochs=c["epochs"], burnin=c["burnin"], batch_size=B,
+                              rng=np.random.RandomState(c["rng_seed"]), X_train=X, y_train=Y)
+    for v in ("weights", "bias"):
+        np.testing.assert_allclose(post_g[v], post_r[v], rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(logp_g, logp_r, rtol=1e-10)
+    assert [l for l in s.out.getvalue().splitlines() if "loss" in l] == \
+        [l for l in log_r.splitlines() if "loss" in l]
+    # the variant differs from the CPU update (the momentum carries)
+    post_c, _, _, _ = _run_oracle(dict(c, kind="sgld", path_length=1.0, np_seed=0))
+    assert not np.allclose(post_c["weights"], post_r["weights"], rtol=1e-6)
+
+
+def test_sgld_gpu_variant_step_api():
+    """step(state, momentum, rng) of variant='gpu' returns (q, p) and threads p through."""
+    softmax, _, sgld = _gpu_classes()
+    D, K, B = 20, 4, 30
+    X, Y = gi.dataset(3, B, D, K)
+    start = {"weights": np.zeros((D, K)), "bias": np.zeros(K)}
+    o = osm.sgld_gpu_variant(om.softmax({"alpha": 0.1}), start, step_size=0.1)
+    g = sgld(softmax({"alpha": 0.1}, dtype=torch.float64, device="cuda:0"), start, step_size=0.1, variant="gpu")
+    r1, r2 = np.random.RandomState(7), np.random.RandomState(7)
+    qo, po = start, {v: np.zeros_like(start[v]) for v in start}
+    qg, pg = start, None
+    for _ in range(3):
+        qo, po = o.step(qo, po, r1, X_train=X, y_train=Y)
+        qg, pg = g.step(qg, pg, r2, X_train=X, y_train=Y)
+    for v in start:
+        np.testing.assert_allclose(qg[v].cpu().numpy(), qo[v], rtol=1e-10, atol=1e-14)
+        np.testing.assert_allclose(pg[v].cpu().numpy(), po[v], rtol=1e-10, atol=1e-14)
