@@ -33,7 +33,8 @@ class SamplerArgs(ctypes.Structure):
                 ("noise_mode", c_int), ("noise", c_void_p), ("noise_off", c_i64p),
                 ("seed", ctypes.c_uint64), ("chain0", ctypes.c_uint32), ("step_base", ctypes.c_uint32),
                 ("W", c_void_p), ("b", c_void_p), ("out_A", c_void_p), ("out_accepted", c_void_p),
-                ("out_ll", c_void_p), ("out_E", c_void_p), ("pW", c_void_p), ("pb", c_void_p)]
+                ("out_ll", c_void_p), ("out_E", c_void_p), ("pW", c_void_p), ("pb", c_void_p),
+                ("out_trace", c_void_p)]
 
 
 class MvnArgs(ctypes.Structure):

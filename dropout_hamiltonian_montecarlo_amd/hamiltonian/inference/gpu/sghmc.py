@@ -127,10 +127,15 @@ class sghmc(sgmcmc):
         a.seed, a.chain0, a.step_base = self.seed, self.chain, self.global_step & 0xFFFFFFFF
         a.W, a.b = ptr(W), ptr(b)
         a.out_A, a.out_accepted, a.out_ll, a.out_E = ptr(out_A), ptr(out_acc), ptr(out_ll), ptr(out_E)
+        out_steps = None
+        if self.record_steps:
+            out_steps = torch.empty((n_steps, C, P), dtype=self.model.dtype, device=dev)
+            a.out_trace = ptr(out_steps)
         ctx = nat.context(dev)
         ctx.check(ctx.lib.hmcx_sghmc_run(ctx.h, a), "hmcx_sghmc_run")
         self.global_step += n_steps
-        return dict(out_f=out_f, out_acc=out_acc, noise_d=noise_d, n_steps=n_steps, C=C, t0=t0, ctx=ctx)
+        return dict(out_f=out_f, out_acc=out_acc, noise_d=noise_d, n_steps=n_steps, C=C, t0=t0, ctx=ctx,
+                    out_steps=out_steps)
 
     def _collect(self, h):
         """Read back one enqueued call (waits for it) and fill the trace entries of its steps."""
@@ -141,11 +146,12 @@ class sghmc(sgmcmc):
         ctx.check(ctx.lib.hmcx_synchronize(ctx.h), "hmcx_sghmc_run")        # deferred abort check
         nsc = n_steps * C
         A, ll, E = f[:nsc], f[nsc:2 * nsc], f[2 * nsc:]
+        steps = h['out_steps'].cpu().numpy() if h.get('out_steps') is not None else None
         if C == 1:
-            res = RunResult(A, acc, ll, E.reshape(n_steps, 2))
+            res = RunResult(A, acc, ll, E.reshape(n_steps, 2), steps=steps)
         else:
             res = RunResult(A.reshape(n_steps, C), acc.reshape(n_steps, C), ll.reshape(n_steps, C),
-                            E.reshape(n_steps, C, 2))
+                            E.reshape(n_steps, C, 2), steps=steps)
         if self.trace is not None:
             for s in range(n_steps):
                 t = self.trace[h['t0'] + s]

@@ -83,6 +83,10 @@ class sgld(sgmcmc):
             mom = self._momentum(state)
             a.pW, a.pb = ptr(mom['weights']), ptr(mom['bias'])
         a.out_ll = ptr(out_ll)
+        out_steps = None
+        if self.record_steps:
+            out_steps = torch.empty((n_steps, C, P), dtype=self.model.dtype, device=dev)
+            a.out_trace = ptr(out_steps)
         ctx = nat.context(dev)
         ctx.check(ctx.lib.hmcx_sgld_run(ctx.h, a), "hmcx_sgld_run")
         self.global_step += n_steps
@@ -91,7 +95,8 @@ class sgld(sgmcmc):
             ll = ll.reshape(n_steps, C)
         if self.trace is not None:
             self.trace.extend({'L': 1.0, 'A': 1.0, 'accepted': True, 'eps': float(e)} for e in eps)
-        return RunResult(np.ones(n_steps), np.ones(n_steps, dtype=bool), ll)
+        return RunResult(np.ones(n_steps), np.ones(n_steps, dtype=bool), ll,
+                         steps=out_steps.cpu().numpy() if out_steps is not None else None)
 
     def step(self, state, momentum, rng, **args):                         # sgld.py:31-39
         """variant='cpu': returns (q, None) — the drawn momentum is not part of the result the

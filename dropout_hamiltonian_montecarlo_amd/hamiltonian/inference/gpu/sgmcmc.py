@@ -37,8 +37,9 @@ from dropout_hamiltonian_montecarlo_amd._native import HmcxError, ptr
 class RunResult:
     """Per-step outputs of one libhmcx run call (host numpy arrays)."""
 
-    def __init__(self, A, accepted, ll, E=None, nlp=None):
+    def __init__(self, A, accepted, ll, E=None, nlp=None, steps=None):
         self.A, self.accepted, self.ll, self.E, self.nlp = A, accepted, ll, E, nlp
+        self.steps = steps      # [n_steps, C, P] state after every step (record_steps), else None
 
 
 class sgmcmc:
@@ -58,6 +59,7 @@ class sgmcmc:
         if self.chains < 1:
             raise ValueError("chains must be >= 1")
         self.global_step = 0
+        self.record_steps = False  # _run also returns the state after every step (RunResult.steps)
         self.trace = None          # optional list: per-step dict(L, A, accepted, eps)
         self.out = sys.stdout
         self.log_every = 10

@@ -164,6 +164,9 @@ typedef struct hmcx_sampler_args {
   double* out_E;           /* device [n_steps*C*2] (E_current, E_new) or NULL          */
   void* pW;                /* SGLD only, or NULL: device [D][C*K] momentum carried     */
   void* pb;                /*   across steps; selects the CuPy file's update (A2g)     */
+  void* out_trace;         /* device [n_steps][C][D*K+K] (dtype) or NULL: the state     */
+                           /* after every step (weights row-major, then bias) — the rows */
+                           /* of the HDF5 backend (sghmc_multicore.py:49-51)            */
 } hmcx_sampler_args;
 
 /* Replaces hamiltonian/inference/{cpu,gpu}/sghmc.py:19-39 (step, with the A1 completion:

@@ -306,3 +306,33 @@ class sgd:
             if verbose and (i % (epochs / 10) == 0):
                 print('loss: {0:.4f}'.format(loss_val[i]), file=self.out)
         return par, loss_val
+
+
+def backend_mean_arrays(start, backends, niter):
+    """cpu/hmc.py:132-138 (backend_mean) over in-memory stand-ins of the backend files: each
+    element of ``backends`` maps dataset name → float32 array (the file's contents)."""
+    aux = []
+    for f in backends:
+        aux.append({var: np.sum(f[var], axis=0) for var in f.keys()})
+    return {var: ((np.sum([r[var] for r in aux], axis=0).reshape(start[var].shape)) / niter) for var in start.keys()}
+
+
+def multicore_steps(sampler, X, y, niter_w, burnin_w, batch_size, rng):
+    """One worker of cpu/sghmc_multicore.py:19-53 / gpu/sgld_multicore.py:21-47 fed the minibatches
+    in order: burnin_w passes, then niter_w passes recording the state after every step (the rows
+    appended to the backend).  Returns {var: [T, *shape]} float64 and the per-pass logp of the last
+    minibatch (negative_log_posterior)."""
+    q = {var: np.array(sampler.start[var], dtype=np.float64) for var in sampler.start}
+    p = {var: np.zeros_like(q[var]) for var in q}
+    rows = {var: [] for var in q}
+    logp = np.zeros(niter_w)
+    for i in range(burnin_w + niter_w):
+        for X_b, y_b in sampler.iterate_minibatches(X, y, batch_size):
+            out = sampler.step(q, p, rng, X_train=X_b, y_train=y_b)
+            q, p = out[0], out[1]
+            if i >= burnin_w:
+                for var in q:
+                    rows[var].append(np.array(q[var]))
+        if i >= burnin_w:
+            logp[i - burnin_w] = sampler.model.negative_log_posterior(q, X_train=X_b, y_train=y_b)
+    return {var: np.array(rows[var]) for var in rows}, logp
