@@ -66,6 +66,9 @@ struct Q2Args {
   int zoff;                                 // noise off the A-RS pollers (HMCX_P2_ZOFF, default on)
   int spread;                               // rounds with spread gathers, bits A-RS, A-AG, B-RS, B-AG
                                             // (HMCX_P2_SPREAD=<mask>; default A-AG, where it measured faster)
+  int xmap;                                 // 1: logical id (b % 8)·(G/8) + b/8 — row teams on one XCD
+  int fl2;                                  // feature teams share an XCD: B-round stores plain (kept in L2)
+  int al2;                                  // row teams share an XCD (xmap): A-round stores plain
   int* abort_flag;                          // inside the arena
   double* out_A; int32_t* out_acc; double* out_ll; double* out_E;
   unsigned long long* prof;                 // HMCX_PERSIST_PROF=1: per-segment s_memtime totals (workgroup 0)
@@ -102,6 +105,13 @@ __device__ inline void put(__amdgpu_buffer_rsrc_t rs, int g, double v, unsigned 
   gran_t w = {(unsigned)x, ep, (unsigned)(x >> 32), ep};
   __builtin_amdgcn_raw_buffer_store_b128(w, rs, g * 16, 0, 16 /* sc1 */);
 }
+// XCD-local team regions (fl2): plain store, kept in the XCD's L2
+__device__ inline void put_t(bool l2, __amdgpu_buffer_rsrc_t rs, int g, double v, unsigned ep) {
+  const unsigned long long x = __builtin_bit_cast(unsigned long long, v);
+  gran_t w = {(unsigned)x, ep, (unsigned)(x >> 32), ep};
+  if (l2) __builtin_amdgcn_raw_buffer_store_b128(w, rs, g * 16, 0, 0);
+  else __builtin_amdgcn_raw_buffer_store_b128(w, rs, g * 16, 0, 16 /* sc1 */);
+}
 __device__ inline double decode(gran_t w) {
   return __builtin_bit_cast(double, (unsigned long long)w.x | ((unsigned long long)w.z << 32));
 }
@@ -110,7 +120,7 @@ __device__ inline double decode(gran_t w) {
 // words match.  Loads go out unpredicated in one batch of 8·NB (absent producers clamped to a
 // valid address and ignored); a pass re-reads the batch while any granule is missing.
 // SUM: *sum = v_0 + v_1 + … in producer order; else v_p → dst[p·dstride].  false on timeout/abort.
-template <int NB, bool SUM, typename V>
+template <int NB, bool SUM, typename V, int AUX = 16>
 __device__ inline bool poll_nb(__amdgpu_buffer_rsrc_t rs, int base0, int pstride, int np, int pskip, int off,
                                bool valid, unsigned ep, double* sum, int* abort_flag, V* dst, int dstride) {
   constexpr int N = 8 * NB;
@@ -129,7 +139,7 @@ __device__ inline bool poll_nb(__amdgpu_buffer_rsrc_t rs, int base0, int pstride
   for (int spins = 0; pend; ++spins) {
     gran_t v[N];
 #pragma unroll
-    for (int u = 0; u < N; ++u) v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, o[u], 0, 16 /* sc1 */);
+    for (int u = 0; u < N; ++u) v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, o[u], 0, AUX /* 16: sc1 */);
 #pragma unroll
     for (int u = 0; u < N; ++u)
       if (((pend >> u) & 1u) && v[u].y == ep && v[u].w == ep) {
@@ -160,12 +170,14 @@ __device__ inline bool poll_nb(__amdgpu_buffer_rsrc_t rs, int base0, int pstride
   }
   return true;
 }
-template <bool SUM, typename V = double>
+// AUX = 1 (sc0: coherent at the XCD's L2) is used only for teams whose members share an XCD; the
+// L2 is invalidated at launch, and every round's epoch is new within the launch.
+template <bool SUM, typename V = double, int AUX = 16>
 __device__ inline bool poll(__amdgpu_buffer_rsrc_t rs, int base0, int pstride, int np, int pskip, int off, bool valid,
                             unsigned ep, double* /*unused*/, int /*unused*/, double* sum, int* abort_flag,
                             V* dst = nullptr, int dstride = 0) {
-  return np <= 8 ? poll_nb<1, SUM, V>(rs, base0, pstride, np, pskip, off, valid, ep, sum, abort_flag, dst, dstride)
-                 : poll_nb<2, SUM, V>(rs, base0, pstride, np, pskip, off, valid, ep, sum, abort_flag, dst, dstride);
+  return np <= 8 ? poll_nb<1, SUM, V, AUX>(rs, base0, pstride, np, pskip, off, valid, ep, sum, abort_flag, dst, dstride)
+                 : poll_nb<2, SUM, V, AUX>(rs, base0, pstride, np, pskip, off, valid, ep, sum, abort_flag, dst, dstride);
 }
 
 // Spread gather: the (producer, item) pairs of a round are dealt over ALL threads of the workgroup
@@ -354,7 +366,10 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
   extern __shared__ __align__(16) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15;
   const int Gr = a.Gr, Gf = a.Gf, G = Gr * Gf;
-  const int bid = blockIdx.x;
+  // workgroups are dealt to the 8 XCDs round-robin by blockIdx: with the identity map feature team
+  // f (blocks f, f+Gf, …) shares an XCD when Gf % 8 == 0; xmap = 1 puts each row team on one XCD
+  const int pbid = blockIdx.x;
+  const int bid = a.xmap ? (pbid & 7) * (G >> 3) + (pbid >> 3) : pbid;
   const int r = bid / Gf, f = bid - (bid / Gf) * Gf;
   const int Br = a.Br, Bf = a.Bf, BfP = a.BfP, BFP = a.BFP, Ro = a.Ro, Fo = a.Fo;
   const int K = a.K, D = a.D, B = a.B;
@@ -447,7 +462,7 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int row = mt * 16 + M::row(lane, q);
-          if (row < nrow && lr < KC) put(rs, reg + row * KC + lr, (double)c[q], ep);
+          if (row < nrow && lr < KC) put_t(a.al2, rs, reg + row * KC + lr, (double)c[q], ep);
         }
       } else {
 #pragma unroll
@@ -460,7 +475,7 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
         const int i = e / KC, k = e - (e / KC) * KC;
         T v = Zp[i * 16 + k];
         for (int p = 1; p < WPA; ++p) v += Zp[(p * Br + i) * 16 + k];
-        put(rs, reg + e, (double)v, ep);
+        put_t(a.al2, rs, reg + e, (double)v, ep);
       }
     }
     return true;
@@ -660,7 +675,7 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
             const int m = t - HA;
             v = (double)Dme[(m / KC) * 16 + (m % KC)];
           }
-          put(rs, reg + t, v, ep);
+          put_t(a.al2, rs, reg + t, v, ep);
         }
         tstamp(s, it, 2);
         const int base0 = a.oXD + ((int)(uD & 1) * Gr + r) * Gf * NXA;
@@ -694,7 +709,7 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
       {
         ++ep;
         const int reg = a.oXB + (((int)(uB & 1) * Gf + f) * Gr + r) * NXB;
-        if (tid < HA) put(rs, reg + tid, hv, ep);
+        if (tid < HA) put_t(a.fl2, rs, reg + tid, hv, ep);
         const int nkp = (Br / 4) / WPB;
         for (int item = wave; item < MTB * WPB; item += QNW) {
           const int mt = item % MTB, part = item / MTB;
@@ -704,7 +719,7 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
               const int d = mt * 16 + M::row(lane, q);
-              if (d < nfeat && lr < KC) put(rs, reg + HA + d * KC + lr, (double)c[q], ep);
+              if (d < nfeat && lr < KC) put_t(a.fl2, rs, reg + HA + d * KC + lr, (double)c[q], ep);
             }
           } else {
 #pragma unroll
@@ -717,7 +732,7 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
             const int i = e / KC, k = e - (e / KC) * KC;
             T v = Zp[i * 16 + k];
             for (int q = 1; q < WPB; ++q) v += Zp[(q * BfP + i) * 16 + k];
-            put(rs, reg + HA + e, (double)v, ep);
+            put_t(a.fl2, rs, reg + HA + e, (double)v, ep);
           }
         }
         const int base0 = a.oXB + ((int)(uB & 1) * Gf + f) * Gr * NXB;
@@ -741,7 +756,9 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
           if (ish_) hdr[tid - ng] = sum;
           __syncthreads();
         } else {
-          const bool ok = poll<true>(rs, base0, NXB, Gr, -1, offB, isg || ish_, ep, nullptr, 0, &sum, a.abort_flag);
+          const bool ok = a.fl2 ? poll<true, double, 16>(rs, base0, NXB, Gr, -1, offB, isg || ish_, ep, nullptr, 0, &sum,
+                                                        a.abort_flag)
+                                : poll<true>(rs, base0, NXB, Gr, -1, offB, isg || ish_, ep, nullptr, 0, &sum, a.abort_flag);
           if (ish_) hdr[tid - ng] = sum;
           if (!all_ok(ok, ish)) return;
         }
@@ -769,7 +786,7 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
         ++ep;
         const int per = p2_pad(Fo * KC, a.pad);
         const int reg = a.oXW + (((int)(uW & 1) * Gf + f) * Gr + r) * per;
-        if (tid < nfo * KC) put(rs, reg + tid, own ? (double)wv : 0.0, ep);
+        if (tid < nfo * KC) put_t(a.fl2, rs, reg + tid, own ? (double)wv : 0.0, ep);
         tstamp(s, it, 6);
         if (own) Wf[wl] = wv;
         const int base0 = a.oXW + ((int)(uW & 1) * Gf + f) * Gr * per;
@@ -789,8 +806,10 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
         }
         const int dloc = tid / KC, kk = tid - (tid / KC) * KC;
         const int npd = tid < Fo * KC ? min(Gr, (nfeat - dloc + Fo - 1) / Fo) : 0;   // producers owning feature dloc
-        const bool ok = poll<false>(rs, base0, per, npd, r, tid, tid < Fo * KC, ep, nullptr, 0, nullptr, a.abort_flag,
-                                    Wf + dloc * 16 + kk, Fo * 16);
+        const bool ok = a.fl2 ? poll<false, T, 16>(rs, base0, per, npd, r, tid, tid < Fo * KC, ep, nullptr, 0, nullptr,
+                                                  a.abort_flag, Wf + dloc * 16 + kk, Fo * 16)
+                              : poll<false>(rs, base0, per, npd, r, tid, tid < Fo * KC, ep, nullptr, 0, nullptr,
+                                            a.abort_flag, Wf + dloc * 16 + kk, Fo * 16);
         if (!all_ok(ok, ish)) return;
         tstamp(s, it, 7);
       }
@@ -964,6 +983,11 @@ int sghmc_p2_t(hmcx_ctx* ctx, const hmcx_sampler_args* s, const PersistPlan2& pl
     static const int spread_env = getenv("HMCX_P2_SPREAD") ? atoi(getenv("HMCX_P2_SPREAD")) : 2;
     a.spread = fits ? spread_env : 0;
     a.zoff = !(getenv("HMCX_P2_ZOFF") && getenv("HMCX_P2_ZOFF")[0] == '0');
+    static const int xmap_env = getenv("HMCX_P2_XMAP") ? atoi(getenv("HMCX_P2_XMAP")) : 1;
+    a.xmap = (xmap_env == 1 && (pl.Gr * pl.Gf) % 8 == 0) ? 1 : 0;
+    static const int fl2_env = getenv("HMCX_P2_FL2") ? atoi(getenv("HMCX_P2_FL2")) : 1;
+    a.fl2 = (fl2_env == 1 && !a.xmap && pl.Gf % 8 == 0) ? 1 : 0;
+    a.al2 = (fl2_env == 1 && a.xmap && ((pl.Gr * pl.Gf) / 8) % pl.Gf == 0) ? 1 : 0;
   }
   a.abort_flag = reinterpret_cast<int*>(arena + (ngran - 1) * 16);
   a.out_A = s->out_A; a.out_acc = s->out_accepted; a.out_ll = s->out_ll; a.out_E = s->out_E;
