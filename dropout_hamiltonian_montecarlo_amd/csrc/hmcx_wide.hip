@@ -25,9 +25,15 @@ namespace hmcx {
 
 constexpr int WTH = 256;        // threads per workgroup (4 waves)
 constexpr int WRB = 32;         // forward row block
-constexpr int WDZ = 128;        // forward D slice (max)
+#ifndef HMCX_WDZ
+#define HMCX_WDZ 128
+#endif
+#ifndef HMCX_GNW
+#define HMCX_GNW 8
+#endif
+constexpr int WDZ = HMCX_WDZ;   // forward D slice (max)
 constexpr int WSR = 4;          // rows per k_wsoft workgroup (one per wave)
-constexpr int GNW = 8;          // k_wgrad waves: 8 so that its D/16 workgroups cover every SIMD
+constexpr int GNW = HMCX_GNW;   // k_wgrad waves: 8 so that its D/16 workgroups cover every SIMD
 constexpr int GTH = GNW * 64;
 
 template <typename T> struct WideArgs {
@@ -49,7 +55,8 @@ __global__ __launch_bounds__(WTH) void k_wfwd(WideArgs<T> a) {
   constexpr int XP = WDZ + (sizeof(T) == 8 ? 2 : 1);       // conflict-free row pitches
   constexpr int WP = KP + (sizeof(T) == 8 ? 2 : 1);
   __shared__ __align__(16) T Xs[WRB * XP];
-  __shared__ __align__(16) T Ws[WDZ * WP];
+  constexpr int WSN = WDZ * WP > 4 * WRB * KP ? WDZ * WP : 4 * WRB * KP;   // also the reduction area
+  __shared__ __align__(16) T Ws[WSN];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lg = lane >> 4;
   const int m0 = blockIdx.x * WRB, z = blockIdx.y;
   const int dlo = min(a.D, z * a.Dz), dhi = min(a.D, dlo + a.Dz), nd = dhi - dlo;
@@ -111,7 +118,7 @@ __global__ __launch_bounds__(WTH) void k_wfwd(WideArgs<T> a) {
     }
   }
   __syncthreads();                                           // staging buffers become the reduction area
-  T* red = Ws;                                               // [4][32][KP] ⊂ Ws (WDZ·WP ≥ 4·32·KP)
+  T* red = Ws;                                               // [4][32][KP] ⊂ Ws
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
