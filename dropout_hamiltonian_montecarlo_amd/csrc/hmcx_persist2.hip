@@ -69,6 +69,7 @@ struct Q2Args {
   int xmap;                                 // 1: logical id (b % 8)·(G/8) + b/8 — row teams on one XCD
   int fl2;                                  // feature teams share an XCD: B-round stores plain (kept in L2)
   int al2;                                  // row teams share an XCD (xmap): A-round stores plain
+  int prefetch;                             // 1: next step's tile/labels loaded during the accept round
   int* abort_flag;                          // inside the arena
   double* out_A; int32_t* out_acc; double* out_ll; double* out_E;
   unsigned long long* prof;                 // HMCX_PERSIST_PROF=1: per-segment s_memtime totals (workgroup 0)
@@ -332,6 +333,25 @@ __device__ inline void load_tile(T* Xs, const T* Xg, int Br, int BfP, int BFP, i
   }
 }
 
+// One step's minibatch rows: the X tile of this workgroup and the labels of its softmax rows
+// (label loads issued first so they travel with the tile's).
+template <typename T>
+__device__ inline void load_step_rows(T* Xs, T* Yo, const T* Xg, const T* Yg, int Br, int BfP, int BFP, int nrow,
+                                      int nfeat, int row0, int feat0, int D, int K, int Ro, int nro, int ro0) {
+  const int tid = threadIdx.x;
+  T y = T(0);
+  if (tid < Ro * 16) {                       // Ro·16 ≤ QTH (plan_p2: Ro·KC + KC + 1 ≤ QTH, KC ≥ 10)
+    const int ii = tid >> 4, k = tid & 15;
+    if (ii < nro && k < K) y = Yg[(size_t)(row0 + ro0 + ii) * K + k];
+  }
+  for (int e = tid + QTH; e < Ro * 16; e += QTH) {
+    const int ii = e >> 4, k = e & 15;
+    Yo[e] = (ii < nro && k < K) ? Yg[(size_t)(row0 + ro0 + ii) * K + k] : T(0);
+  }
+  load_tile<T>(Xs, Xg, Br, BfP, BFP, nrow, nfeat, row0, feat0, D);
+  if (tid < Ro * 16) Yo[tid] = y;
+}
+
 // C[16 x 16] += A[16 x 4·nk] · B[4·nk x 16] on one wave (v_mfma_*_16x16x4): A(i, kk) = a[i·as_i +
 // kk·as_k], B(kk, j) = b[kk·bs_k + j]; operands of 8 k-steps are loaded before their MFMAs, two
 // accumulators alternate.  Returns the D fragment (rows M::row(lane, q), column lane & 15).
@@ -511,12 +531,9 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
     const T* Yg = reinterpret_cast<const T*>(a.Y) + (size_t)a.row0[s] * K;
     prof.stamp(0);
 
-    // ---- step start: tile, labels of my rows, momentum (hmc.py:82-87), step-start copies
-    load_tile<T>(Xs, Xg, Br, BfP, BFP, nrow, nfeat, row0, feat0, D);
-    for (int e = tid; e < Ro * 16; e += QTH) {
-      const int ii = e >> 4, k = e & 15;
-      Yo[e] = (ii < nro && k < K) ? Yg[(size_t)(row0 + ro0 + ii) * K + k] : T(0);
-    }
+    // ---- step start: tile, labels of my rows (step 0 only: later steps' were loaded while the
+    //      previous accept round travelled), momentum (hmc.py:82-87), step-start copies
+    if (s == 0 || !a.prefetch) load_step_rows<T>(Xs, Yo, Xg, Yg, Br, BfP, BFP, nrow, nfeat, row0, feat0, D, K, Ro, nro, ro0);
     for (int e = tid; e < BfP * 16; e += QTH) Wf0[e] = Wf[e];
     {
       float z4[4];
@@ -827,6 +844,13 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
       if (tid == 1) put(rs, reg + 1, kin1w, ep);
       if (tid == 2) put(rs, reg + 2, ll0, ep);
     }
+    // next step's tile and labels while the partials travel: Xs and Yo have no reader left in this
+    // step (the last B-gemm and softmax ended before a barrier)
+    if (a.prefetch && s + 1 < a.n_steps) {
+      const T* Xn = reinterpret_cast<const T*>(a.X) + (size_t)a.row0[s + 1] * D;
+      const T* Yn = reinterpret_cast<const T*>(a.Y) + (size_t)a.row0[s + 1] * K;
+      load_step_rows<T>(Xs, Yo, Xn, Yn, Br, BfP, BFP, nrow, nfeat, row0, feat0, D, K, Ro, nro, ro0);
+    }
     const int sbase = a.oXS + (int)(uS & 1) * G * NXS;
     ++uS;
     double v3[3] = {0.0, 0.0, 0.0};
@@ -988,6 +1012,8 @@ int sghmc_p2_t(hmcx_ctx* ctx, const hmcx_sampler_args* s, const PersistPlan2& pl
     static const int fl2_env = getenv("HMCX_P2_FL2") ? atoi(getenv("HMCX_P2_FL2")) : 1;
     a.fl2 = (fl2_env == 1 && !a.xmap && pl.Gf % 8 == 0) ? 1 : 0;
     a.al2 = (fl2_env == 1 && a.xmap && ((pl.Gr * pl.Gf) / 8) % pl.Gf == 0) ? 1 : 0;
+    static const int pf_env = getenv("HMCX_P2_PREFETCH") ? atoi(getenv("HMCX_P2_PREFETCH")) : 1;
+    a.prefetch = pf_env == 1 ? 1 : 0;
   }
   a.abort_flag = reinterpret_cast<int*>(arena + (ngran - 1) * 16);
   a.out_A = s->out_A; a.out_acc = s->out_accepted; a.out_ll = s->out_ll; a.out_E = s->out_E;
