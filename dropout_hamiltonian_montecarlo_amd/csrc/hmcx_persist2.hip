@@ -70,6 +70,7 @@ struct Q2Args {
   int fl2;                                  // feature teams share an XCD: B-round stores plain (kept in L2)
   int al2;                                  // row teams share an XCD (xmap): A-round stores plain
   int prefetch;                             // 1: next step's tile/labels loaded during the accept round
+  int acc1;                                 // 1: accept partials polled in one batch (HMCX_P2_ACC1)
   int* abort_flag;                          // inside the arena
   double* out_A; int32_t* out_acc; double* out_ll; double* out_E;
   unsigned long long* prof;                 // HMCX_PERSIST_PROF=1: per-segment s_memtime totals (workgroup 0)
@@ -854,11 +855,19 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
     const int sbase = a.oXS + (int)(uS & 1) * G * NXS;
     ++uS;
     double v3[3] = {0.0, 0.0, 0.0};
-    bool ok = true;
+    if (a.acc1) {
+      // the three partials of workgroup tid in one batch of loads (one round trip, not three)
+      const bool ok = poll_nb<1, false, double>(rs, sbase + tid * NXS, 1, 3, -1, 0, tid < G, ep, nullptr,
+                                                a.abort_flag, stg + 3 * tid, 1);
+      if (!all_ok(ok, ish)) return;
+      if (tid < G) { v3[0] = stg[3 * tid]; v3[1] = stg[3 * tid + 1]; v3[2] = stg[3 * tid + 2]; }
+    } else {
+      bool ok = true;
 #pragma unroll
-    for (int j = 0; j < 3; ++j)
-      ok = ok && poll<true>(rs, sbase + j, NXS, 1, -1, tid * NXS, tid < G, ep, nullptr, 0, &v3[j], a.abort_flag);
-    if (!all_ok(ok, ish)) return;
+      for (int j = 0; j < 3; ++j)
+        ok = ok && poll<true>(rs, sbase + j, NXS, 1, -1, tid * NXS, tid < G, ep, nullptr, 0, &v3[j], a.abort_flag);
+      if (!all_ok(ok, ish)) return;
+    }
     const double S0 = wsum(v3[0], dsh), S1 = wsum(v3[1], dsh), L0 = wsum(v3[2], dsh);
     const double K0 = (0.0 + 0.5 * S0) + 0.5 * kb0;
     const double Ecur = a.neg_inv_n * (L0 + a.log_prior) + K0;
@@ -1014,6 +1023,8 @@ int sghmc_p2_t(hmcx_ctx* ctx, const hmcx_sampler_args* s, const PersistPlan2& pl
     a.al2 = (fl2_env == 1 && a.xmap && ((pl.Gr * pl.Gf) / 8) % pl.Gf == 0) ? 1 : 0;
     static const int pf_env = getenv("HMCX_P2_PREFETCH") ? atoi(getenv("HMCX_P2_PREFETCH")) : 1;
     a.prefetch = pf_env == 1 ? 1 : 0;
+    static const int acc1_env = getenv("HMCX_P2_ACC1") ? atoi(getenv("HMCX_P2_ACC1")) : 1;
+    a.acc1 = acc1_env == 1 ? 1 : 0;
   }
   a.abort_flag = reinterpret_cast<int*>(arena + (ngran - 1) * 16);
   a.out_A = s->out_A; a.out_acc = s->out_accepted; a.out_ll = s->out_ll; a.out_E = s->out_E;
