@@ -553,7 +553,8 @@ __global__ void k_trace_snapshot(const T* __restrict__ W, const T* __restrict__ 
 }
 
 // A traced run is a sequence of one-step runs, each followed by a snapshot launch on the same
-// stream: every kernel path (persistent, chain-batched, wide, kernel-per-phase) traces the same way.
+// stream (chain-batched, wide and kernel-per-phase paths); the single-chain persistent SGHMC kernel
+// stores the rows itself at the end of every step and keeps one launch per call.
 template <typename F>
 static int run_traced(hmcx_ctx* ctx, const hmcx_sampler_args* a, F run_one) {
   if (!a->out_trace) return run_one(a);
@@ -596,6 +597,8 @@ int hmcx_sghmc_run(hmcx_ctx* ctx, const hmcx_sampler_args* a) {
   if (rc) return rc;
   if (a->pW || a->pb) return set_error(ctx, HMCX_EINVAL, "sghmc: pW/pb are SGLD-only fields");
   if (a->n_steps == 0) return HMCX_OK;
+  if (a->out_trace && sghmc_p2_selected(ctx, a))   // the persistent kernel stores the trace rows itself
+    return a->dtype == HMCX_F64 ? sghmc_run_t<double>(ctx, a) : sghmc_run_t<float>(ctx, a);
   return run_traced(ctx, a, [ctx](const hmcx_sampler_args* s) {
     return s->dtype == HMCX_F64 ? sghmc_run_t<double>(ctx, s) : sghmc_run_t<float>(ctx, s);
   });

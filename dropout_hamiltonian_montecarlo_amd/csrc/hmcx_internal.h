@@ -185,6 +185,7 @@ template <typename T> int softmax_predict_t(hmcx_ctx*, const void*, int, int, in
 template <typename T> int sgd_run_t(hmcx_ctx*, const hmcx_sgd_args*);
 template <typename T> int sumsq_t(hmcx_ctx*, const void*, int64_t, double*);
 template <typename T> int sghmc_run_t(hmcx_ctx*, const hmcx_sampler_args*);
+bool sghmc_p2_selected(hmcx_ctx*, const hmcx_sampler_args*);   // hmcx_softmax.hip
 template <typename T> int sgld_run_t(hmcx_ctx*, const hmcx_sampler_args*);
 bool sgld_wide_eligible(const hmcx_sampler_args*);       // hmcx_wide.hip: one chain, K ≤ 64
 template <typename T> int sgld_wide_t(hmcx_ctx*, const hmcx_sampler_args*);

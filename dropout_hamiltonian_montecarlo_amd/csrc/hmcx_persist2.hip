@@ -73,6 +73,7 @@ struct Q2Args {
   int acc1;                                 // 1: accept partials polled in one batch (HMCX_P2_ACC1)
   int* abort_flag;                          // inside the arena
   double* out_A; int32_t* out_acc; double* out_ll; double* out_E;
+  void* out_trace;                          // [n_steps][P] state after every step, or null
   unsigned long long* prof;                 // HMCX_PERSIST_PROF=1: per-segment s_memtime totals (workgroup 0)
   unsigned long long* trace;                // HMCX_P2_TRACE=1: [G][P2TR_IT][8] s_memrealtime stamps (step 0)
 };
@@ -889,6 +890,11 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
       wv = w0;
       if (tid < 16) bsh[tid] = b0sh[tid];
     }
+    if (a.out_trace) {                                                     // sghmc_multicore.py:49-51 row
+      T* tr = reinterpret_cast<T*>(a.out_trace) + (size_t)s * a.P;
+      if (own) tr[e_own] = wv;
+      if (bid == 0 && tid < K) tr[D * K + tid] = bsh[tid];
+    }
     if (bid == 0 && tid == 0) {
       a.out_A[s] = A;
       a.out_acc[s] = acc;
@@ -1028,6 +1034,7 @@ int sghmc_p2_t(hmcx_ctx* ctx, const hmcx_sampler_args* s, const PersistPlan2& pl
   }
   a.abort_flag = reinterpret_cast<int*>(arena + (ngran - 1) * 16);
   a.out_A = s->out_A; a.out_acc = s->out_accepted; a.out_ll = s->out_ll; a.out_E = s->out_E;
+  a.out_trace = s->out_trace;
   static const bool prof_on = getenv("HMCX_PERSIST_PROF") && getenv("HMCX_PERSIST_PROF")[0] == '1';
   unsigned long long* dprof = nullptr;
   if (prof_on) {

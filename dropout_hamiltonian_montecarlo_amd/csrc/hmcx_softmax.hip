@@ -1066,12 +1066,23 @@ int sghmc_batch_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
   return timing_end(ctx, ctx->stream);
 }
 
+static bool persist_v1() {
+  static const bool v1 = getenv("HMCX_PERSIST_V1") && getenv("HMCX_PERSIST_V1")[0] == '1';
+  return v1;
+}
+
+// True when sghmc_run_t serves this call with k_sghmc_p2, which writes out_trace itself.
+bool sghmc_p2_selected(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
+  if (s->C != 1 || ctx->sghmc_path == 1 || persist_v1()) return false;
+  const size_t ts = s->dtype == HMCX_F64 ? sizeof(double) : sizeof(float);
+  return plan_p2(s->B, s->D, s->K, ts, ctx->num_cus, ctx->lds_max).ok;
+}
+
 template <typename T>
 int sghmc_run_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
   const int B = s->B, D = s->D, K = s->K, C = s->C, N = C * K;
   if (C == 1 && ctx->sghmc_path != 1) {   // single chain: persistent kernel
-    static const bool v1 = getenv("HMCX_PERSIST_V1") && getenv("HMCX_PERSIST_V1")[0] == '1';
-    if (!v1) {                            // hmcx_persist2.hip (tagged-granule teams)
+    if (!persist_v1()) {                  // hmcx_persist2.hip (tagged-granule teams)
       const PersistPlan2 p2 = plan_p2(B, D, K, sizeof(T), ctx->num_cus, ctx->lds_max);
       if (p2.ok) return sghmc_p2_t<T>(ctx, s, p2);
     }

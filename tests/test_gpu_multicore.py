@@ -104,3 +104,57 @@ def test_multicore_traced_equals_untraced(kind, tmp_path):
     for c, f in enumerate(files):
         w = h5trace.read_dataset(f, "weights")
         np.testing.assert_array_equal(w[1:].reshape(T, -1), post["weights"][c * T:(c + 1) * T].astype(np.float32))
+
+
+@pytest.mark.parametrize("dtype", ["float64", "float32"])
+@pytest.mark.parametrize("noise", ["philox", "numpy"])
+def test_persistent_trace_rows_equal_one_step_calls(dtype, noise):
+    """One chain on the persistent kernel (path 2), whose launch stores the trace rows itself: a
+    traced 8-step call records after every step exactly (bit for bit) the state that eight one-step
+    untraced calls reach, with the same path lengths, acceptance probabilities, flags and
+    log-likelihoods; the last row is the final state."""
+    from dropout_hamiltonian_montecarlo_amd.hamiltonian.models.gpu.softmax import softmax
+    from dropout_hamiltonian_montecarlo_amd.hamiltonian.inference.gpu.sghmc import sghmc
+    N, B, D, K = 400, 50, 40, 6
+    X, Y = gi.dataset(63, N, D, K)
+    start = {"weights": np.zeros((D, K)), "bias": np.zeros(K)}
+    dt = getattr(torch, dtype)
+    rows = list(range(0, N - B + 1, B))
+
+    def make():
+        kw = dict(noise="philox", seed=5) if noise == "philox" else {}
+        s = sghmc(softmax({"alpha": 0.1}, dtype=dt, device="cuda:0"), start, path_length=0.05,
+                  step_size=0.01, **kw)
+        s.out = io.StringIO()
+        s.trace = []
+        s.model.ctx.set_sghmc_path(2)
+        return s
+
+    np.random.seed(7)
+    g = make()
+    g.record_steps = True
+    data = g._upload_data(X, Y)
+    st = g._init_state()
+    res = g._run(st, data, rows, [g.step_size] * len(rows), np.random.RandomState(1), B)
+    fin = g._state_to_host(st)
+    assert res.steps.shape == (len(rows), 1, D * K + K)
+
+    np.random.seed(7)
+    h = make()
+    data_h = h._upload_data(X, Y)
+    st_h = h._init_state()
+    rng = np.random.RandomState(1)
+    A, acc, ll = [], [], []
+    for i, r in enumerate(rows):
+        ri = h._run(st_h, data_h, [r], [h.step_size], rng, B)
+        A.append(ri.A[0]); acc.append(ri.accepted[0]); ll.append(ri.ll[0])
+        sh = h._state_to_host(st_h)
+        row = res.steps[i, 0].astype(np.float64)
+        np.testing.assert_array_equal(row[:D * K], sh["weights"].reshape(-1))
+        np.testing.assert_array_equal(row[D * K:], sh["bias"])
+    np.testing.assert_array_equal(res.A, np.array(A))
+    np.testing.assert_array_equal(res.accepted, np.array(acc))
+    np.testing.assert_array_equal(res.ll, np.array(ll))
+    assert [t["L"] for t in g.trace] == [t["L"] for t in h.trace]
+    np.testing.assert_array_equal(res.steps[-1, 0, :D * K].astype(np.float64), fin["weights"].reshape(-1))
+    assert 0 < np.sum(res.accepted) and len(np.unique(res.steps[:, 0, 0])) > 1   # the chain moves
