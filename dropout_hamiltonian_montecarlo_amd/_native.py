@@ -71,6 +71,16 @@ class SgdArgs(ctypes.Structure):
                 ("W", c_void_p), ("b", c_void_p), ("mW", c_void_p), ("mb", c_void_p)]
 
 
+class HmcArgs(ctypes.Structure):
+    _fields_ = [("dtype", c_int), ("model", c_int), ("B", c_int), ("D", c_int), ("K", c_int), ("n_steps", c_int),
+                ("alpha", c_double), ("log_prior", c_double), ("lp_const", c_double * 2),
+                ("X", c_void_p), ("Y", c_void_p), ("eps", c_dblp), ("n_iter", c_i32p), ("u_accept", c_dblp),
+                ("noise_mode", c_int), ("noise", c_void_p), ("noise_off", c_i64p),
+                ("seed", ctypes.c_uint64), ("chain", ctypes.c_uint32), ("step_base", ctypes.c_uint32),
+                ("W", c_void_p), ("b", c_void_p), ("out_A", c_void_p), ("out_accepted", c_void_p),
+                ("out_nlp", c_void_p), ("out_E", c_void_p), ("out_trace", c_void_p), ("out_mom", c_void_p)]
+
+
 MODEL_SOFTMAX, MODEL_LOGISTIC = 0, 1
 MLP_MASK_SLOT0 = 0x80000000
 
@@ -78,11 +88,11 @@ MLP_MASK_SLOT0 = 0x80000000
 # Every symbol include/hmcx.h declares (checked by tests/test_capi.py).
 EXPORTS = ("hmcx_version", "hmcx_create", "hmcx_destroy", "hmcx_last_error", "hmcx_set_stream",
            "hmcx_synchronize", "hmcx_set_graph_mode", "hmcx_set_sghmc_path", "hmcx_set_timing", "hmcx_get_timing",
-           "hmcx_philox_uniforms", "hmcx_philox_normals",
+           "hmcx_philox_uniforms", "hmcx_philox_normals", "hmcx_philox_normals_f64",
            "hmcx_softmax_grad", "hmcx_softmax_loglik", "hmcx_softmax_predict", "hmcx_sghmc_run",
            "hmcx_sgld_run", "hmcx_hmc_mvn_run", "hmcx_mlp_masks", "hmcx_mlp_grad", "hmcx_mlp_loss",
            "hmcx_mlp_sghmc_run", "hmcx_logistic_grad", "hmcx_logistic_loglik", "hmcx_logistic_predict",
-           "hmcx_sumsq", "hmcx_sgd_run")
+           "hmcx_sumsq", "hmcx_sgd_run", "hmcx_hmc_run", "hmcx_axpy", "hmcx_mvn_eval")
 
 _lib = None
 _lock = threading.Lock()
@@ -119,6 +129,8 @@ def load_library():
         lib.hmcx_philox_normals.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                             ctypes.c_uint32, ctypes.c_uint32, c_dblp]
         lib.hmcx_philox_normals.restype = None
+        lib.hmcx_philox_normals_f64.argtypes = lib.hmcx_philox_normals.argtypes
+        lib.hmcx_philox_normals_f64.restype = None
         lib.hmcx_softmax_grad.argtypes = [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                                           c_void_p, c_void_p, c_double, c_void_p, c_void_p]
         lib.hmcx_softmax_loglik.argtypes = [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
@@ -144,6 +156,10 @@ def load_library():
                                               c_void_p]
         lib.hmcx_sumsq.argtypes = [c_void_p, c_int, c_void_p, ctypes.c_int64, c_void_p]
         lib.hmcx_sgd_run.argtypes = [c_void_p, ctypes.POINTER(SgdArgs)]
+        lib.hmcx_hmc_run.argtypes = [c_void_p, ctypes.POINTER(HmcArgs)]
+        lib.hmcx_axpy.argtypes = [c_void_p, c_int, c_int, ctypes.c_int64, c_double, c_void_p, c_void_p]
+        lib.hmcx_mvn_eval.argtypes = [c_void_p, c_int, c_int, c_void_p, c_void_p, c_double, c_void_p, c_void_p,
+                                      c_void_p]
         _lib = lib
         return lib
 
@@ -248,11 +264,14 @@ def philox_uniforms(seed, chain, step, slot, n):
     return out
 
 
-def philox_normals(seed, chain, step, slot, e0, n):
+def philox_normals(seed, chain, step, slot, e0, n, dtype="f32"):
+    """Host twin of the device noise stream: dtype 'f32' (float Box–Muller, f32 chains) or 'f64'
+    (53-bit uniforms, double Box–Muller, f64 chains)."""
     import numpy as np
     lib = load_library()
     out = np.empty(n, dtype=np.float64)
-    lib.hmcx_philox_normals(seed, chain, step, slot, e0, n, out.ctypes.data_as(c_dblp))
+    fn = lib.hmcx_philox_normals_f64 if dtype == "f64" else lib.hmcx_philox_normals
+    fn(seed, chain, step, slot, e0, n, out.ctypes.data_as(c_dblp))
     return out
 
 

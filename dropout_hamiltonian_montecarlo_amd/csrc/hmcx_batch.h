@@ -310,9 +310,45 @@ __global__ __launch_bounds__(256) void k_bfwd(BFwdArgs<T> a) {
 }
 
 template <typename T>
-__device__ inline T bnoise(const BGradArgs<T>& a, int ch, uint32_t e, const float* z4) {
+__device__ inline T bnoise(const BGradArgs<T>& a, int ch, uint32_t e) {
   if (a.noise_mode == HMCX_NOISE_BUFFER) return (T)a.noise[a.noff[ch] + (int64_t)a.slot * a.P + e];
-  return (T)z4[e & 3];
+  return philox_normal_t<T>(a.seed, a.chain0 + ch, a.step, a.slot, e);
+}
+
+// Friction noise of a feature tile into LDS: Nz[fl][cs·K + k] for the local features fl < nfl (tile
+// feature fi = fmap(fl)), chain slots cs.  f64 chains: one Philox block per element pair (k, k+1)
+// of one feature (K = 10 is even), double Box–Muller; f32 chains: blocks of four elements of the
+// flat index e = d·K + k (they may straddle two features), float Box–Muller (hmcx_common.h).
+template <typename T, typename FMap>
+__device__ inline void gen_tile_noise(const BGradArgs<T>& a, const int* chs, int d0, int nfeat, T* Nz, int nfl,
+                                      FMap fmap) {
+  const int tid = threadIdx.x;
+  if constexpr (sizeof(T) == 8) {
+    constexpr int NP = BKC / 2;
+    for (int t = tid; t < BCT * nfl * NP; t += 256) {
+      const int cs = t / (nfl * NP), r = t - cs * (nfl * NP), fl = r / NP, kk = r - fl * NP;
+      const int ch = chs[cs], fi = fmap(fl);
+      if (ch < 0 || fi >= nfeat) continue;
+      double z0, z1;
+      philox_pair_d(a.seed, a.chain0 + ch, a.step, a.slot, (uint32_t)((d0 + fi) * NP + kk), z0, z1);
+      Nz[fl * BNT + cs * BKC + 2 * kk] = z0;
+      Nz[fl * BNT + cs * BKC + 2 * kk + 1] = z1;
+    }
+  } else {                                        // nfl == tile width, fmap = identity
+    const int e0 = d0 * BKC, ne = min(nfl, nfeat) * BKC;
+    const int g0 = e0 >> 2, ng = ((e0 + ne + 3) >> 2) - g0;
+    for (int t = tid; t < BCT * ng; t += 256) {
+      const int cs = t / ng, g = g0 + (t - cs * ng), ch = chs[cs];
+      if (ch < 0) continue;
+      float z4[4];
+      philox_normal4(a.seed, a.chain0 + ch, a.step, a.slot, (uint32_t)g, z4);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int e = 4 * g + q - e0;
+        if (e >= 0 && e < ne) Nz[(e / BKC) * BNT + cs * BKC + (e % BKC)] = z4[q];
+      }
+    }
+  }
 }
 
 // Bias sub-step of one 16-chain tile (sghmc.py:32-34 on the bias), run by the feature-tile-0
@@ -331,10 +367,7 @@ __device__ inline void bias_substep(const BGradArgs<T>& a, const int* chs, T* pb
       T p = a.pb[col];
       const T bp = bb + a.eps * p;
       const T gr = -(c - a.alpha * bp);
-      float z4[4] = {0.f, 0.f, 0.f, 0.f};
-      const uint32_t e = (uint32_t)(D * BKC + k);
-      if (a.noise_mode != HMCX_NOISE_BUFFER) philox_normal4(a.seed, a.chain0 + ch, a.step, a.slot, e >> 2, z4);
-      const T z = bnoise(a, ch, e, z4);
+      const T z = bnoise(a, ch, (uint32_t)(D * BKC + k));
       p = (a.one_minus_eps * p + a.eps * gr) + a.noise_scale * z;
       a.pb[col] = p;
       a.b[col] = bp;
@@ -361,9 +394,9 @@ __device__ inline void bias_substep(const BGradArgs<T>& a, const int* chs, T* pb
 template <typename T>
 __global__ __launch_bounds__(256) void k_bgrad(BGradArgs<T> a) {
   using M = mfma16<T>;
-  __shared__ T Xs[BCH * BXPG];         // [row][feature]
-  __shared__ T Ds[BCH * BWP];          // [row][column]; later the p² tile
-  __shared__ float Nz[BRW * BNT];      // friction noise of the tile
+  constexpr int XSN = BCH * BXPG > 8 * BNT * 8 / (int)sizeof(T) ? BCH * BXPG : 8 * BNT * 8 / (int)sizeof(T);
+  __shared__ __attribute__((aligned(16))) T Xs[XSN];   // [row][feature]; later the per-lane-group p² sums
+  __shared__ __attribute__((aligned(16))) T Ds[BCH * BWP];   // [row][column]; later the friction noise
   __shared__ int chs[BCT];
   __shared__ T pbs[BNT];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lg = lane >> 4;
@@ -374,23 +407,6 @@ __global__ __launch_bounds__(256) void k_bgrad(BGradArgs<T> a) {
   const int D = a.D, N = a.N, B = a.B;
   if (tid < BCT) chs[tid] = rank0 + tid < a.c_act ? a.perm[rank0 + tid] : -1;
   __syncthreads();
-
-  // noise of the tile: chain slot cs, elements e = d·K + k (d in [d0, d0+nfeat)), 4 per Philox block
-  if (a.noise_mode != HMCX_NOISE_BUFFER) {
-    const int e0 = d0 * BKC, ne = nfeat * BKC;
-    const int g0 = e0 >> 2, ng = ((e0 + ne + 3) >> 2) - g0;
-    for (int t = tid; t < BCT * ng; t += 256) {
-      const int cs = t / ng, g = g0 + (t - cs * ng), ch = chs[cs];
-      if (ch < 0) continue;
-      float z4[4];
-      philox_normal4(a.seed, a.chain0 + ch, a.step, a.slot, (uint32_t)g, z4);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int e = 4 * g + q - e0;
-        if (e >= 0 && e < ne) Nz[(e / BKC) * BNT + cs * BKC + (e % BKC)] = z4[q];
-      }
-    }
-  }
 
   StageMap<T> sm(tid, chs);                          // X chunk [32 rows][32 features]
   const StageCM scm(tid, chs, (size_t)B * BKC);      // diff chunk [32 rows][16 chains × 10]
@@ -436,9 +452,15 @@ __global__ __launch_bounds__(256) void k_bgrad(BGradArgs<T> a) {
     }
   }
   __syncthreads();
+  // friction noise of the tile into the diff chunk's space ([32 features][160], T)
+  T* Nz = Ds;
+  if (a.noise_mode != HMCX_NOISE_BUFFER) {
+    gen_tile_noise(a, chs, d0, nfeat, Nz, BRW, [](int fl) { return fl; });
+    __syncthreads();
+  }
 
   // ---- epilogue on the accumulators: softmax.py:57-58 gradient, sghmc.py:31,34 momentum, :32 drift
-  T* P2 = Ds;                                        // [BRW][BWP] p² of chains ending here
+  double* kp = reinterpret_cast<double*>(Xs);        // [mt·4 + lg][160] Σ p² over the lane's rows
   T* __restrict__ Wg = a.W;                          // all 20 W / pW loads first (no aliasing), then
   T* __restrict__ Pg = a.pW;                         // the updates: one HBM round trip per thread
   T wv[5][4], pv[5][4];
@@ -454,12 +476,13 @@ __global__ __launch_bounds__(256) void k_bgrad(BGradArgs<T> a) {
       pv[j][q] = ok ? Pg[idx] : T(0);
     }
 #pragma unroll
-  for (int j = 0; j < 5; ++j)
+  for (int j = 0; j < 5; ++j) {
+    const int col = (nh * 5 + j) * 16 + lr;
+    double p2s = 0.0;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int fi = mt * 16 + M::row(lane, q), col = (nh * 5 + j) * 16 + lr;
+      const int fi = mt * 16 + M::row(lane, q);
       const int cs = col / BKC, k = col - cs * BKC, ch = chs[cs];
-      T p2 = T(0);
       if (ch >= 0 && fi < nfeat) {
         const int d = d0 + fi;
         const size_t idx = ((size_t)ch * D + d) * BKC + k;
@@ -467,22 +490,23 @@ __global__ __launch_bounds__(256) void k_bgrad(BGradArgs<T> a) {
         const T gr = -(acc[j][q] - a.alpha * w);
         const T z = a.noise_mode == HMCX_NOISE_BUFFER
                         ? (T)a.noise[a.noff[ch] + (int64_t)a.slot * a.P + (uint32_t)(d * BKC + k)]
-                        : (T)Nz[fi * BNT + col];
+                        : Nz[fi * BNT + col];
         const T p = (a.one_minus_eps * pv[j][q] + a.eps * gr) + a.noise_scale * z;
         Pg[idx] = p;
         const int n = a.n_iter[ch];
         if (a.iter < n - 1) Wg[idx] = w + a.eps * p;
-        else p2 = p * p;
+        else p2s += (double)(p * p);
       }
-      P2[fi * BWP + col] = p2;
     }
+    kp[(mt * 4 + lg) * BNT + col] = p2s;
+  }
   __syncthreads();
   if (tid < BCT) {                                   // Σ pW² per chain ending at this iteration
     const int ch = chs[tid];
     if (ch >= 0 && a.iter == a.n_iter[ch] - 1) {
       double v = 0.0;
-      for (int fi = 0; fi < nfeat; ++fi)
-        for (int k = 0; k < BKC; ++k) v += (double)P2[fi * BWP + tid * BKC + k];
+      for (int k = 0; k < BKC; ++k)
+        for (int g = 0; g < 8; ++g) v += kp[g * BNT + tid * BKC + k];
       a.kin_part[(size_t)bx * a.C + ch] = v;
     }
   }
@@ -501,8 +525,9 @@ __global__ __launch_bounds__(256) void k_bgrad2(BGradArgs<T> a) {
   typedef typename StageMap<T>::v2 v2;
   constexpr int XSN = BCH * BXP2 > 8 * BNT * 8 / (int)sizeof(T) ? BCH * BXP2 : 8 * BNT * 8 / (int)sizeof(T);
   __shared__ __attribute__((aligned(16))) T Xs[XSN];   // [row][feature]; later the per-lane-group p² sums
-  constexpr int DSN = BCH * BWP > BRW2 * BNT * 4 / (int)sizeof(T) ? BCH * BWP : BRW2 * BNT * 4 / (int)sizeof(T);
-  __shared__ __attribute__((aligned(16))) T Ds[DSN];   // [row][column]; later the friction noise (float)
+  constexpr int NZN = sizeof(T) == 8 ? 32 * BNT : BRW2 * BNT;   // noise rows of one pass
+  constexpr int DSN = BCH * BWP > NZN ? BCH * BWP : NZN;
+  __shared__ __attribute__((aligned(16))) T Ds[DSN];   // [row][column]; later the friction noise
   __shared__ int chs[BCT];
   __shared__ T pbs[BNT];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lg = lane >> 4;
@@ -569,74 +594,71 @@ __global__ __launch_bounds__(256) void k_bgrad2(BGradArgs<T> a) {
     }
   }
   __syncthreads();
-  // friction noise of the tile into the diff chunk's space: chain slot cs, elements e = d·K + k
-  float* Nz = reinterpret_cast<float*>(Ds);          // [64 features][160]
-  if (a.noise_mode != HMCX_NOISE_BUFFER) {
-    const int e0 = d0 * BKC, ne = nfeat * BKC;
-    const int g0 = e0 >> 2, ng = ((e0 + ne + 3) >> 2) - g0;
-    for (int t = tid; t < BCT * ng; t += 256) {
-      const int cs = t / ng, g = g0 + (t - cs * ng), ch = chs[cs];
-      if (ch < 0) continue;
-      float z4[4];
-      philox_normal4(a.seed, a.chain0 + ch, a.step, a.slot, (uint32_t)g, z4);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int e = 4 * g + q - e0;
-        if (e >= 0 && e < ne) Nz[(e / BKC) * BNT + cs * BKC + (e % BKC)] = z4[q];
-      }
-    }
-    __syncthreads();
-  }
-
-  // ---- epilogue on the accumulators: softmax.py:57-58 gradient, sghmc.py:31,34 momentum, :32 drift
+  // ---- epilogue on the accumulators: softmax.py:57-58 gradient, sghmc.py:31,34 momentum, :32 drift.
+  // The friction noise of the tile goes into the diff chunk's space first: f32 chains in one pass
+  // ([64 features][160] floats); f64 chains in two passes of 32 features (m-tile i = pass: local
+  // feature fl = mt·16 + row), [32][160] doubles each, so two workgroups still fit per CU.
+  constexpr int NPASS = sizeof(T) == 8 ? 2 : 1;
+  T* Nz = Ds;
   double* kp = reinterpret_cast<double*>(Xs);        // [mt·4 + lg][160] Σ p² over the lane's rows
-  // The 8 elements of one column (2 m-tiles × 4 rows) are loaded together (W and pW never alias):
-  // five HBM round trips per thread instead of one per element.
+  // The elements of one column (the pass's m-tiles × 4 rows) are loaded together (W and pW never
+  // alias): one HBM round trip per column instead of one per element.
   T* __restrict__ Wg = a.W;
   T* __restrict__ Pg = a.pW;
-  T wv[1][8], pv[1][8];
-  auto ld_col = [&](int j, T (&w8)[8], T (&p8)[8]) {
-    const int col = (nh * 5 + j) * 16 + lr;
-    const int cs = col / BKC, k = col - cs * BKC, ch = chs[cs];
+  double p2s[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+  for (int h = 0; h < NPASS; ++h) {
+    if (a.noise_mode != HMCX_NOISE_BUFFER) {
+      if (h) __syncthreads();                      // pass 0's noise has been read
+      if constexpr (NPASS == 2)
+        gen_tile_noise(a, chs, d0, nfeat, Nz, 32, [h](int fl) { return (fl >> 4) * 32 + h * 16 + (fl & 15); });
+      else
+        gen_tile_noise(a, chs, d0, nfeat, Nz, BRW2, [](int fl) { return fl; });
+      __syncthreads();
+    }
+    constexpr int NI = 2 / NPASS;                    // m-tiles of this pass
+    const int i0 = NPASS == 2 ? h : 0;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int fi = mt * 32 + i * 16 + M::row(lane, q);
-        const bool ok = ch >= 0 && fi < nfeat;
-        const size_t idx = ok ? ((size_t)ch * D + (d0 + fi)) * BKC + k : 0;
-        w8[i * 4 + q] = ok ? Wg[idx] : T(0);
-        p8[i * 4 + q] = ok ? Pg[idx] : T(0);
-      }
-  };
+    for (int j = 0; j < 5; ++j) {
+      const int col = (nh * 5 + j) * 16 + lr;
+      const int cs = col / BKC, k = col - cs * BKC, ch = chs[cs];
+      const bool last = ch >= 0 && a.iter >= a.n_iter[ch] - 1;
+      T wv[NI * 4], pv[NI * 4];
 #pragma unroll
-  for (int j = 0; j < 5; ++j) {
-    ld_col(j, wv[0], pv[0]);
-    const int col = (nh * 5 + j) * 16 + lr;
-    const int cs = col / BKC, k = col - cs * BKC, ch = chs[cs];
-    const bool last = ch >= 0 && a.iter >= a.n_iter[ch] - 1;
-    double p2s = 0.0;
+      for (int ii = 0; ii < NI; ++ii)
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int fi = mt * 32 + i * 16 + M::row(lane, q);
-        if (ch >= 0 && fi < nfeat) {
-          const int d = d0 + fi;
-          const size_t idx = ((size_t)ch * D + d) * BKC + k;
-          const T w = wv[0][i * 4 + q];
-          const T gr = -(acc[i][j][q] - a.alpha * w);
-          const T z = a.noise_mode == HMCX_NOISE_BUFFER
-                          ? (T)a.noise[a.noff[ch] + (int64_t)a.slot * a.P + (uint32_t)(d * BKC + k)]
-                          : (T)Nz[fi * BNT + col];
-          const T p = (a.one_minus_eps * pv[0][i * 4 + q] + a.eps * gr) + a.noise_scale * z;
-          Pg[idx] = p;
-          if (!last) Wg[idx] = w + a.eps * p;
-          else p2s += (double)(p * p);
+        for (int q = 0; q < 4; ++q) {
+          const int fi = mt * 32 + (i0 + ii) * 16 + M::row(lane, q);
+          const bool ok = ch >= 0 && fi < nfeat;
+          const size_t idx = ok ? ((size_t)ch * D + (d0 + fi)) * BKC + k : 0;
+          wv[ii * 4 + q] = ok ? Wg[idx] : T(0);
+          pv[ii * 4 + q] = ok ? Pg[idx] : T(0);
         }
-      }
-    kp[(mt * 4 + lg) * BNT + col] = p2s;
+#pragma unroll
+      for (int ii = 0; ii < NI; ++ii)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int i = i0 + ii;
+          const int fi = mt * 32 + i * 16 + M::row(lane, q);
+          if (ch >= 0 && fi < nfeat) {
+            const int d = d0 + fi;
+            const size_t idx = ((size_t)ch * D + d) * BKC + k;
+            const T w = wv[ii * 4 + q];
+            const T gr = -(acc[i][j][q] - a.alpha * w);
+            const int nzr = NPASS == 2 ? mt * 16 + M::row(lane, q) : fi;
+            const T z = a.noise_mode == HMCX_NOISE_BUFFER
+                            ? (T)a.noise[a.noff[ch] + (int64_t)a.slot * a.P + (uint32_t)(d * BKC + k)]
+                            : Nz[nzr * BNT + col];
+            const T p = (a.one_minus_eps * pv[ii * 4 + q] + a.eps * gr) + a.noise_scale * z;
+            Pg[idx] = p;
+            if (!last) Wg[idx] = w + a.eps * p;
+            else p2s[j] += (double)(p * p);
+          }
+        }
+    }
   }
+#pragma unroll
+  for (int j = 0; j < 5; ++j) kp[(mt * 4 + lg) * BNT + (nh * 5 + j) * 16 + lr] = p2s[j];
   __syncthreads();
   if (tid < BCT) {                                   // Σ pW² per chain ending at this iteration
     const int ch = chs[tid];

@@ -95,6 +95,70 @@ __host__ __device__ inline float philox_normal(uint64_t seed, uint32_t chain, ui
   return (e & 1u) ? z1 : z0;
 }
 
+// Float64 standard normals for the f64 chains (the reference draws f64 normals, cpu/sghmc.py:21,31,
+// cpu/sgld.py:45): one Philox block = two 53-bit uniforms = one Box–Muller pair in double precision
+// (u1 = (k+1)·2⁻⁵³ ∈ (0,1], so |z| reaches sqrt(2·53·ln 2) ≈ 8.57σ; θ = 2π·u2 via sincospi, no
+// range reduction).  Element e uses the block with counter e >> 1 (e & 1 picks cos / sin), so four
+// elements 4b..4b+3 are blocks 2b and 2b+1.
+__host__ __device__ inline void box_muller_d(const u32x4& r, double& z0, double& z1) {
+  const uint64_t k1 = ((uint64_t)r.v[0] << 21) ^ (uint64_t)(r.v[1] >> 11);
+  const double u1 = (double)(k1 + 1) * (1.0 / 9007199254740992.0);       // (0,1]
+  const double u2 = u53(r.v[2], r.v[3]);                                 // [0,1)
+  const double rad = sqrt(-2.0 * log(u1));
+  double s, c;
+#if defined(__HIP_DEVICE_COMPILE__)
+  sincospi(2.0 * u2, &s, &c);
+#else
+  const double th = 6.283185307179586476925 * u2;
+  s = sin(th);
+  c = cos(th);
+#endif
+  z0 = rad * c;
+  z1 = rad * s;
+}
+
+__host__ __device__ inline void philox_normal4(uint64_t seed, uint32_t chain, uint32_t step, uint32_t slot,
+                                               uint32_t blk, double z[4]) {
+  const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+  u32x4 c0 = {{2u * blk, slot, step, chain}}, c1 = {{2u * blk + 1u, slot, step, chain}};
+  box_muller_d(philox4x32_10(c0, k0, k1), z[0], z[1]);
+  box_muller_d(philox4x32_10(c1, k0, k1), z[2], z[3]);
+}
+
+// Elements 2·pair and 2·pair + 1 of the f64 stream.
+__host__ __device__ inline void philox_pair_d(uint64_t seed, uint32_t chain, uint32_t step, uint32_t slot,
+                                              uint32_t pair, double& z0, double& z1) {
+  u32x4 c = {{pair, slot, step, chain}};
+  box_muller_d(philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32)), z0, z1);
+}
+
+__host__ __device__ inline double philox_normal_d(uint64_t seed, uint32_t chain, uint32_t step,
+                                                  uint32_t slot, uint32_t e) {
+  u32x4 c = {{e >> 1, slot, step, chain}};
+  double z0, z1;
+  box_muller_d(philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32)), z0, z1);
+  return (e & 1u) ? z1 : z0;
+}
+
+// Noise of a chain computing in T: f32 chains take the float Box–Muller above (24-bit uniforms,
+// |z| ≤ 5.77σ, fast transcendentals), f64 chains the double one.
+template <typename T> struct NormalT;
+template <> struct NormalT<float> {
+  __host__ __device__ static inline float one(uint64_t s, uint32_t c, uint32_t st, uint32_t sl, uint32_t e) {
+    return philox_normal(s, c, st, sl, e);
+  }
+};
+template <> struct NormalT<double> {
+  __host__ __device__ static inline double one(uint64_t s, uint32_t c, uint32_t st, uint32_t sl, uint32_t e) {
+    return philox_normal_d(s, c, st, sl, e);
+  }
+};
+template <typename T>
+__host__ __device__ inline T philox_normal_t(uint64_t seed, uint32_t chain, uint32_t step, uint32_t slot,
+                                             uint32_t e) {
+  return NormalT<T>::one(seed, chain, step, slot, e);
+}
+
 // ---------------------------------------------------------------- MFMA 16x16x4
 // A[i][k]: lane l holds i = l&15, k = l>>4; B[k][j]: k = l>>4, j = l&15 (both dtypes).
 // C/D: f32: row = (l>>4)*4 + r, col = l&15;  f64: row = (l>>4) + 4*r, col = l&15.

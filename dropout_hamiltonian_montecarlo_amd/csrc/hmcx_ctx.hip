@@ -246,7 +246,7 @@ __global__ void k_hmc_mvn(MvnArgs a) {
     for (int j = 0; j < a.dim; ++j) {
       double z;
       if (a.noise_mode == HMCX_NOISE_BUFFER) z = a.noise[a.noff[(size_t)s * a.C + c] + j];
-      else z = philox_normal(a.seed, a.chain0 + c, a.step_base + s, 0u, (uint32_t)j);
+      else z = philox_normal_d(a.seed, a.chain0 + c, a.step_base + s, 0u, (uint32_t)j);
       p0[j] = z; p[j] = z; xn[j] = x[j];
     }
     mvn_grad(a, x, g);                                   // hmc.py:47
@@ -272,6 +272,29 @@ __global__ void k_hmc_mvn(MvnArgs a) {
       for (int j = 0; j < a.dim; ++j) a.out_trace[((size_t)s * a.C + c) * a.dim + j] = x[j];
   }
   for (int j = 0; j < a.dim; ++j) a.x[c * a.dim + j] = x[j];
+}
+
+// Per-call MVN surface (mvn_gaussian.py:14-31): one thread per parameter set.
+__global__ void k_mvn_eval(MvnArgs a, const double* x, double* g, double* nlp) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= a.C) return;
+  double xv[MVN_MAXDIM], gv[MVN_MAXDIM];
+  for (int j = 0; j < a.dim; ++j) xv[j] = x[c * a.dim + j];
+  if (g) {
+    mvn_grad(a, xv, gv);
+    for (int j = 0; j < a.dim; ++j) g[c * a.dim + j] = gv[j];
+  }
+  if (nlp) nlp[c] = mvn_nlp(a, xv);
+}
+
+int mvn_eval(hmcx_ctx* ctx, int dim, int C, const double* mu, const double* prec, double nlp_const, const double* x,
+             double* g, double* nlp) {
+  if (dim < 1 || dim > MVN_MAXDIM) return set_error(ctx, HMCX_EUNSUPPORTED, "mvn: dim must be 1..16");
+  MvnArgs a{};
+  a.dim = dim; a.C = C; a.mu = mu; a.prec = prec; a.nlp_const = nlp_const;
+  hipLaunchKernelGGL(k_mvn_eval, dim3((C + 63) / 64), dim3(64), 0, ctx->stream, a, x, g, nlp);
+  HMCX_HIP(ctx, hipGetLastError());
+  return HMCX_OK;
 }
 
 int hmc_mvn_run(hmcx_ctx* ctx, const hmcx_hmc_mvn_args* s) {
@@ -420,6 +443,11 @@ void hmcx_philox_normals(uint64_t seed, uint32_t chain, uint32_t step, uint32_t 
   for (uint32_t i = 0; i < n; ++i) out[i] = philox_normal(seed, chain, step, slot, e0 + i);
 }
 
+void hmcx_philox_normals_f64(uint64_t seed, uint32_t chain, uint32_t step, uint32_t slot, uint32_t e0, uint32_t n,
+                             double* out) {
+  for (uint32_t i = 0; i < n; ++i) out[i] = philox_normal_d(seed, chain, step, slot, e0 + i);
+}
+
 static int check_dims(hmcx_ctx* ctx, int dtype, int B, int D, int K, int C) {
   if (dtype != HMCX_F32 && dtype != HMCX_F64) return set_error(ctx, HMCX_EINVAL, "dtype must be HMCX_F32/HMCX_F64");
   if (B < 1 || D < 1 || K < 1 || C < 1) return set_error(ctx, HMCX_EINVAL, "B, D, K, C must be >= 1");
@@ -492,6 +520,43 @@ int hmcx_sumsq(hmcx_ctx* ctx, int dtype, const void* x, int64_t n, double* out) 
   if (dtype != HMCX_F32 && dtype != HMCX_F64) return set_error(ctx, HMCX_EINVAL, "dtype must be HMCX_F32/HMCX_F64");
   if (n < 0 || (n > 0 && !x) || !out) return set_error(ctx, HMCX_EINVAL, "hmcx_sumsq: bad arguments");
   return dtype == HMCX_F64 ? sumsq_t<double>(ctx, x, n, out) : sumsq_t<float>(ctx, x, n, out);
+}
+
+int hmcx_hmc_run(hmcx_ctx* ctx, const hmcx_hmc_args* a) {
+  HMCX_GUARD_CTX(ctx);
+  if (!a) return set_error(ctx, HMCX_EINVAL, "null args");
+  if (a->model != HMCX_MODEL_SOFTMAX && a->model != HMCX_MODEL_LOGISTIC)
+    return set_error(ctx, HMCX_EINVAL, "hmc: model must be HMCX_MODEL_SOFTMAX or HMCX_MODEL_LOGISTIC");
+  if (a->model == HMCX_MODEL_LOGISTIC && a->K != 1) return set_error(ctx, HMCX_EINVAL, "hmc: logistic needs K = 1");
+  int rc = check_dims(ctx, a->dtype, a->B, a->D, a->K, 1);
+  if (rc) return rc;
+  if (a->n_steps < 0) return set_error(ctx, HMCX_EINVAL, "n_steps < 0");
+  if (a->n_steps == 0) return HMCX_OK;
+  if (!a->X || !a->Y || !a->W || !a->b || !a->eps || !a->n_iter || !a->u_accept || !a->out_A || !a->out_accepted ||
+      !a->out_nlp)
+    return set_error(ctx, HMCX_EINVAL, "null pointer");
+  if (a->noise_mode == HMCX_NOISE_BUFFER && (!a->noise || !a->noise_off))
+    return set_error(ctx, HMCX_EINVAL, "BUFFER noise needs noise and noise_off");
+  if (a->noise_mode != HMCX_NOISE_BUFFER && a->noise_mode != HMCX_NOISE_PHILOX)
+    return set_error(ctx, HMCX_EINVAL, "bad noise_mode");
+  for (int i = 0; i < a->n_steps; ++i)
+    if (a->n_iter[i] < 0) return set_error(ctx, HMCX_EINVAL, "n_iter < 0");
+  return a->dtype == HMCX_F64 ? hmc_run_t<double>(ctx, a) : hmc_run_t<float>(ctx, a);
+}
+
+int hmcx_mvn_eval(hmcx_ctx* ctx, int dim, int C, const double* mu, const double* prec, double nlp_const,
+                  const double* x, double* g, double* nlp) {
+  HMCX_GUARD_CTX(ctx);
+  if (C < 1 || !mu || !prec || !x || (!g && !nlp)) return set_error(ctx, HMCX_EINVAL, "hmcx_mvn_eval: bad arguments");
+  return mvn_eval(ctx, dim, C, mu, prec, nlp_const, x, g, nlp);
+}
+
+int hmcx_axpy(hmcx_ctx* ctx, int dtype, int mode, int64_t n, double a, const void* x, void* y) {
+  HMCX_GUARD_CTX(ctx);
+  if (dtype != HMCX_F32 && dtype != HMCX_F64) return set_error(ctx, HMCX_EINVAL, "dtype must be HMCX_F32/HMCX_F64");
+  if (mode != 0 && mode != 1) return set_error(ctx, HMCX_EINVAL, "hmcx_axpy: mode must be 0 or 1");
+  if (n < 0 || (n > 0 && (!x || !y))) return set_error(ctx, HMCX_EINVAL, "hmcx_axpy: bad arguments");
+  return dtype == HMCX_F64 ? axpy_t<double>(ctx, mode, n, a, x, y) : axpy_t<float>(ctx, mode, n, a, x, y);
 }
 
 int hmcx_sgd_run(hmcx_ctx* ctx, const hmcx_sgd_args* a) {

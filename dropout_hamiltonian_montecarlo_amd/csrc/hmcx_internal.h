@@ -95,7 +95,11 @@ Tiling make_tiling(int B, int D, int K, int C);
 
 enum FwdMode { FWD_GRAD = 0, FWD_SGHMC = 1, FWD_LL = 2, FWD_PRED = 3 };
 // GRAD_SGLD_GPU: the CuPy file's SGLD update p = ν⊙p_prev − ½ε∇U, q += p (gpu/sgld.py:11-20, A2g)
-enum GradMode { GRAD_OUT = 0, GRAD_SGHMC = 1, GRAD_SGLD = 2, GRAD_SGD = 3, GRAD_SGLD_GPU = 4 };
+// GRAD_HMC: full-batch HMC sub-steps (cpu/hmc.py:49-54) fused into the gradient epilogue, per hmc_flags
+enum GradMode { GRAD_OUT = 0, GRAD_SGHMC = 1, GRAD_SGLD = 2, GRAD_SGD = 3, GRAD_SGLD_GPU = 4, GRAD_HMC = 5 };
+// After gradient evaluation k of an HMC trajectory: full kick of the variable drifted before it
+// (p_v −= ε·g_v) and the half kick + drift of the next one (p_v −= ½ε·g_v; q_v += ε·p_v).
+enum HmcFlags { HMC_KICK_W = 1, HMC_KICK_B = 2, HMC_HALF_W = 4, HMC_HALF_B = 8 };
 // Output link of the linear model: softmax over K classes (models/cpu/softmax.py) or the
 // sigmoid of K = 1 logistic regression (models/cpu/logistic.py:43-55).
 enum Link { LINK_SOFTMAX = 0, LINK_SIGMOID = 1 };
@@ -123,6 +127,8 @@ template <typename T> struct GradArgs {
   int mode;
   T alpha, eps, one_minus_eps, noise_scale, m_half_eps;
   T gamma, lr;               // GRAD_SGD: momentum decay and step size (sgd.py:40)
+  T half_eps;                // GRAD_HMC: 0.5·ε (hmc.py:50)
+  int hmc_flags;             // GRAD_HMC: HmcFlags
   int iter;
   const int32_t* n_iter;
   const T* Wsrc; const T* bsrc;
@@ -185,11 +191,14 @@ template <typename T> int softmax_predict_t(hmcx_ctx*, const void*, int, int, in
 template <typename T> int sgd_run_t(hmcx_ctx*, const hmcx_sgd_args*);
 template <typename T> int sumsq_t(hmcx_ctx*, const void*, int64_t, double*);
 template <typename T> int sghmc_run_t(hmcx_ctx*, const hmcx_sampler_args*);
+template <typename T> int hmc_run_t(hmcx_ctx*, const hmcx_hmc_args*);
+template <typename T> int axpy_t(hmcx_ctx*, int, int64_t, double, const void*, void*);
 bool sghmc_p2_selected(hmcx_ctx*, const hmcx_sampler_args*);   // hmcx_softmax.hip
 template <typename T> int sgld_run_t(hmcx_ctx*, const hmcx_sampler_args*);
 bool sgld_wide_eligible(const hmcx_sampler_args*);       // hmcx_wide.hip: one chain, K ≤ 64
 template <typename T> int sgld_wide_t(hmcx_ctx*, const hmcx_sampler_args*);
 int hmc_mvn_run(hmcx_ctx*, const hmcx_hmc_mvn_args*);
+int mvn_eval(hmcx_ctx*, int, int, const double*, const double*, double, const double*, double*, double*);
 template <typename T> int mlp_grad_t(hmcx_ctx*, const void*, const int32_t*, int, int, int, int,
                                      const hmcx_mlp_params*, const void*, double, hmcx_mlp_params*, double*);
 template <typename T> int mlp_loss_t(hmcx_ctx*, const void*, const int32_t*, int, int, int, int,

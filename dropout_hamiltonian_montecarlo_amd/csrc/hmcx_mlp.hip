@@ -110,7 +110,7 @@ __device__ inline void apply_upd(const Upd<T>& u, int mode, size_t i, T v) {
   } else {
     const T g = v + u.half_alpha * u.W[i];
     const T z = u.noise_mode == HMCX_NOISE_BUFFER ? (T)u.noise[i]
-                                                  : (T)philox_normal(u.seed, u.chain, u.step, u.slot, u.e0 + (uint32_t)i);
+                                                  : philox_normal_t<T>(u.seed, u.chain, u.step, u.slot, u.e0 + (uint32_t)i);
     const T p = (u.one_minus_eps * u.P[i] + u.eps * g) + u.noise_scale * z;
     u.P[i] = p;
     if (u.Qn) u.Qn[i] = u.W[i] + u.eps * p;                   // sghmc.py:32 of the next iteration
@@ -581,7 +581,7 @@ __global__ __launch_bounds__(256) void k_mlp_init(VarTab vt, T eps, int drift, i
   double sp = 0.0, sq = 0.0;
   for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += NPART * 256) {
     const uint32_t e = (uint32_t)(vt.e0[v] + i);
-    const T z = noise_mode == HMCX_NOISE_BUFFER ? (T)noise[e] : (T)philox_normal(seed, chain, step, 0u, e);
+    const T z = noise_mode == HMCX_NOISE_BUFFER ? (T)noise[e] : philox_normal_t<T>(seed, chain, step, 0u, e);
     const T qv = q[i];
     p[i] = z;
     if (drift) qn[i] = qv + eps * z;

@@ -289,12 +289,19 @@ __device__ inline int qdiv(int e, float inv) { return (int)(((float)e + 0.5f) * 
 // Noise value of flat element e for slot `slot` of step s: Philox block z4 (already generated for
 // block e >> 2) or the host-drawn buffer (cpu/sghmc.py:21,31 draw order).
 template <typename T>
-__device__ inline T noise_at(const Q2Args& a, int s, uint32_t slot, uint32_t e, const float* z4) {
+__device__ inline T noise_at(const Q2Args& a, int s, uint32_t slot, uint32_t e, const T* z4) {
   if (a.noise_mode == HMCX_NOISE_BUFFER) return (T)a.noise[a.noff[s] + (int64_t)slot * a.P + e];
-  return (T)z4[e & 3];
+  return z4[e & 3];
 }
-__device__ inline void philox4_if(const Q2Args& a, int s, uint32_t slot, uint32_t g, float z[4]) {
+template <typename T>
+__device__ inline void philox4_if(const Q2Args& a, int s, uint32_t slot, uint32_t g, T z[4]) {
   if (a.noise_mode != HMCX_NOISE_BUFFER) philox_normal4(a.seed, a.chain0, a.step_base + (uint32_t)s, slot, g, z);
+}
+// One element's noise (f32 chains: float Box–Muller; f64 chains: the double one, hmcx_common.h).
+template <typename T>
+__device__ inline T noise1(const Q2Args& a, int s, uint32_t slot, uint32_t e) {
+  if (a.noise_mode == HMCX_NOISE_BUFFER) return (T)a.noise[a.noff[s] + (int64_t)slot * a.P + e];
+  return philox_normal_t<T>(a.seed, a.chain0, a.step_base + (uint32_t)s, slot, e);
 }
 
 // Minibatch tile X[row0:+nrow, feat0:+nfeat] → LDS [Br][BFP], zero padded to BfP columns;
@@ -537,17 +544,10 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
     //      previous accept round travelled), momentum (hmc.py:82-87), step-start copies
     if (s == 0 || !a.prefetch) load_step_rows<T>(Xs, Yo, Xg, Yg, Br, BfP, BFP, nrow, nfeat, row0, feat0, D, K, Ro, nro, ro0);
     for (int e = tid; e < BfP * 16; e += QTH) Wf0[e] = Wf[e];
-    {
-      float z4[4];
-      if (own) philox4_if(a, s, 0u, (uint32_t)(e_own >> 2), z4);
-      pw = own ? noise_at<T>(a, s, 0u, (uint32_t)e_own, z4) : T(0);
-      w0 = wv;
-    }
+    pw = own ? noise1<T>(a, s, 0u, (uint32_t)e_own) : T(0);
+    w0 = wv;
     if (tid < 16) {
-      float z4[4];
-      const uint32_t e = (uint32_t)(D * K + tid);
-      if (tid < K) philox4_if(a, s, 0u, e >> 2, z4);
-      pbsh[tid] = tid < K ? noise_at<T>(a, s, 0u, e, z4) : T(0);
+      pbsh[tid] = tid < K ? noise1<T>(a, s, 0u, (uint32_t)(D * K + tid)) : T(0);
       b0sh[tid] = bsh[tid];
     }
     const double kin0 = wsum((double)pw * (double)pw, dsh);
@@ -589,7 +589,7 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
         // drift of the whole F_f slice by p0 (every member computes it identically; sghmc.py:32)
         const int ge0 = (feat0 * K) >> 2, ge1 = ((feat0 + nfeat) * K + 3) >> 2;
         for (int g = ge0 + tid; g < ge1; g += QTH) {
-          float z4[4];
+          T z4[4];
           philox4_if(a, s, 0u, (uint32_t)g, z4);
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
@@ -615,7 +615,6 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
         // by the waves that do not poll the A-RS round, into LDS; the owners pick it up below
         const int zi = tid - NZ0;
         if (zi >= 0 && zi < nfo * KC + K) {
-          float z4[4];
           bool v = true;
           uint32_t e;
           if (zi < nfo * KC) {
@@ -625,18 +624,11 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
           } else {
             e = (uint32_t)(D * K + zi - nfo * KC);
           }
-          if (v) philox4_if(a, s, (uint32_t)(it + 1), e >> 2, z4);
-          zbuf[zi] = v ? noise_at<T>(a, s, (uint32_t)(it + 1), e, z4) : T(0);
+          zbuf[zi] = v ? noise1<T>(a, s, (uint32_t)(it + 1), e) : T(0);
         }
       } else {
-        float z4[4];
-        if (own) philox4_if(a, s, (uint32_t)(it + 1), (uint32_t)(e_own >> 2), z4);
-        zn = own ? noise_at<T>(a, s, (uint32_t)(it + 1), (uint32_t)e_own, z4) : T(0);
-        if (tid < K) {
-          const uint32_t e = (uint32_t)(D * K + tid);
-          philox4_if(a, s, (uint32_t)(it + 1), e >> 2, z4);
-          zb = noise_at<T>(a, s, (uint32_t)(it + 1), e, z4);
-        }
+        zn = own ? noise1<T>(a, s, (uint32_t)(it + 1), (uint32_t)e_own) : T(0);
+        if (tid < K) zb = noise1<T>(a, s, (uint32_t)(it + 1), (uint32_t)(D * K + tid));
       }
       prof.stamp(3);
       if (!consumeA()) return;

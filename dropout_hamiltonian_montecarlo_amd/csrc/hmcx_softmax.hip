@@ -272,7 +272,7 @@ __global__ __launch_bounds__(NW * 64) void k_fwd(FwdArgs<T> a) {
 template <typename T>
 __device__ inline double noise_at(const GradArgs<T>& a, int c, uint32_t e) {
   if (a.noise_mode == HMCX_NOISE_BUFFER) return a.noise[a.noff[c] + (int64_t)a.slot * a.P + e];
-  return (double)philox_normal(a.seed, a.chain0 + c, a.step, a.slot, e);
+  return (double)philox_normal_t<T>(a.seed, a.chain0 + c, a.step, a.slot, e);
 }
 
 // ------------------------------------------------------------------ gradient (Xᵀ·diff) kernel
@@ -313,8 +313,8 @@ __global__ __launch_bounds__(NW * 64) void k_grad(GradArgs<T> a) {
         wreg[q] = a.Wsrc[idx];
       } else {
         wreg[q] = a.W[idx];
-        if (mode == GRAD_SGHMC || mode == GRAD_SGD || mode == GRAD_SGLD_GPU) preg[q] = a.pW[idx];
-        if (mode != GRAD_SGD) zreg[q] = (T)noise_at(a, c0 + cc, (uint32_t)(d * K + k));
+        if (mode == GRAD_SGHMC || mode == GRAD_SGD || mode == GRAD_SGLD_GPU || mode == GRAD_HMC) preg[q] = a.pW[idx];
+        if (mode != GRAD_SGD && mode != GRAD_HMC) zreg[q] = (T)noise_at(a, c0 + cc, (uint32_t)(d * K + k));
       }
     }
   }
@@ -382,6 +382,14 @@ __global__ __launch_bounds__(NW * 64) void k_grad(GradArgs<T> a) {
       const T m = a.gamma * preg[q] - a.lr * gr;                          // sgd.py:40
       a.pW[idx] = m;
       a.W[idx] = wreg[q] + m;                                             // sgd.py:41
+    } else if (mode == GRAD_HMC) {
+      T p = preg[q];
+      if (a.hmc_flags & HMC_KICK_W) p = p - a.eps * gr;                   // hmc.py:53
+      if (a.hmc_flags & HMC_HALF_W) {
+        p = p - a.half_eps * gr;                                          // hmc.py:50
+        a.W[idx] = wreg[q] + a.eps * p;                                   // hmc.py:51
+      }
+      a.pW[idx] = p;
     } else if (mode == GRAD_SGLD_GPU) {
       T p = (a.noise_scale * zreg[q]) * preg[q];                          // gpu/sgld.py:18 ν⊙p
       p = p + a.m_half_eps * gr;
@@ -457,6 +465,16 @@ __global__ __launch_bounds__(NW * 64) void k_grad(GradArgs<T> a) {
           const T m = a.gamma * a.pb[col] - a.lr * gr;                      // sgd.py:40-41
           a.pb[col] = m;
           a.b[col] = bb + m;
+        } else if (mode == GRAD_HMC) {
+          const T bb = a.b[col];
+          const T gr = -(cs - a.alpha * bb);
+          T p = a.pb[col];
+          if (a.hmc_flags & HMC_KICK_B) p = p - a.eps * gr;                 // hmc.py:53
+          if (a.hmc_flags & HMC_HALF_B) {
+            p = p - a.half_eps * gr;                                        // hmc.py:50
+            a.b[col] = bb + a.eps * p;                                      // hmc.py:51
+          }
+          a.pb[col] = p;
         } else {
           const T bb = a.b[col];
           const T gr = -(cs - a.alpha * bb);
@@ -502,7 +520,7 @@ __global__ __launch_bounds__(256) void k_sghmc_init(InitArgs<T> a) {
     const size_t w = (size_t)d * a.N + c * K + k;
     double z;
     if (a.noise_mode == HMCX_NOISE_BUFFER) z = a.noise[a.noff[c] + d * K + k];
-    else z = (double)philox_normal(a.seed, a.chain0 + c, a.step, 0u, (uint32_t)(d * K + k));
+    else z = (double)philox_normal_t<T>(a.seed, a.chain0 + c, a.step, 0u, (uint32_t)(d * K + k));
     const T p = (T)z;                                                     // hmc.py:86 N(0,1)
     T q = a.W[w];
     if (take) { q = a.Wwork[w]; a.W[w] = q; }                             // commit (sghmc.py:37)
@@ -524,7 +542,7 @@ __global__ __launch_bounds__(256) void k_sghmc_init(InitArgs<T> a) {
       const int col = c * K + tid;
       double z;
       if (a.noise_mode == HMCX_NOISE_BUFFER) z = a.noise[a.noff[c] + a.D * K + tid];
-      else z = (double)philox_normal(a.seed, a.chain0 + c, a.step, 0u, (uint32_t)(a.D * K + tid));
+      else z = (double)philox_normal_t<T>(a.seed, a.chain0 + c, a.step, 0u, (uint32_t)(a.D * K + tid));
       const T p = (T)z;
       T q = a.b[col];
       if (take) { q = a.bwork[col]; a.b[col] = q; }
@@ -842,6 +860,276 @@ int sumsq_t(hmcx_ctx* ctx, const void* x, int64_t n, double* out) {
   return HMCX_OK;
 }
 
+// ------------------------------------------------------------------ leapfrog axpy (hmc.py:50-53)
+template <typename T>
+__global__ __launch_bounds__(256) void k_axpy(int mode, int64_t n, T a, const T* x, T* y) {   // x may alias y
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const T ax = a * x[i];
+    y[i] = mode == 0 ? y[i] - ax : y[i] + ax;
+  }
+}
+
+template <typename T>
+int axpy_t(hmcx_ctx* ctx, int mode, int64_t n, double a, const void* x, void* y) {
+  if (n == 0) return HMCX_OK;
+  const int64_t nb = std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_axpy<T>, dim3((unsigned)nb), dim3(256), 0, ctx->stream, mode, n, (T)a, (const T*)x, (T*)y);
+  HMCX_HIP(ctx, hipGetLastError());
+  return HMCX_OK;
+}
+
+// ------------------------------------------------------------------ full-batch HMC, linear models
+// hmc.py:39-64 with the softmax / logistic model, one chain.  State: q = (W, b) (caller's buffers),
+// the proposal (Wn, bn) and its momentum (pW, pb) in the workspace.  Per step:
+//   k_hmc_init     p0 (hmc.py:41), proposal := q, Σp0² partials
+//   [n_iter ≥ 1]   1 + 2·n_iter gradient evaluations at the proposal: k_fwd(FWD_GRAD) + k_grad(GRAD_HMC)
+//                  whose epilogue applies the kicks/drifts that follow that evaluation (HmcFlags)
+//   k_fwd(FWD_LL)  log-likelihood of the proposal
+//   k_hmc_accept   energies (hmc.py:67-79), MH decision, nlp of the kept state (carried to the next
+//                  step as its E_current's nlp: the same kernel output, so no recomputation)
+//   k_hmc_commit   q := proposal if accepted; trace row of the kept state
+struct HmcState {
+  double ll, sW, sb;   // log-likelihood and Σθ² (weights, bias) of the current state q
+};
+
+template <typename T>
+struct HmcInitArgs {
+  int D, K, P, nDB;
+  int noise_mode; const double* noise; int64_t noff;
+  uint64_t seed; uint32_t chain, step;
+  const T* W; const T* b; T* Wn; T* bn; T* pW; T* pb; T* mom;
+  double* kin0_part;   // [nDB + 1]: Σ pW0² per block, then Σ pb0²
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_hmc_init(HmcInitArgs<T> a) {
+  __shared__ double ksh[256];
+  const int tid = threadIdx.x, K = a.K;
+  const int e0 = blockIdx.x * 16 * K, ne = min(16 * K, a.D * K - e0);
+  double kin = 0.0;
+  for (int e = tid; e < ne; e += 256) {
+    const int i = e0 + e;
+    const T p = a.noise_mode == HMCX_NOISE_BUFFER ? (T)a.noise[a.noff + i]
+                                                  : philox_normal_t<T>(a.seed, a.chain, a.step, 0u, (uint32_t)i);
+    a.pW[i] = p;
+    a.Wn[i] = a.W[i];
+    if (a.mom) a.mom[i] = p;
+    kin += (double)p * (double)p;
+  }
+  ksh[tid] = kin;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (tid < s) ksh[tid] += ksh[tid + s];
+    __syncthreads();
+  }
+  if (tid == 0) a.kin0_part[blockIdx.x] = ksh[0];
+  if (blockIdx.x == 0) {
+    __syncthreads();
+    double kb = 0.0;
+    if (tid < K) {
+      const int i = a.D * K + tid;
+      const T p = a.noise_mode == HMCX_NOISE_BUFFER ? (T)a.noise[a.noff + i]
+                                                    : philox_normal_t<T>(a.seed, a.chain, a.step, 0u, (uint32_t)i);
+      a.pb[tid] = p;
+      a.bn[tid] = a.b[tid];
+      if (a.mom) a.mom[i] = p;
+      kb = (double)p * (double)p;
+    }
+    ksh[tid] = kb;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+      if (tid < s) ksh[tid] += ksh[tid + s];
+      __syncthreads();
+    }
+    if (tid == 0) a.kin0_part[a.nDB] = ksh[0];
+  }
+}
+
+template <typename T>
+struct HmcAcceptArgs {
+  int D, K, nRB, nDB, n_iter, first, logistic;
+  double u, neg_inv_n, log_prior, lpc0, lpc1, half_alpha;
+  const double* kin0_part; const double* ll0_part; const double* ll1_part;
+  const T* W; const T* b; const T* Wn; const T* bn; const T* pW; const T* pb;
+  HmcState* st;
+  double* out_A; int32_t* out_acc; double* out_nlp; double* out_E;
+};
+
+// Fixed-order Σ f(i) for i < n over the 256 threads of the block.
+template <typename F>
+__device__ inline double block_sum256(int n, F f, double* sh) {
+  const int t = threadIdx.x;
+  double s = 0.0;
+  for (int i = t; i < n; i += 256) s += f(i);
+  sh[t] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (t < w) sh[t] += sh[t + w];
+    __syncthreads();
+  }
+  const double r = sh[0];
+  __syncthreads();
+  return r;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_hmc_accept(HmcAcceptArgs<T> a) {
+  __shared__ double sh[256];
+  const int DK = a.D * a.K;
+  const bool moved = a.n_iter > 0;
+  // current state: computed at the call's first step, carried afterwards
+  double ll0, sW0, sb0;
+  if (a.first) {
+    ll0 = block_sum256(a.nRB, [&](int i) { return a.ll0_part[i]; }, sh);
+    sW0 = a.logistic ? block_sum256(DK, [&](int i) { const double v = (double)a.W[i]; return v * v; }, sh) : 0.0;
+    sb0 = a.logistic ? block_sum256(a.K, [&](int i) { const double v = (double)a.b[i]; return v * v; }, sh) : 0.0;
+  } else {
+    ll0 = a.st->ll; sW0 = a.st->sW; sb0 = a.st->sb;
+  }
+  const double S0W = block_sum256(a.nDB, [&](int i) { return a.kin0_part[i]; }, sh);
+  double ll1 = ll0, sW1 = sW0, sb1 = sb0, S1W = 0.0, S1b = 0.0;
+  if (moved) {
+    ll1 = block_sum256(a.nRB, [&](int i) { return a.ll1_part[i]; }, sh);
+    if (a.logistic) {
+      sW1 = block_sum256(DK, [&](int i) { const double v = (double)a.Wn[i]; return v * v; }, sh);
+      sb1 = block_sum256(a.K, [&](int i) { const double v = (double)a.bn[i]; return v * v; }, sh);
+    }
+    S1W = block_sum256(DK, [&](int i) { const double v = (double)a.pW[i]; return v * v; }, sh);
+    S1b = block_sum256(a.K, [&](int i) { const double v = (double)a.pb[i]; return v * v; }, sh);
+  }
+  if (threadIdx.x == 0) {
+    auto nlp = [&](double ll, double sW, double sb) {
+      double lp = a.log_prior;                                   // softmax.py:22-30 (constant)
+      if (a.logistic) lp = (((0.0 + a.lpc0) - a.half_alpha * sW) + a.lpc1) - a.half_alpha * sb;   // logistic.py:15-21
+      return a.neg_inv_n * (ll + lp);
+    };
+    const double K0 = (0.0 + 0.5 * S0W) + 0.5 * a.kin0_part[a.nDB];
+    const double nlp0 = nlp(ll0, sW0, sb0);
+    const double Ecur = nlp0 + K0;
+    double Enew = Ecur, A = 1.0;
+    if (moved) {
+      const double K1 = (0.0 + 0.5 * S1W) + 0.5 * S1b;           // ½Σ(−p)² = ½Σp² (hmc.py:55-56)
+      Enew = nlp(ll1, sW1, sb1) + K1;
+      const double x = exp(Ecur - Enew);
+      A = (x < 1.0) ? x : 1.0;                                   // Python min(1, x): NaN → 1
+    }
+    const int acc = a.u < A;
+    a.out_A[0] = A;
+    a.out_acc[0] = acc;
+    if (a.out_E) { a.out_E[0] = Ecur; a.out_E[1] = Enew; }
+    HmcState s;
+    if (acc && moved) { s.ll = ll1; s.sW = sW1; s.sb = sb1; }
+    else { s.ll = ll0; s.sW = sW0; s.sb = sb0; }
+    *a.st = s;
+    a.out_nlp[0] = (acc && moved) ? nlp(ll1, sW1, sb1) : nlp0;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_hmc_commit(int DK, int K, const int32_t* acc, const T* Wn, const T* bn,
+                                                    T* W, T* b, T* trace) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const bool take = *acc != 0;
+  if (i < DK) {
+    T v = W[i];
+    if (take) { v = Wn[i]; W[i] = v; }
+    if (trace) trace[i] = v;
+  } else if (i < DK + K) {
+    T v = b[i - DK];
+    if (take) { v = bn[i - DK]; b[i - DK] = v; }
+    if (trace) trace[i] = v;
+  }
+}
+
+template <typename T>
+int hmc_run_t(hmcx_ctx* ctx, const hmcx_hmc_args* s) {
+  const int B = s->B, D = s->D, K = s->K, DK = D * K, P = DK + K;
+  const bool logistic = s->model == HMCX_MODEL_LOGISTIC;
+  const int link = logistic ? LINK_SIGMOID : LINK_SOFTMAX;
+  const Tiling t = make_tiling(B, D, K, 1);
+  Workspace ws(ctx);
+  T *Wn, *bn, *pW, *pb, *diff, *csp;
+  double *kin0, *ll0p, *ll1p;
+  HmcState* st;
+  do {
+    ws.reset();
+    Wn = ws.take<T>(DK); bn = ws.take<T>(K); pW = ws.take<T>(DK); pb = ws.take<T>(K);
+    diff = ws.take<T>((size_t)B * K); csp = ws.take<T>((size_t)t.nRB * K);
+    kin0 = ws.take<double>(t.nDB + 1); ll0p = ws.take<double>(t.nRB); ll1p = ws.take<double>(t.nRB);
+    st = ws.take<HmcState>(1);
+  } while (ws.retry());
+  if (ws.failed) return HMCX_ENOMEM;
+  begin_call(ctx);
+  int rc;
+  if ((rc = timing_begin(ctx, ctx->stream))) return rc;
+  GraphScope gs(ctx);
+  hipStream_t st_ = ctx->stream;
+  T* W = (T*)s->W;
+  T* b = (T*)s->b;
+  // log-likelihood of the call's starting state (its nlp enters step 0's E_current)
+  {
+    FwdArgs<T> f = fwd_args<T>(s->X, s->Y, W, b, B, D, K, 1, t, FWD_LL);
+    f.link = link;
+    f.ll_part = ll0p;
+    HMCX_HIP(ctx, launch_fwd<T>(f, t, st_));
+  }
+  for (int i = 0; i < s->n_steps; ++i) {
+    const double eps = s->eps[i];
+    const int n = s->n_iter[i];
+    HmcInitArgs<T> ia{};
+    ia.D = D; ia.K = K; ia.P = P; ia.nDB = t.nDB;
+    ia.noise_mode = s->noise_mode; ia.noise = s->noise;
+    ia.noff = s->noise_mode == HMCX_NOISE_BUFFER ? s->noise_off[i] : 0;
+    ia.seed = s->seed; ia.chain = s->chain; ia.step = s->step_base + (uint32_t)i;
+    ia.W = W; ia.b = b; ia.Wn = Wn; ia.bn = bn; ia.pW = pW; ia.pb = pb;
+    ia.mom = s->out_mom ? (T*)s->out_mom + (size_t)i * P : nullptr;
+    ia.kin0_part = kin0;
+    hipLaunchKernelGGL(k_hmc_init<T>, dim3(t.nDB), dim3(256), 0, st_, ia);
+    HMCX_HIP(ctx, hipGetLastError());
+    const int n_eval = n > 0 ? 1 + 2 * n : 0;
+    for (int e = 0; e < n_eval; ++e) {
+      FwdArgs<T> f = fwd_args<T>(s->X, s->Y, Wn, bn, B, D, K, 1, t, FWD_GRAD);
+      f.link = link;
+      f.diff = diff; f.colsum_part = csp;
+      HMCX_HIP(ctx, launch_fwd<T>(f, t, st_));
+      GradArgs<T> g = grad_args<T>((const T*)s->X, diff, csp, B, D, K, 1, t, GRAD_HMC, s->alpha);
+      g.eps = (T)eps; g.half_eps = (T)(0.5 * eps);
+      g.W = Wn; g.b = bn; g.pW = pW; g.pb = pb;
+      int fl;
+      if (e == 0) fl = HMC_HALF_W;                               // hmc.py:47 then it 0, weights
+      else if (e & 1) fl = HMC_KICK_W | HMC_HALF_B;              // after the weights' drift
+      else fl = HMC_KICK_B | (e < 2 * n ? HMC_HALF_W : 0);       // after the bias' drift
+      g.hmc_flags = fl;
+      HMCX_HIP(ctx, launch_grad<T>(g, t, st_));
+    }
+    if (n > 0) {
+      FwdArgs<T> f = fwd_args<T>(s->X, s->Y, Wn, bn, B, D, K, 1, t, FWD_LL);
+      f.link = link;
+      f.ll_part = ll1p;
+      HMCX_HIP(ctx, launch_fwd<T>(f, t, st_));
+    }
+    HmcAcceptArgs<T> aa{};
+    aa.D = D; aa.K = K; aa.nRB = t.nRB; aa.nDB = t.nDB; aa.n_iter = n; aa.first = i == 0; aa.logistic = logistic;
+    aa.u = s->u_accept[i]; aa.neg_inv_n = -1.0 / (double)B; aa.log_prior = s->log_prior;
+    aa.lpc0 = s->lp_const[0]; aa.lpc1 = s->lp_const[1]; aa.half_alpha = 0.5 * s->alpha;
+    aa.kin0_part = kin0; aa.ll0_part = ll0p; aa.ll1_part = ll1p;
+    aa.W = W; aa.b = b; aa.Wn = Wn; aa.bn = bn; aa.pW = pW; aa.pb = pb;
+    aa.st = st;
+    aa.out_A = s->out_A + i; aa.out_acc = s->out_accepted + i; aa.out_nlp = s->out_nlp + i;
+    aa.out_E = s->out_E ? s->out_E + 2 * i : nullptr;
+    hipLaunchKernelGGL(k_hmc_accept<T>, dim3(1), dim3(256), 0, st_, aa);
+    HMCX_HIP(ctx, hipGetLastError());
+    T* tr = s->out_trace ? (T*)s->out_trace + (size_t)i * P : nullptr;
+    if (n > 0 || tr) {
+      hipLaunchKernelGGL(k_hmc_commit<T>, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, st_, DK, K,
+                         s->out_accepted + i, Wn, bn, W, b, tr);
+      HMCX_HIP(ctx, hipGetLastError());
+    }
+  }
+  if ((rc = gs.finish())) return rc;
+  return timing_end(ctx, ctx->stream);
+}
+
 // k_sghmc_init for the chain-batched path: same arithmetic, but the working copy Wwork and the
 // momentum pW are chain-major [C][D][K] (each chain's block contiguous, so every tile of the batched
 // kernels owns whole cache lines); W stays in the caller's [D][C·K] layout.
@@ -861,7 +1149,7 @@ __global__ __launch_bounds__(256) void k_binit(InitArgs<T> a) {
     const size_t wc = ((size_t)c * a.D + d) * K + k;
     double z;
     if (a.noise_mode == HMCX_NOISE_BUFFER) z = a.noise[a.noff[c] + d * K + k];
-    else z = (double)philox_normal(a.seed, a.chain0 + c, a.step, 0u, (uint32_t)(d * K + k));
+    else z = (double)philox_normal_t<T>(a.seed, a.chain0 + c, a.step, 0u, (uint32_t)(d * K + k));
     const T p = (T)z;                                                     // hmc.py:86 N(0,1)
     T q = a.W[w];
     if (take) { q = a.Wwork[wc]; a.W[w] = q; }                            // commit (sghmc.py:37)
@@ -883,7 +1171,7 @@ __global__ __launch_bounds__(256) void k_binit(InitArgs<T> a) {
       const int col = c * K + tid;
       double z;
       if (a.noise_mode == HMCX_NOISE_BUFFER) z = a.noise[a.noff[c] + a.D * K + tid];
-      else z = (double)philox_normal(a.seed, a.chain0 + c, a.step, 0u, (uint32_t)(a.D * K + tid));
+      else z = (double)philox_normal_t<T>(a.seed, a.chain0 + c, a.step, 0u, (uint32_t)(a.D * K + tid));
       const T p = (T)z;
       T q = a.b[col];
       if (take) { q = a.bwork[col]; a.b[col] = q; }
@@ -1066,14 +1354,9 @@ int sghmc_batch_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
   return timing_end(ctx, ctx->stream);
 }
 
-static bool persist_v1() {
-  static const bool v1 = getenv("HMCX_PERSIST_V1") && getenv("HMCX_PERSIST_V1")[0] == '1';
-  return v1;
-}
-
 // True when sghmc_run_t serves this call with k_sghmc_p2, which writes out_trace itself.
 bool sghmc_p2_selected(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
-  if (s->C != 1 || ctx->sghmc_path == 1 || persist_v1()) return false;
+  if (s->C != 1 || ctx->sghmc_path == 1) return false;
   const size_t ts = s->dtype == HMCX_F64 ? sizeof(double) : sizeof(float);
   return plan_p2(s->B, s->D, s->K, ts, ctx->num_cus, ctx->lds_max).ok;
 }
@@ -1081,13 +1364,9 @@ bool sghmc_p2_selected(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
 template <typename T>
 int sghmc_run_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
   const int B = s->B, D = s->D, K = s->K, C = s->C, N = C * K;
-  if (C == 1 && ctx->sghmc_path != 1) {   // single chain: persistent kernel
-    if (!persist_v1()) {                  // hmcx_persist2.hip (tagged-granule teams)
-      const PersistPlan2 p2 = plan_p2(B, D, K, sizeof(T), ctx->num_cus, ctx->lds_max);
-      if (p2.ok) return sghmc_p2_t<T>(ctx, s, p2);
-    }
-    const PersistPlan pl = plan_persist(B, D, K, sizeof(T), ctx->num_cus, ctx->lds_max);   // hmcx_persist.hip
-    if (pl.ok) return sghmc_persist_t<T>(ctx, s, pl);
+  if (C == 1 && ctx->sghmc_path != 1) {   // single chain: persistent kernel (hmcx_persist2.hip)
+    const PersistPlan2 p2 = plan_p2(B, D, K, sizeof(T), ctx->num_cus, ctx->lds_max);
+    if (p2.ok) return sghmc_p2_t<T>(ctx, s, p2);
     if (ctx->sghmc_path == 2) return set_error(ctx, HMCX_EUNSUPPORTED, "persistent SGHMC: shape not supported");
   } else if (ctx->sghmc_path == 2) {
     return set_error(ctx, HMCX_EUNSUPPORTED, "persistent SGHMC needs C == 1");
@@ -1274,6 +1553,10 @@ template int softmax_predict_t<double>(hmcx_ctx*, const void*, int, int, int, in
                                        int);
 template int sgd_run_t<float>(hmcx_ctx*, const hmcx_sgd_args*);
 template int sgd_run_t<double>(hmcx_ctx*, const hmcx_sgd_args*);
+template int hmc_run_t<float>(hmcx_ctx*, const hmcx_hmc_args*);
+template int hmc_run_t<double>(hmcx_ctx*, const hmcx_hmc_args*);
+template int axpy_t<float>(hmcx_ctx*, int, int64_t, double, const void*, void*);
+template int axpy_t<double>(hmcx_ctx*, int, int64_t, double, const void*, void*);
 template int sumsq_t<float>(hmcx_ctx*, const void*, int64_t, double*);
 template int sumsq_t<double>(hmcx_ctx*, const void*, int64_t, double*);
 template int sghmc_run_t<float>(hmcx_ctx*, const hmcx_sampler_args*);

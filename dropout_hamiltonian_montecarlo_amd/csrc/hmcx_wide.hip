@@ -202,7 +202,7 @@ __global__ __launch_bounds__(WTH) void k_wsoft(WideArgs<T> a) {
 template <typename T>
 __device__ inline double wide_noise(const WideArgs<T>& a, uint32_t e) {
   if (a.noise_mode == HMCX_NOISE_BUFFER) return a.noise[a.noff + e];
-  return (double)philox_normal(a.seed, a.chain, a.step, 0u, e);
+  return (double)philox_normal_t<T>(a.seed, a.chain, a.step, 0u, e);
 }
 
 // ---------------------------------------------------------------- Xᵀ·diff + SGLD update

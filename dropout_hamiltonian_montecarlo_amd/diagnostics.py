@@ -34,46 +34,44 @@ def split_rhat(chains):
 
 
 def _autocov(x):
-    """Autocovariance of x along axis 0 (FFT), biased estimator."""
-    n = x.shape[0]
-    xc = x - x.mean(axis=0)
+    """Autocovariance of x along axis 1 ([m, n, P]; FFT), biased estimator."""
+    n = x.shape[1]
+    xc = x - x.mean(axis=1, keepdims=True)
     nfft = 1 << (2 * n - 1).bit_length()
-    f = np.fft.rfft(xc, n=nfft, axis=0)
-    ac = np.fft.irfft(f * np.conj(f), n=nfft, axis=0)[:n]
+    f = np.fft.rfft(xc, n=nfft, axis=1)
+    ac = np.fft.irfft(f * np.conj(f), n=nfft, axis=1)[:, :n]
     return ac / n
 
 
 def ess(chains):
-    """chains: [C, T, ...] → bulk effective sample size per trailing index (split chains)."""
+    """chains: [C, T, ...] → bulk effective sample size per trailing index (split chains).
+    Vectorised over the trailing indices: one FFT per chain half for all parameters, then Geyer's
+    initial positive / monotone sequence advanced lag pair by lag pair for every parameter at once."""
     x = _split(chains)
     m, n = x.shape[:2]
     flat = x.reshape(m, n, -1)
-    out = np.empty(flat.shape[2])
-    for p in range(flat.shape[2]):
-        acov = np.stack([_autocov(flat[c, :, p]) for c in range(m)])   # [m, n]
-        chain_var = acov[:, 0] * n / (n - 1)
-        W = chain_var.mean()
-        mean_c = flat[:, :, p].mean(axis=1)
-        B_over_n = mean_c.var(ddof=1) if m > 1 else 0.0
-        var_plus = W * (n - 1) / n + B_over_n
-        if var_plus <= 0:
-            out[p] = np.nan
-            continue
-        rho = 1.0 - (W - acov.mean(axis=0)) / var_plus
-        rho[0] = 1.0
-        # Geyer initial positive / monotone sequence over pairs
-        t = 0
-        s = 0.0
-        prev = np.inf
-        while t + 1 < n:
-            pair = rho[t] + rho[t + 1]
-            if pair < 0:
-                break
-            pair = min(pair, prev)
-            s += pair
-            prev = pair
-            t += 2
-        tau = -1.0 + 2.0 * s
-        out[p] = m * n / max(tau, 1.0 / np.log10(m * n + 10))
+    acov = _autocov(flat)                                  # [m, n, P]
+    chain_var = acov[:, 0, :] * n / (n - 1)
+    W = chain_var.mean(axis=0)
+    B_over_n = flat.mean(axis=1).var(axis=0, ddof=1) if m > 1 else np.zeros(flat.shape[2])
+    var_plus = W * (n - 1) / n + B_over_n
+    ok = var_plus > 0
+    with np.errstate(divide='ignore', invalid='ignore'):
+        rho = 1.0 - (W[None, :] - acov.mean(axis=0)) / var_plus[None, :]   # [n, P]
+    rho[0] = 1.0
+    s = np.zeros(flat.shape[2])
+    prev = np.full(flat.shape[2], np.inf)
+    live = ok.copy()
+    for t in range(0, n - 1, 2):
+        pair = rho[t] + rho[t + 1]
+        live &= pair >= 0
+        if not live.any():
+            break
+        pair = np.minimum(pair, prev)
+        s = np.where(live, s + pair, s)
+        prev = np.where(live, pair, prev)
+    tau = -1.0 + 2.0 * s
+    out = m * n / np.maximum(tau, 1.0 / np.log10(m * n + 10))
+    out = np.where(ok, out, np.nan)
     shape = x.shape[2:]
     return out.reshape(shape) if shape else out[0]

@@ -6,9 +6,16 @@ MH accept min(1, exp(E_cur − E_new)).  sample (hmc.py:90-119) draws one discar
 first (hmc.py:93), runs burn-in, updates DualAveragingStepSize once and prints it (the value
 is not used, hmc.py:101-102), then samples.
 
-For the MVN model (config 1) every step of a burn-in / sampling phase runs in ONE device
-launch (hmcx_hmc_mvn_run, one thread per chain).  Other libhmcx models run the reference's
-loop with device gradients (model.grad → libhmcx kernels).
+Device paths:
+
+* MVN model (config 1): every step of a burn-in / sampling phase runs in ONE device launch
+  (hmcx_hmc_mvn_run, one thread per chain);
+* softmax (CPU prior) and logistic models: a burn-in / sampling phase is ONE hmcx_hmc_run call —
+  momentum, every kick/drift (fused into the gradient kernels' epilogues), the energies, the MH
+  accept and the commit run on the device; the host only draws the schedule (path lengths, accept
+  uniforms and, in noise='numpy' mode, the momenta) in the reference's order;
+* other libhmcx models (the MLP): the reference's loop with device gradients (model.grad) and the
+  leapfrog arithmetic / kinetic energies as libhmcx calls (hmcx_axpy, hmcx_sumsq).
 """
 import sys
 from copy import deepcopy
@@ -56,7 +63,7 @@ class hmc:
                 L = np.ceil(2 * np.random.rand() * self.path_length / self.step_size)  # :46
                 u[s] = np.random.rand()                                        # :61
             else:
-                noise[s] = nat.philox_normals(self.seed, self.chain, g, 0, 0, dim)
+                noise[s] = nat.philox_normals(self.seed, self.chain, g, 0, 0, dim, dtype="f64")
                 L = np.ceil(2 * nat.philox_uniforms(self.seed, self.chain, g, nat.SLOT_PATH, 1)[0]
                             * self.path_length / self.step_size)
                 u[s] = nat.philox_uniforms(self.seed, self.chain, g, nat.SLOT_ACCEPT, 1)[0]
@@ -74,7 +81,9 @@ class hmc:
         a.eps = eps.ctypes.data_as(nat.c_dblp)
         a.n_iter = n_iter.ctypes.data_as(nat.c_i32p)
         a.u_accept = u.ctypes.data_as(nat.c_dblp)
-        a.noise_mode = nat.NOISE_BUFFER if self.noise == 'numpy' else nat.NOISE_PHILOX
+        # both modes hand the device the host-drawn momenta (philox: the f64 Philox stream's host twin),
+        # so the returned momentums are exactly the ones used (dim = 2: nothing to save on the device)
+        a.noise_mode = nat.NOISE_BUFFER
         a.noise = ptr(noise_d)
         a.noise_off = noff.ctypes.data_as(nat.c_i64p)
         a.seed, a.chain0, a.step_base = self.seed, self.chain, self.global_step & 0xFFFFFFFF
@@ -99,7 +108,121 @@ class hmc:
         step_size_tuning = DualAveragingStepSize(self.step_size)
         if self.model._hmcx_model == 'mvn_gaussian':
             return self._sample_fused(niter, nburn, burnin, rng, step_size_tuning)
+        if self._linear_fused():
+            return self._sample_linear(niter, nburn, burnin, rng, step_size_tuning, args)
         return self._sample_generic(niter, nburn, burnin, rng, step_size_tuning, args)
+
+    # ------------------------------------------------------------------ softmax / logistic fused path
+    def _linear_fused(self):
+        m = self.model
+        return (m._hmcx_model in ('softmax', 'logistic') and getattr(m, 'prior', 'cpu') == 'cpu'
+                and list(self.start.keys()) == ['weights', 'bias'])
+
+    def _linear_data(self, args):
+        m = self.model
+        X, y = m._xy(args)
+        return X.contiguous(), y.contiguous()
+
+    def _linear_run(self, W, b, data, n_steps, rng, record):
+        """n_steps HMC steps in one hmcx_hmc_run call.  Host work: the schedule in the reference's
+        draw order (hmc.py:41 momentum from rng, :46 path length and :61 accept uniform from the
+        global np.random) or, with noise='philox', path lengths / uniforms from the Philox twin."""
+        m = self.model
+        Xd, Yd = data
+        D, K = W.shape
+        P = D * K + K
+        eps = np.full(n_steps, self.step_size, dtype=np.float64)
+        n_iter = np.empty(n_steps, dtype=np.int32)
+        u = np.empty(n_steps, dtype=np.float64)
+        noise = np.empty((n_steps, P), dtype=np.float64) if self.noise == 'numpy' else None
+        for s in range(n_steps):
+            g = (self.global_step + s) & 0xFFFFFFFF
+            if self.noise == 'numpy':
+                mom = self.draw_momentum(rng)                                  # hmc.py:41
+                noise[s, :D * K] = mom['weights'].reshape(-1)
+                noise[s, D * K:] = mom['bias'].reshape(-1)
+                L = np.ceil(2 * np.random.rand() * self.path_length / self.step_size)   # hmc.py:46
+                n_iter[s] = _n_iter(L)
+                u[s] = np.random.rand()                                        # hmc.py:61
+            else:
+                L = np.ceil(2 * nat.philox_uniforms(self.seed, self.chain, g, nat.SLOT_PATH, 1)[0]
+                            * self.path_length / self.step_size)
+                n_iter[s] = _n_iter(L)
+                u[s] = nat.philox_uniforms(self.seed, self.chain, g, nat.SLOT_ACCEPT, 1)[0]
+        dev = m.device
+        noise_d = torch.from_numpy(noise.ravel()).to(dev) if noise is not None else None
+        noff = np.arange(n_steps, dtype=np.int64) * P
+        out_f = torch.empty(4 * n_steps, dtype=torch.float64, device=dev)        # A, nlp, E (2)
+        out_acc = torch.empty(n_steps, dtype=torch.int32, device=dev)
+        tr = torch.empty((n_steps, P), dtype=m.dtype, device=dev) if record else None
+        mo = torch.empty((n_steps, P), dtype=m.dtype, device=dev) if (record and noise is None) else None
+        a = nat.HmcArgs()
+        a.dtype, a.model = m.code, nat.MODEL_LOGISTIC if m._hmcx_model == 'logistic' else nat.MODEL_SOFTMAX
+        a.B, a.D, a.K, a.n_steps = Xd.shape[0], D, K, n_steps
+        a.alpha = m.alpha
+        if m._hmcx_model == 'logistic':                                        # logistic.py:15-21
+            for i, var in enumerate(('weights', 'bias')):
+                dim = int(np.prod(np.shape(self.start[var])))
+                a.lp_const[i] = dim * 0.5 * np.log(m.hyper['alpha'] / (2 * np.pi))
+        else:
+            a.log_prior = m.log_prior_const([np.shape(self.start[v]) for v in self.start])
+        a.X, a.Y = ptr(Xd), ptr(Yd)
+        a.eps = eps.ctypes.data_as(nat.c_dblp)
+        a.n_iter = n_iter.ctypes.data_as(nat.c_i32p)
+        a.u_accept = u.ctypes.data_as(nat.c_dblp)
+        a.noise_mode = nat.NOISE_BUFFER if noise is not None else nat.NOISE_PHILOX
+        a.noise = ptr(noise_d)
+        a.noise_off = noff.ctypes.data_as(nat.c_i64p)
+        a.seed, a.chain, a.step_base = self.seed, self.chain, self.global_step & 0xFFFFFFFF
+        a.W, a.b = ptr(W), ptr(b)
+        a.out_A, a.out_nlp, a.out_E = ptr(out_f[:n_steps]), ptr(out_f[n_steps:2 * n_steps]), ptr(out_f[2 * n_steps:])
+        a.out_accepted = ptr(out_acc)
+        a.out_trace, a.out_mom = ptr(tr), ptr(mo)
+        ctx = nat.context(dev)
+        ctx.check(ctx.lib.hmcx_hmc_run(ctx.h, a), "hmcx_hmc_run")
+        self.global_step += n_steps
+        f = out_f.cpu().numpy()
+        A, nlp = f[:n_steps], f[n_steps:2 * n_steps]
+        acc = out_acc.cpu().numpy().astype(bool)
+        if self.trace is not None:
+            self.trace.extend({'L': float(n + 1), 'A': float(A[s]), 'accepted': bool(acc[s]), 'eps': self.step_size}
+                              for s, n in enumerate(n_iter))
+        trace = tr.cpu().numpy().astype(np.float64) if tr is not None else None
+        mom = (noise if noise is not None else mo.cpu().numpy().astype(np.float64)) if record else None
+        return A, acc, nlp, trace, mom
+
+    def _split(self, flat):
+        D, K = np.shape(self.start['weights'])
+        return {'weights': flat[:D * K].reshape(D, K).copy(), 'bias': flat[D * K:].reshape(np.shape(self.start['bias'])).copy()}
+
+    def _sample_linear(self, niter, nburn, burnin, rng, tuning, args):
+        m = self.model
+        data = self._linear_data(args)
+        W = m._dev(self.start['weights']).clone()
+        b = m._dev(np.reshape(self.start['bias'], -1)).clone()
+        p_accept = None
+        if nburn > 0:
+            A, _, nlp, _, _ = self._linear_run(W, b, data, nburn, rng, False)
+            for i in range(nburn):
+                if self.verbose is not None and (i % (burnin / 10) == 0):
+                    print('loss: {0:.4f}'.format(nlp[i]), file=self.out)
+            p_accept = A[-1]
+        _, avg_step_size = tuning.update(p_accept)
+        print('adapted step size : ', avg_step_size, file=self.out)
+        before = np.concatenate([W.cpu().numpy().reshape(-1), b.cpu().numpy().reshape(-1)]).astype(np.float64)
+        if niter == 0:
+            return {v: np.zeros((0,) + np.shape(self.start[v])) for v in self.start}, np.zeros(0), [], []
+        A, acc, nlp, tr, mom = self._linear_run(W, b, data, niter, rng, True)
+        positions = [[self._split(before if i == 0 else tr[i - 1])] for i in range(niter)]
+        momentums = [[self._split(mom[i])] for i in range(niter)]
+        for i in range(niter):
+            if self.verbose and (i % (niter / 10) == 0):
+                print('loss: {0:.4f}'.format(nlp[i]), file=self.out)
+        D, K = np.shape(self.start['weights'])
+        posterior = {'weights': tr[:, :D * K].reshape((niter,) + np.shape(self.start['weights'])),
+                     'bias': tr[:, D * K:].reshape((niter,) + np.shape(self.start['bias']))}
+        self.last_state = {'weights': W, 'bias': b}
+        return posterior, nlp, positions, momentums
 
     def _sample_fused(self, niter, nburn, burnin, rng, tuning):
         x = torch.as_tensor(np.asarray(self.start['x'], dtype=np.float64)).to(self.model.device).contiguous().clone()
@@ -122,18 +245,27 @@ class hmc:
         return {'x': tr}, nlp, positions, momentums
 
     # ------------------------------------------------------------------ generic path (device grads)
-    def _K(self, p):
+    def _K(self, p):                                                         # hmc.py:74-79
         K = 0
+        ctx = nat.context(self.model.device)
         for var in p.keys():
-            K += 0.5 * float(torch.sum(p[var] * p[var]))
+            v = p[var].reshape(-1)
+            ss = torch.empty(1, dtype=torch.float64, device=v.device)
+            ctx.check(ctx.lib.hmcx_sumsq(ctx.h, self.model.code, ptr(v), v.numel(), ptr(ss)), "hmcx_sumsq")
+            K += 0.5 * ss.item()
         return K
+
+    def _axpy(self, mode, a, x, y):
+        """y −= a·x (mode 0) / y += a·x (mode 1) on the device (hmcx_axpy)."""
+        ctx = nat.context(self.model.device)
+        ctx.check(ctx.lib.hmcx_axpy(ctx.h, self.model.code, mode, y.numel(), float(a), ptr(x), ptr(y)), "hmcx_axpy")
 
     def step(self, state, momentum, rng, **args):                           # hmc.py:39-64
         m = self.model
         dev, dt = m.device, m.dtype
-        q = {k: torch.as_tensor(np.asarray(v) if not isinstance(v, torch.Tensor) else v).to(dev, dt)
+        q = {k: torch.as_tensor(np.asarray(v) if not isinstance(v, torch.Tensor) else v).to(dev, dt).contiguous()
              for k, v in state.items()}
-        p = {k: torch.as_tensor(v).to(dev, dt) for k, v in self.draw_momentum(rng).items()}
+        p = {k: torch.as_tensor(v).to(dev, dt).contiguous() for k, v in self.draw_momentum(rng).items()}
         q_new = {k: v.clone() for k, v in q.items()}
         p_new = {k: v.clone() for k, v in p.items()}
         positions, momentums = [deepcopy(state)], [{k: v.cpu().numpy() for k, v in p.items()}]
@@ -142,12 +274,12 @@ class hmc:
         grad_q = m.grad(q, **args)
         for _ in range(_n_iter(path_length)):
             for var in self.start.keys():
-                p_new[var] -= (0.5 * epsilon) * grad_q[var]
-                q_new[var] += epsilon * p_new[var]
+                self._axpy(0, 0.5 * epsilon, grad_q[var], p_new[var])          # hmc.py:50
+                self._axpy(1, epsilon, p_new[var], q_new[var])                 # hmc.py:51
                 grad_q = m.grad(q_new, **args)
-                p_new[var] -= epsilon * grad_q[var]
+                self._axpy(0, epsilon, grad_q[var], p_new[var])                # hmc.py:53
         for var in self.start.keys():
-            p_new[var] = -p_new[var]
+            self._axpy(0, 2.0, p_new[var], p_new[var])                         # hmc.py:55-56: p − 2p = −p
         E_new = m.negative_log_posterior(q_new, **args) + self._K(p_new)
         E_cur = m.negative_log_posterior(q, **args) + self._K(p)
         acceptprob = min(1, np.exp(E_cur - E_new))

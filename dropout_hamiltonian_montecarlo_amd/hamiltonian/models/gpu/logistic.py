@@ -77,6 +77,9 @@ class logistic:
         return {'weights': gW, 'bias': gb}
 
     def net(self, par, **args):                                           # logistic.py:43-51
+        return self._net_device(par, **args)
+
+    def _net_device(self, par, **args):
         X, _ = _batch(args)
         X = self._x(X)
         W, b = self._par(par)
@@ -113,7 +116,7 @@ class logistic:
         n = (X.shape[0] // batchsize) * batchsize
         if n == 0:
             return np.asarray([]).flatten()
-        yhat = self.net(par, X_train=X[:n]).cpu().numpy()
+        yhat = self._net_device(par, X_train=X[:n]).cpu().numpy()
         if prob:
             return yhat.flatten()
         return (yhat > 0.5).astype(int).flatten()

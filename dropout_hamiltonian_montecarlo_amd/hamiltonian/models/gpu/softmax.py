@@ -101,9 +101,12 @@ class softmax:
                 dim = int(np.prod(tuple(par[var].shape)))
                 K -= 0.5 * dim * np.log(2 * np.pi) - 0.5 * dim * np.log(self.hyper['alpha'])
             return K
+        ctx = context(self.device)
         for var in par.keys():                                            # gpu/softmax.py:29-39
-            v = self._dev(par[var])
-            K -= 0.5 * self.alpha * float(torch.sum(v * v)) / v.numel()
+            v = self._dev(par[var]).reshape(-1)
+            ss = torch.empty(1, dtype=torch.float64, device=self.device)   # Σθ² on the device (hmcx_sumsq)
+            ctx.check(ctx.lib.hmcx_sumsq(ctx.h, self.code, ptr(v), v.numel(), ptr(ss)), "hmcx_sumsq")
+            K -= 0.5 * self.alpha * ss.item() / v.numel()
         return K
 
     def log_prior_const(self, shapes):
@@ -125,6 +128,9 @@ class softmax:
         return self.negative_log_posterior(par, **args)
 
     def net(self, par, X):                                                # softmax.py:38-43
+        return self._net_device(par, X)
+
+    def _net_device(self, par, X):
         X = self._dev(X)
         W, b = self._par(par)
         B, D = X.shape
@@ -141,10 +147,10 @@ class softmax:
         probabilities flattened to 1-D (its ``results.reshape(-1,)``)."""
         if batchsize:
             n = (X.shape[0] // batchsize) * batchsize
-            yhat = self.net(par, X[:n])
+            yhat = self._net_device(par, X[:n])
             out = yhat if prob else yhat.argmax(dim=1)
             return out.cpu().numpy().reshape(-1)
-        yhat = self.net(par, X)
+        yhat = self._net_device(par, X)
         out = yhat if prob else yhat.argmax(dim=1)
         return out.cpu().numpy()
 
@@ -161,7 +167,7 @@ class softmax:
             Z = torch.bernoulli(torch.full_like(X, p))
         else:
             Z = self._dev(Z)
-        yhat = self.net(par, X * Z)
+        yhat = self._net_device(par, X * Z)
         out = (yhat if prob else yhat.argmax(dim=1)).cpu().numpy()
         if batchsize:
             out = out.reshape(-1, out.shape[-1]) if prob else out.reshape(-1, batchsize)

@@ -62,9 +62,14 @@ int hmcx_get_timing(hmcx_ctx* ctx, double* kernel_ms, long long* launches);
 /* Philox4x32-10 uniforms in [0,1), bit-identical to the device generator (host function). */
 void hmcx_philox_uniforms(uint64_t seed, uint32_t chain, uint32_t step, uint32_t slot,
                           uint32_t n, double* out /* host [n] */);
-/* Philox standard normals for slot/element range (host function; used by tests). */
+/* Philox standard normals for slot/element range (host function; used by tests): the float32
+ * Box–Muller stream of the f32 chains. */
 void hmcx_philox_normals(uint64_t seed, uint32_t chain, uint32_t step, uint32_t slot,
                          uint32_t e0, uint32_t n, double* out /* host [n] */);
+/* The float64 stream of the f64 chains (53-bit uniforms, double Box–Muller; host function).
+ * Replaces the f64 draws of cpu/sghmc.py:21,31 and cpu/sgld.py:45 in noise='philox' mode. */
+void hmcx_philox_normals_f64(uint64_t seed, uint32_t chain, uint32_t step, uint32_t slot,
+                             uint32_t e0, uint32_t n, double* out /* host [n] */);
 
 /* ------------------------------------------------------------------ softmax model
  * Replaces hamiltonian/models/cpu/softmax.py:45-61 (grad) and gpu/softmax.py:53-69.
@@ -204,6 +209,56 @@ typedef struct hmcx_hmc_mvn_args {
   double* out_trace;       /* device [n_steps][C][dim] or NULL */
 } hmcx_hmc_mvn_args;
 int hmcx_hmc_mvn_run(hmcx_ctx* ctx, const hmcx_hmc_mvn_args* a);
+/* Per-call MVN surface, mvn_gaussian.py:14-31: for C points x [C][dim], g = (x − μ)·prec (grad) and
+ * nlp = 0.5·(nlp_const + (x−μ)ᵀ·prec·(x−μ)) (negative_log_posterior); g or nlp may be NULL. */
+int hmcx_mvn_eval(hmcx_ctx* ctx, int dim, int C, const double* mu, const double* prec, double nlp_const,
+                  const double* x, double* g, double* nlp);
+
+/* ------------------------------------------------------------------ full-batch HMC, linear models
+ * Replaces cpu/hmc.py:39-64 (step) with the softmax (models/cpu/softmax.py) or logistic
+ * (models/cpu/logistic.py) model, one chain: per step, momentum p ~ N(0,1) (hmc.py:41, draw order
+ * weights then bias), then for it < n_iter, per var v in (weights, bias):
+ *   p_v −= (½ε)·g_v;  q_v += ε·p_v;  g = grad(q);  p_v −= ε·g_v          (hmc.py:49-54)
+ * with g = grad(q0) before the loop (hmc.py:47), p ← −p, and the MH accept
+ * A = min(1, exp(E_cur − E_new)), E = nlp + ½Σp² (hmc.py:56-79; nlp = −(ll + log_prior)/N).
+ * The whole schedule runs on the device: per gradient one k_fwd + one k_grad launch with the
+ * kick/drift fused into the gradient epilogue; energies, accept and commit in step kernels.
+ * log_prior: softmax — the constant `log_prior` (softmax.py:22-30); logistic — Σ_var
+ * (lp_const[var] − ½·alpha·Σθ_var²) with Σθ² on the device (logistic.py:15-21).
+ * X [N][D] (full batch: B = N rows), Y [N][K] one-hot (softmax) or [N] 0/1 (logistic, K = 1).
+ * Noise as hmcx_sampler_args (BUFFER: noise_off[s], P = D·K + K momentum normals per step). */
+typedef struct hmcx_hmc_args {
+  int dtype;
+  int model;               /* HMCX_MODEL_SOFTMAX or HMCX_MODEL_LOGISTIC                  */
+  int B, D, K, n_steps;    /* B = N (full batch)                                        */
+  double alpha;
+  double log_prior;        /* softmax: constant log prior                               */
+  double lp_const[2];      /* logistic: dim·½·log(alpha/2π) of weights, bias            */
+  const void* X;
+  const void* Y;
+  const double* eps;       /* host [n_steps]                                            */
+  const int32_t* n_iter;   /* host [n_steps]  max(0, L − 1)                            */
+  const double* u_accept;  /* host [n_steps]                                            */
+  int noise_mode;
+  const double* noise;     /* device, BUFFER                                            */
+  const int64_t* noise_off;/* host [n_steps], BUFFER                                    */
+  uint64_t seed;
+  uint32_t chain, step_base;
+  void* W;                 /* device [D][K] state, updated in place                     */
+  void* b;                 /* device [K]                                                */
+  double* out_A;           /* device [n_steps]                                          */
+  int32_t* out_accepted;   /* device [n_steps]                                          */
+  double* out_nlp;         /* device [n_steps]: nlp of the state kept after step s     */
+  double* out_E;           /* device [n_steps*2] (E_current, E_new) or NULL             */
+  void* out_trace;         /* device [n_steps][D*K+K] (dtype) or NULL: state after s    */
+  void* out_mom;           /* device [n_steps][D*K+K] (dtype) or NULL: momentum drawn   */
+} hmcx_hmc_args;
+int hmcx_hmc_run(hmcx_ctx* ctx, const hmcx_hmc_args* a);
+
+/* Leapfrog arithmetic on device vectors of n elements (dtype), for hmc.step on models without a
+ * fused entry (the MLP): mode 0  y −= a·x;  mode 1  y += a·x  (hmc.py:50-53, p −= ε·g, q += ε·p).
+ * hmcx_sumsq gives the kinetic energy's Σp² (hmc.py:74-79). */
+int hmcx_axpy(hmcx_ctx* ctx, int dtype, int mode, int64_t n, double a, const void* x, void* y);
 
 /* ------------------------------------------------------------------ MLP model (config 3)
  * Replaces hamiltonian/models/gpu/mlp.py:19-31 (MyNetwork: l1 -> relu(dropout) -> l2 ->

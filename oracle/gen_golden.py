@@ -3,7 +3,8 @@
 REFERENCE's own NumPy code (/root/reference, read-only) in a child process.
 
 Run once in the build container:  ``python oracle/gen_golden.py`` (``--logistic``: only the
-logistic-model / momentum-SGD fixtures of section 4)
+logistic-model / momentum-SGD fixtures of section 4; ``--notebook``: only the notebook-harness
+fixture of section 5)
 (the reference does not exist on the GPU box; the committed .npz files travel instead).
 
 The reference needs a four-line import shim on Python 3.10 / NumPy 2:
@@ -219,6 +220,69 @@ print('ok')
 '''
 
 
+# ---- (5) the notebook harness (benchmarks/1.-Simulated_data.ipynb cells 2, 6, 10) through the
+# reference's own import paths hamiltonian.models.cpu.logistic / inference.cpu.sgd / inference.cpu.hmc.
+CHILD_NOTEBOOK = r'''
+import sys, types, collections, collections.abc, io, contextlib, importlib.util
+sys.dont_write_bytecode = True
+sys.path.insert(0, '/root/reference')
+collections.Iterable = collections.abc.Iterable
+sys.modules['h5py'] = types.ModuleType('h5py')
+import numpy as np
+np.int = int
+np.float = float
+spec = importlib.util.spec_from_file_location('golden_inputs', sys.argv[1])
+gi = importlib.util.module_from_spec(spec); spec.loader.exec_module(gi)
+OUT = sys.argv[2]
+import hamiltonian.models.cpu.logistic as base_model_cpu
+import hamiltonian.inference.cpu.sgd as inference_cpu
+import hamiltonian.inference.cpu.hmc as sampler_cpu
+
+X_train, X_test, y_train, y_test = gi.notebook_data()
+c = gi.NOTEBOOK['sgd']
+D = X_train.shape[1]
+np.random.seed(c['start_seed'])
+start_p = {'weights': 2 * np.random.random((D, 1)), 'bias': 2 * np.random.random(1)}
+hyper_p = {'alpha': c['alpha']}
+model_cpu = base_model_cpu.logistic(hyper_p)
+optim_cpu = inference_cpu.sgd(model_cpu, {k: v.copy() for k, v in start_p.items()}, step_size=c['eta'])
+with contextlib.redirect_stdout(io.StringIO()), contextlib.redirect_stderr(io.StringIO()):
+    par_cpu, loss = optim_cpu.fit(epochs=c['epochs'], batch_size=c['batch_size'], gamma=c['gamma'],
+                                  X_train=X_train, y_train=y_train, verbose=True)
+y_pred = model_cpu.predict(par_cpu, X_test, batchsize=c['batch_size'])
+
+h = gi.NOTEBOOK['hmc']
+class rec(sampler_cpu.hmc):
+    def step(self, state, momentum, rng, **args):
+        self._calls = 0
+        out = sampler_cpu.hmc.step(self, state, momentum, rng, **args)
+        n_iter = (self._calls - 1) // len(self.start)
+        accepted = any(out[0][v] is not state[v] for v in state)
+        self.rec.append((n_iter, float(out[4]), int(accepted)))
+        return out
+class counting(base_model_cpu.logistic):
+    def grad(self, par, **args):
+        self.owner._calls += 1
+        return super().grad(par, **args)
+m = counting(hyper_p)
+s = rec(m, start_p, path_length=h['path_length'], step_size=h['step_size'])
+m.owner = s; s.rec = []
+np.random.seed(h['np_seed'])
+with contextlib.redirect_stdout(io.StringIO()), contextlib.redirect_stderr(io.StringIO()):
+    samples, hloss, positions, momentums = s.sample(h['niter'], h['burnin'], np.random.RandomState(h['rng_seed']),
+                                                    X_train=X_train, y_train=y_train)
+par_mean = {var: np.mean(samples[var], axis=0).reshape(start_p[var].shape) for var in samples.keys()}
+np.savez_compressed(OUT + '/notebook_simulated.npz', X_train=X_train, y_train=y_train, X_test=X_test, y_test=y_test,
+                    start_weights=start_p['weights'], start_bias=start_p['bias'],
+                    sgd_weights=par_cpu['weights'], sgd_bias=par_cpu['bias'], sgd_loss=loss, sgd_pred=y_pred,
+                    hmc_weights=samples['weights'], hmc_bias=samples['bias'], hmc_loss=hloss,
+                    hmc_trace=np.array(s.rec, dtype=np.float64),
+                    hmc_mom0=np.array([np.concatenate([p[0]['weights'].ravel(), p[0]['bias'].ravel()]) for p in momentums]),
+                    hmc_pred=model_cpu.predict(par_mean, X_test, batchsize=c['batch_size']))
+print('ok')
+'''
+
+
 def _run_child(code, env):
     r = subprocess.run([sys.executable, '-c', code, os.path.join(REPO, 'oracle', 'inputs.py'), OUT],
                        env=env, capture_output=True, text=True)
@@ -233,6 +297,9 @@ def main():
     env = dict(os.environ, PYTHONDONTWRITEBYTECODE='1', OPENBLAS_NUM_THREADS='1')
     if '--logistic' in sys.argv:            # only the logistic / sgd fixtures (4)
         _run_child(CHILD_LOGISTIC, env)
+        return
+    if '--notebook' in sys.argv:            # only the notebook-harness fixture (5)
+        _run_child(CHILD_NOTEBOOK, env)
         return
     r = subprocess.run([sys.executable, '-c', CHILD, os.path.join(REPO, 'oracle', 'inputs.py'), OUT],
                        env=env, capture_output=True, text=True)

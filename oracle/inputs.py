@@ -81,6 +81,26 @@ SGD_CONFIGS = {
 }
 
 
+# benchmarks/1.-Simulated_data.ipynb, cells 2, 6 and 10 (the reference's one live harness): blobs data,
+# logistic sgd.fit and hmc.sample through the hamiltonian.models.cpu / inference.cpu import paths.
+# Reduced so the reference finishes in seconds: sgd 200 epochs (notebook 1e4); hmc path_length 2e-3,
+# step 1e-4, 40 samples after 10 burn-in (notebook: path 1, step 1e-5 — ≈10⁵ leapfrogs per step).
+NOTEBOOK = dict(centers=[[-5, 0], [5, -1]], n_samples=1000, cluster_std=1, random_state=40, split_state=0,
+                sgd=dict(epochs=200, batch_size=50, eta=1e-5, gamma=0.9, alpha=0.25, start_seed=3),
+                hmc=dict(path_length=2e-3, step_size=1e-4, niter=40, burnin=10, np_seed=4, rng_seed=5))
+
+
+def notebook_data():
+    """Cell 2: make_blobs → standardise → train_test_split (needs scikit-learn)."""
+    from sklearn.datasets import make_blobs
+    from sklearn.model_selection import train_test_split
+    c = NOTEBOOK
+    X, y = make_blobs(n_samples=c['n_samples'], centers=c['centers'], cluster_std=c['cluster_std'],
+                      random_state=c['random_state'])
+    X = (X - X.mean(axis=0)) / X.std(axis=0)
+    return train_test_split(X, y, random_state=c['split_state'])
+
+
 def sgd_problem(c):
     """Dataset and start point of an SGD_CONFIGS entry."""
     if c['model'] == 'logistic':

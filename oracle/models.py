@@ -39,8 +39,9 @@ def _batch(args):
 class softmax:
     """models/cpu/softmax.py:12-100 — softmax regression, float64."""
 
-    def __init__(self, _hyper):
+    def __init__(self, _hyper, prior='cpu'):
         self.hyper = _hyper                                              # :14-15
+        self.prior = prior       # 'gpu': the CuPy file's log_prior (models/gpu/softmax.py:29-39)
 
     def cross_entropy(self, y_linear, y):                                # :17-20
         lse = logsumexp(y_linear, axis=1)
@@ -49,6 +50,11 @@ class softmax:
 
     def log_prior(self, par, **args):                                    # :22-30 (constant in par)
         K = 0
+        if self.prior == 'gpu':                                          # gpu/softmax.py:29-39
+            for var in par.keys():
+                dim = (np.asarray(par[var])).size
+                K -= 0.5 * self.hyper['alpha'] * np.sum(np.square(par[var])) / dim
+            return K
         for var in par.keys():
             dim = (np.array(par[var])).size
             K -= 0.5 * dim * np.log(2 * np.pi) - 0.5 * dim * np.log(self.hyper['alpha'])

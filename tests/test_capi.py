@@ -37,7 +37,7 @@ def test_argument_validation_without_device(nat):
 
 
 _MIRRORS = [("SamplerArgs", "hmcx_sampler_args"), ("SgdArgs", "hmcx_sgd_args"), ("MvnArgs", "hmcx_hmc_mvn_args"),
-            ("MlpParams", "hmcx_mlp_params"), ("MlpSghmcArgs", "hmcx_mlp_sghmc_args")]
+            ("MlpParams", "hmcx_mlp_params"), ("MlpSghmcArgs", "hmcx_mlp_sghmc_args"), ("HmcArgs", "hmcx_hmc_args")]
 
 
 def test_struct_layout_matches_header(nat, tmp_path):
@@ -106,6 +106,40 @@ def test_python_surface_imports():
     assert hasattr(m4, "softmax") and hasattr(m5, "mvn_gaussian")
     assert hasattr(m6, "logistic") and hasattr(m7, "sgd")
     np.testing.assert_array_equal(u.one_hot([2, 0], 3), [[0, 0, 1], [1, 0, 0]])
+
+
+# Every module path the reference's own files import and that exists in the reference tree
+# (benchmarks/1.-Simulated_data.ipynb cells 6, 8, 10; models/cpu/*.py import hamiltonian.models.model;
+# inference/*/sgmcmc subclasses), plus the remaining sampler modules of inference/cpu.
+_REFERENCE_PATHS = {
+    "hamiltonian.models.cpu.logistic": "logistic", "hamiltonian.models.cpu.softmax": "softmax",
+    "hamiltonian.models.cpu.mvn_gaussian": "mvn_gaussian", "hamiltonian.models.gpu.logistic": "logistic",
+    "hamiltonian.models.gpu.softmax": "softmax", "hamiltonian.models.gpu.mlp": "mlp",
+    "hamiltonian.models.gpu.mvn_gaussian": "mvn_gaussian", "hamiltonian.models.model": "model",
+    "hamiltonian.inference.cpu.sgd": "sgd", "hamiltonian.inference.cpu.hmc": "hmc",
+    "hamiltonian.inference.cpu.sgmcmc": "sgmcmc", "hamiltonian.inference.cpu.sghmc": "sghmc",
+    "hamiltonian.inference.cpu.sgld": "sgld", "hamiltonian.inference.cpu.sghmc_multicore": "sghmc_multicore",
+    "hamiltonian.inference.cpu.sgld_multicore": "sgld_multicore", "hamiltonian.inference.gpu.sgd": "sgd",
+    "hamiltonian.inference.gpu.sgmcmc": "sgmcmc", "hamiltonian.inference.gpu.sgld_multicore": "sgld_multicore",
+}
+
+
+def test_reference_import_paths_resolve():
+    """The reference harness's import paths resolve to the libhmcx-backed classes: inference.cpu.X is
+    the same sampler class as inference.gpu.X, models.cpu.X a NumPy-surface subclass of models.gpu.X."""
+    import importlib
+    for path, name in _REFERENCE_PATHS.items():
+        mod = importlib.import_module(path)
+        assert hasattr(mod, name), path
+    import hamiltonian.inference.cpu.hmc as hc
+    import hamiltonian.inference.gpu.hmc as hg
+    import hamiltonian.models.cpu.logistic as lc
+    import hamiltonian.models.gpu.logistic as lg
+    import hamiltonian.models.model as mm
+    assert hc.hmc is hg.hmc and hasattr(hc, "DualAveragingStepSize")
+    assert issubclass(lc.logistic, lg.logistic) and lc.logistic.__name__ == "logistic"
+    assert lc.logistic._hmcx_model == "logistic"
+    assert mm.model().grad(None, None) is None and mm.model().log_p(None, None) is None
 
 
 def test_no_cpu_fallback():
