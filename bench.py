@@ -42,7 +42,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=120)
     ap.add_argument("--dtype", choices=["f64", "f32"], default="f64")
     ap.add_argument("--path", choices=["auto", "kernels", "persistent"], default="auto")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline time budget (0 = skip)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                    help="CPU-baseline time budget per baseline (0 = skip)")
     ap.add_argument("--batched-chains", type=int, default=2048,
                     help="chains per GPU of the secondary chain-batched measurement (0 = skip)")
     ap.add_argument("--mlp-steps", type=int, default=40,
@@ -74,7 +75,8 @@ def cpu_model():
 def cpu_baseline(X, Y, budget_s, threads=None):
     """The oracle (NumPy float64 restatement of the reference SGHMC, bit-exact to it) on host
     cores: bounded sample of the same workload, leapfrogs counted the same way.  threads=None:
-    OpenBLAS default (all cores of the affinity mask); threads=1: one BLAS thread."""
+    OpenBLAS default — on the GPU box that is the job's CPU share for one GPU (the pool sets
+    OMP_NUM_THREADS=16; the affinity mask lists the whole host); threads=1: one BLAS thread."""
     import threadpoolctl
     if threads is None:
         return _cpu_baseline(X, Y, budget_s)
@@ -112,15 +114,18 @@ def _cpu_baseline(X, Y, budget_s):
             "lf_per_s": lf / t_total}
 
 
-def pmc_traffic(dtype, path):
-    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC run of this
-    bench configuration (profiles/pmc_*.json, see tools/gpu_pmc_bench.sh): 2·FETCH_SIZE +
-    WRITE_SIZE (MI355X_MICROARCH.md: FETCH_SIZE counts half of 16-byte streaming reads)."""
-    f = os.path.join(REPO, "profiles", "pmc_r01_%s_%s.json" % (dtype, path))
+def pmc_traffic(dtype, path, leapfrogs_per_launch):
+    """Fabric bytes per launch of the dominant kernel, from the committed rocprofv3 PMC run of the
+    driver's call shape (profiles/pmc_r02_<dtype>_<path>.json, tools/gpu_r02_pmc.sh): 2·FETCH_SIZE +
+    WRITE_SIZE of the timed launches (MI355X_MICROARCH.md: FETCH_SIZE counts half of 16-byte
+    streaming reads) per leapfrog of those launches, times the leapfrogs of this run's launch — the
+    exchange rounds, which carry almost all of the traffic, are per leapfrog."""
+    f = os.path.join(REPO, "profiles", "pmc_r02_%s_%s.json" % (dtype, path))
     if not os.path.exists(f):
         return None
     with open(f) as fh:
-        return json.load(fh).get("traffic_bytes_per_launch")
+        per_lf = json.load(fh).get("traffic_bytes_per_leapfrog")
+    return None if per_lf is None else per_lf * leapfrogs_per_launch
 
 
 def batched_chains(model, X, Y, data, C, n_steps, rank):
@@ -346,9 +351,18 @@ def main():
         pending = h
         done += n
         n_calls += 1
+    t_enq = time.perf_counter()
     lls.append(s._collect(pending).ll)
+    t_col = time.perf_counter()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
+    if os.environ.get("HMCX_BENCH_DEBUG") == "1":
+        print("timed region: last enqueue returned %.1f us, collect %.1f us, sync %.1f us" % (
+            (t_enq - t0) * 1e6, (t_col - t0) * 1e6, (t1 - t0) * 1e6), file=sys.stderr)
+        from dropout_hamiltonian_montecarlo_amd.hamiltonian.inference.gpu import sghmc as _sg
+        m = [x for x in _sg._marks if x[1] >= t0]
+        print("  enqueue phases: " + ", ".join("%s +%.1f" % (n, (t - p) * 1e6) for (n, t), (_, p) in
+                                                zip(m[1:], m[:-1])), file=sys.stderr)
     parallel.barrier()
     elapsed = t1 - t0
     kern_ms, kern_n = model.ctx.get_timing()
@@ -372,11 +386,11 @@ def main():
     mlp_out = None
     if args.mlp_steps > 0:
         lab = np.argmax(Y, axis=1)
-        mlp_out = mlp_measure(X, lab, args.mlp_steps, rank, args.cpu_seconds / 2 if world == 1 and rank == 0 else 0)
+        mlp_out = mlp_measure(X, lab, args.mlp_steps, rank, args.cpu_seconds if world == 1 and rank == 0 else 0)
         parallel.barrier()
     v_out = None
     if args.sgld_steps > 0:
-        v_out = plantvillage_measure(args.sgld_steps, rank, args.cpu_seconds / 2 if world == 1 and rank == 0 else 0)
+        v_out = plantvillage_measure(args.sgld_steps, rank, args.cpu_seconds if world == 1 and rank == 0 else 0)
         parallel.barrier()
     if rank != 0:
         return
@@ -406,11 +420,14 @@ def main():
         "leapfrogs_per_s": lf_total / t_max,
         "leapfrogs": lf_total,
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
-                     "frac": achieved / peak, "traffic": pmc_traffic(args.dtype, path),
-                     "kernel": ("k_sghmc_p2<%s,10> (one launch per %d-step call)" % (
-                         "double" if args.dtype == "f64" else "float", CHUNK)) if path == "persistent"
-                     else "kernel-per-phase sequence of one %d-step call" % CHUNK,
-                     "launch_ms": launch_ms, "flop_per_launch": flop_per_launch},
+                     "frac": achieved / peak, "traffic": pmc_traffic(args.dtype, path, lf_local / n_calls),
+                     "traffic_source": "PMC 2*FETCH_SIZE+WRITE_SIZE per leapfrog of the driver-shape launch "
+                                       "(profiles/pmc_r02_%s_%s.json) x leapfrogs per launch of this run" % (args.dtype, path),
+                     "kernel": ("k_sghmc_p2<%s,10> (one launch per call: %d call(s) of <= %d steps)" % (
+                         "double" if args.dtype == "f64" else "float", n_calls, CHUNK)) if path == "persistent"
+                     else "kernel-per-phase sequence of each call (%d call(s) of <= %d steps)" % (n_calls, CHUNK),
+                     "launch_ms": launch_ms, "flop_per_launch": flop_per_launch, "calls": n_calls,
+                     "leapfrogs_per_launch": lf_local / n_calls},
         "diagnostics": {"rhat_ll": float(np.ravel(diag["rhat"])[0]), "ess_ll": float(np.ravel(diag["ess"])[0]),
                         "gather": "torch.distributed all_gather (%s)" % (parallel.backend_name() if world > 1 else "local")},
         "cpu_baseline": None,

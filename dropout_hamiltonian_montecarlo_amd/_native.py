@@ -34,7 +34,8 @@ class SamplerArgs(ctypes.Structure):
                 ("seed", ctypes.c_uint64), ("chain0", ctypes.c_uint32), ("step_base", ctypes.c_uint32),
                 ("W", c_void_p), ("b", c_void_p), ("out_A", c_void_p), ("out_accepted", c_void_p),
                 ("out_ll", c_void_p), ("out_E", c_void_p), ("pW", c_void_p), ("pb", c_void_p),
-                ("out_trace", c_void_p)]
+                ("out_trace", c_void_p), ("out_abort", c_void_p), ("path_length", c_double),
+                ("out_L", c_dblp)]
 
 
 class MvnArgs(ctypes.Structure):
@@ -92,7 +93,8 @@ EXPORTS = ("hmcx_version", "hmcx_create", "hmcx_destroy", "hmcx_last_error", "hm
            "hmcx_softmax_grad", "hmcx_softmax_loglik", "hmcx_softmax_predict", "hmcx_sghmc_run",
            "hmcx_sgld_run", "hmcx_hmc_mvn_run", "hmcx_mlp_masks", "hmcx_mlp_grad", "hmcx_mlp_loss",
            "hmcx_mlp_sghmc_run", "hmcx_logistic_grad", "hmcx_logistic_loglik", "hmcx_logistic_predict",
-           "hmcx_sumsq", "hmcx_sgd_run", "hmcx_hmc_run", "hmcx_axpy", "hmcx_mvn_eval")
+           "hmcx_sumsq", "hmcx_sgd_run", "hmcx_hmc_run", "hmcx_axpy", "hmcx_mvn_eval",
+           "hmcx_clear_abort", "hmcx_philox_schedule")
 
 _lib = None
 _lock = threading.Lock()
@@ -138,6 +140,9 @@ def load_library():
         lib.hmcx_softmax_predict.argtypes = [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int,
                                              c_void_p, c_void_p, c_void_p]
         lib.hmcx_sghmc_run.argtypes = [c_void_p, ctypes.POINTER(SamplerArgs)]
+        lib.hmcx_clear_abort.argtypes = [c_void_p]
+        lib.hmcx_philox_schedule.argtypes = [ctypes.c_uint64, ctypes.c_uint32, c_int, ctypes.c_uint32, c_int,
+                                             c_double, c_dblp, c_dblp, c_i32p, c_dblp]
         lib.hmcx_sgld_run.argtypes = [c_void_p, ctypes.POINTER(SamplerArgs)]
         lib.hmcx_hmc_mvn_run.argtypes = [c_void_p, ctypes.POINTER(MvnArgs)]
         u32, u64 = ctypes.c_uint32, ctypes.c_uint64
@@ -189,9 +194,16 @@ class Context:
             msg = self.lib.hmcx_last_error(self.h)
             raise HmcxError("%s failed (%d): %s" % (what, rc, msg.decode() if msg else ""))
 
+    path = 0
+
     def set_sghmc_path(self, path):
         """0 auto, 1 kernel-per-phase, 2 persistent (see include/hmcx.h)."""
         self.check(self.lib.hmcx_set_sghmc_path(self.h, int(path)), "hmcx_set_sghmc_path")
+        self.path = int(path)
+
+    def clear_abort(self):
+        """Lower the context's persistent-launch abort word (include/hmcx.h hmcx_clear_abort)."""
+        self.check(self.lib.hmcx_clear_abort(self.h), "hmcx_clear_abort")
 
     def set_timing(self, on):
         """Bracket every sampler run's kernels with HIP events on the launch stream (resets totals)."""
@@ -277,6 +289,24 @@ def philox_normals(seed, chain, step, slot, e0, n, dtype="f32"):
 
 SLOT_PATH = 0xFFFFFFFE
 SLOT_ACCEPT = 0xFFFFFFFD
+
+
+def philox_schedule(seed, chain0, C, step_base, path_length, eps):
+    """Path lengths L, iterations max(0, L − 1) and accept uniforms of len(eps) Philox-mode steps
+    for C chains, [n_steps, C] each (hmcx_philox_schedule; one host C call)."""
+    import numpy as np
+    eps = np.ascontiguousarray(eps, dtype=np.float64)
+    n = eps.shape[0]
+    L = np.empty((n, C), dtype=np.float64)
+    n_iter = np.empty((n, C), dtype=np.int32)
+    u = np.empty((n, C), dtype=np.float64)
+    rc = load_library().hmcx_philox_schedule(seed & 0xFFFFFFFFFFFFFFFF, chain0 & 0xFFFFFFFF, C,
+                                             step_base & 0xFFFFFFFF, n, float(path_length),
+                                             eps.ctypes.data_as(c_dblp), L.ctypes.data_as(c_dblp),
+                                             n_iter.ctypes.data_as(c_i32p), u.ctypes.data_as(c_dblp))
+    if rc != 0:
+        raise HmcxError("non-finite path length (step size 0?)")
+    return L, n_iter, u
 
 
 def philox_uniforms_chains(seed, chains, step, slot, idx=0):

@@ -4,6 +4,7 @@
 #include "hmcx_internal.h"
 #include <new>
 #include <cstring>
+#include <cmath>
 
 namespace hmcx {
 
@@ -93,12 +94,14 @@ int abort_poll(hmcx_ctx* ctx, bool block) {
   return HMCX_OK;
 }
 
+int abort_precheck(hmcx_ctx* ctx) {
+  // earlier launches that have finished (all of them when too many checks are in flight): an abort
+  // is reported here, before the caller enqueues anything
+  return abort_poll(ctx, ctx->abort_pend.size() >= (size_t)ABORT_SLOTS / 2);
+}
+
 int abort_defer(hmcx_ctx* ctx, const int* dev_flag, hipStream_t st) {
   if (!ctx->abort_host) HMCX_HIP(ctx, hipHostMalloc((void**)&ctx->abort_host, ABORT_SLOTS * sizeof(int), hipHostMallocDefault));
-  if (ctx->abort_pend.size() >= (size_t)ABORT_SLOTS / 2) {     // bound the in-flight checks
-    int rc = abort_poll(ctx, true);
-    if (rc) return rc;
-  }
   const int slot = (int)(ctx->abort_next++ % ABORT_SLOTS);
   hipEvent_t ev = nullptr;
   int rc = ev_take(ctx, &ev);
@@ -106,38 +109,95 @@ int abort_defer(hmcx_ctx* ctx, const int* dev_flag, hipStream_t st) {
   HMCX_HIP(ctx, hipMemcpyAsync(ctx->abort_host + slot, dev_flag, sizeof(int), hipMemcpyDeviceToHost, st));
   HMCX_HIP(ctx, hipEventRecord(ev, st));
   ctx->abort_pend.emplace_back(ev, slot);
-  return abort_poll(ctx, false);                                 // earlier launches that have finished
+  return HMCX_OK;          // checked before the next launch (abort_precheck) or by hmcx_synchronize
 }
 
 void begin_call(hmcx_ctx* ctx) {
-  if (ctx->stage_pending) {
-    (void)hipEventSynchronize(ctx->stage_ev);
-    ctx->stage_pending = false;
+  ctx->stage_cur ^= 1;
+  const int c = ctx->stage_cur;
+  if (ctx->stage_pend[c]) {                     // uploads of the call before the previous one
+    (void)hipEventSynchronize(ctx->stage_evv[c]);
+    ctx->stage_pend[c] = false;
   }
   ctx->stage_off = 0;
+}
+
+static int stage_reserve(hmcx_ctx* ctx, size_t bytes, char** h) {
+  const int c = ctx->stage_cur;
+  const size_t need = ctx->stage_off + ((bytes + 255) / 256) * 256;
+  if (need > ctx->stage_capv[c]) {
+    // a grown staging buffer invalidates earlier offsets of this call: drain the stream first.  Both
+    // slots grow together (pinned allocations cost hundreds of µs: not inside the next call too)
+    HMCX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    const size_t cap = std::max(need * 2, (size_t)1 << 20);
+    for (int i = 0; i < 2; ++i) {
+      if (ctx->stage_capv[i] >= cap) continue;
+      if (ctx->stage_pend[i]) {
+        HMCX_HIP(ctx, hipEventSynchronize(ctx->stage_evv[i]));
+        ctx->stage_pend[i] = false;
+      }
+      char* nb = nullptr;
+      HMCX_HIP(ctx, hipHostMalloc((void**)&nb, cap, hipHostMallocDefault));
+      if (ctx->stage_buf[i]) (void)hipHostFree(ctx->stage_buf[i]);
+      ctx->stage_buf[i] = nb;
+      ctx->stage_capv[i] = cap;
+      if (!ctx->stage_evv[i]) HMCX_HIP(ctx, hipEventCreateWithFlags(&ctx->stage_evv[i], hipEventDisableTiming));
+    }
+    ctx->stage_off = 0;
+  }
+  *h = ctx->stage_buf[c] + ctx->stage_off;
+  ctx->stage_off += ((bytes + 255) / 256) * 256;
+  return HMCX_OK;
+}
+
+static int stage_copy(hmcx_ctx* ctx, void* dst, const char* h, size_t bytes) {
+  const int c = ctx->stage_cur;
+  HMCX_HIP(ctx, hipMemcpyAsync(dst, h, bytes, hipMemcpyHostToDevice, ctx->stream));
+  HMCX_HIP(ctx, hipEventRecord(ctx->stage_evv[c], ctx->stream));
+  ctx->stage_pend[c] = true;
+  return HMCX_OK;
 }
 
 int upload(hmcx_ctx* ctx, void* dst, const void* src, size_t bytes) {
   if (bytes == 0) return HMCX_OK;
   if (!src) return set_error(ctx, HMCX_EINVAL, "upload: null host array");
-  const size_t need = ctx->stage_off + ((bytes + 255) / 256) * 256;
-  if (need > ctx->stage_cap) {
-    // a grown staging buffer invalidates earlier offsets of this call: drain the stream first
-    HMCX_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    char* nb = nullptr;
-    const size_t cap = std::max(need * 2, (size_t)1 << 20);
-    HMCX_HIP(ctx, hipHostMalloc((void**)&nb, cap, hipHostMallocDefault));
-    if (ctx->stage) (void)hipHostFree(ctx->stage);
-    ctx->stage = nb;
-    ctx->stage_cap = cap;
-    ctx->stage_off = 0;
-  }
-  char* h = ctx->stage + ctx->stage_off;
+  char* h = nullptr;
+  int rc = stage_reserve(ctx, bytes, &h);
+  if (rc) return rc;
   std::memcpy(h, src, bytes);
-  ctx->stage_off += ((bytes + 255) / 256) * 256;
-  HMCX_HIP(ctx, hipMemcpyAsync(dst, h, bytes, hipMemcpyHostToDevice, ctx->stream));
-  HMCX_HIP(ctx, hipEventRecord(ctx->stage_ev, ctx->stream));
-  ctx->stage_pending = true;
+  return stage_copy(ctx, dst, h, bytes);
+}
+
+size_t packed_bytes(int n, const size_t* bytes) {
+  size_t t = 0;
+  for (int i = 0; i < n; ++i) t += ((bytes[i] + 255) / 256) * 256;
+  return t;
+}
+
+int upload_packed(hmcx_ctx* ctx, char* dst, int n, const void* const* src, const size_t* bytes, char** dev) {
+  const size_t total = packed_bytes(n, bytes);
+  size_t off = 0;
+  for (int i = 0; i < n; ++i) {
+    dev[i] = dst + off;
+    off += ((bytes[i] + 255) / 256) * 256;
+  }
+  if (total == 0) return HMCX_OK;
+  char* h = nullptr;
+  int rc = stage_reserve(ctx, total, &h);
+  if (rc) return rc;
+  for (int i = 0; i < n; ++i)
+    if (bytes[i] && src[i]) std::memcpy(h + (dev[i] - dst), src[i], bytes[i]);
+  return stage_copy(ctx, dst, h, total);
+}
+
+int kernel_occupancy(hmcx_ctx* ctx, const void* kfn, int threads, int lds, int* per_cu) {
+  for (auto& e : ctx->occ_cache)
+    if (e.first.first == kfn && e.first.second == lds) { *per_cu = e.second; return HMCX_OK; }
+  HMCX_HIP(ctx, hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+  int occ = 0;
+  HMCX_HIP(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kfn, threads, lds));
+  ctx->occ_cache.push_back({{kfn, lds}, occ});
+  *per_cu = occ;
   return HMCX_OK;
 }
 
@@ -350,12 +410,15 @@ int hmcx_create(int device, hmcx_ctx** out) {
   if (!c) return HMCX_ENOMEM;
   c->device = device;
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreateWithFlags(&c->stage_ev, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming) != hipSuccess) {
     delete c;
     return HMCX_EHIP;
   }
   c->stream = c->own_stream;
+  if (hipMalloc((void**)&c->abort_dev, sizeof(int)) != hipSuccess || hipMemset(c->abort_dev, 0, sizeof(int)) != hipSuccess) {
+    delete c;
+    return HMCX_EHIP;
+  }
   int ncu = 0, lds = 0;
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
     c->num_cus = ncu;
@@ -370,14 +433,17 @@ int hmcx_destroy(hmcx_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
   if (ctx->ws) (void)hipFree(ctx->ws);
-  if (ctx->stage) (void)hipHostFree(ctx->stage);
-  if (ctx->stage_ev) (void)hipEventDestroy(ctx->stage_ev);
+  for (int i = 0; i < 2; ++i) {
+    if (ctx->stage_buf[i]) (void)hipHostFree(ctx->stage_buf[i]);
+    if (ctx->stage_evv[i]) (void)hipEventDestroy(ctx->stage_evv[i]);
+  }
   if (ctx->ev_in) (void)hipEventDestroy(ctx->ev_in);
   for (auto& pr : ctx->t_pend) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
   if (ctx->t_open) (void)hipEventDestroy(ctx->t_open);
   for (auto& pr : ctx->abort_pend) (void)hipEventDestroy(pr.first);
   for (auto e : ctx->ev_pool) (void)hipEventDestroy(e);
   if (ctx->abort_host) (void)hipHostFree(ctx->abort_host);
+  if (ctx->abort_dev) (void)hipFree(ctx->abort_dev);
   for (auto& g : ctx->graveyard) {
     (void)hipGraphExecDestroy(g.first);
     (void)hipEventDestroy(g.second);
@@ -401,6 +467,14 @@ int hmcx_synchronize(hmcx_ctx* ctx) {
   return abort_poll(ctx, true);                    // reports an aborted persistent launch
 }
 
+int hmcx_clear_abort(hmcx_ctx* ctx) {
+  HMCX_GUARD_CTX(ctx);
+  for (auto& pr : ctx->abort_pend) ctx->ev_pool.push_back(pr.first);
+  ctx->abort_pend.clear();
+  HMCX_HIP(ctx, hipMemsetAsync(ctx->abort_dev, 0, sizeof(int), ctx->stream));
+  return HMCX_OK;
+}
+
 int hmcx_set_sghmc_path(hmcx_ctx* ctx, int path) {
   HMCX_GUARD_CTX(ctx);
   if (path < 0 || path > 2) return set_error(ctx, HMCX_EINVAL, "path must be 0 (auto), 1 (kernels), 2 (persistent)");
@@ -421,6 +495,12 @@ int hmcx_set_timing(hmcx_ctx* ctx, int enabled) {
   ctx->timing = enabled ? 1 : 0;
   ctx->t_ms = 0.0;
   ctx->t_n = 0;
+  // event creation costs tens of µs: create the timed runs' events here, not inside the first run
+  while (enabled && ctx->ev_pool.size() < 8) {
+    hipEvent_t ev = nullptr;
+    HMCX_HIP(ctx, hipEventCreate(&ev));
+    ctx->ev_pool.push_back(ev);
+  }
   return HMCX_OK;
 }
 
@@ -446,6 +526,24 @@ void hmcx_philox_normals(uint64_t seed, uint32_t chain, uint32_t step, uint32_t 
 void hmcx_philox_normals_f64(uint64_t seed, uint32_t chain, uint32_t step, uint32_t slot, uint32_t e0, uint32_t n,
                              double* out) {
   for (uint32_t i = 0; i < n; ++i) out[i] = philox_normal_d(seed, chain, step, slot, e0 + i);
+}
+
+int hmcx_philox_schedule(uint64_t seed, uint32_t chain0, int C, uint32_t step_base, int n_steps, double path_length,
+                         const double* eps, double* L, int32_t* n_iter, double* u) {
+  if (C < 1 || n_steps < 0 || !eps || !L || !n_iter || !u) return HMCX_EINVAL;
+  for (int s = 0; s < n_steps; ++s) {
+    const uint32_t st = step_base + (uint32_t)s;
+    for (int c = 0; c < C; ++c) {
+      const size_t i = (size_t)s * C + c;
+      const double l = std::ceil(2.0 * philox_uniform(seed, chain0 + (uint32_t)c, st, SLOT_PATH, 0) *
+                                 path_length / eps[s]);
+      if (!std::isfinite(l) || l > 2147483647.0) return HMCX_EINVAL;
+      L[i] = l;
+      n_iter[i] = l - 1.0 > 0.0 ? (int32_t)std::ceil(l - 1.0) : 0;
+      u[i] = philox_uniform(seed, chain0 + (uint32_t)c, st, SLOT_ACCEPT, 0);
+    }
+  }
+  return HMCX_OK;
 }
 
 static int check_dims(hmcx_ctx* ctx, int dtype, int B, int D, int K, int C) {
@@ -656,13 +754,34 @@ static int run_traced(hmcx_ctx* ctx, const hmcx_sampler_args* a, F run_one) {
 }
 }  // extern "C++"
 
-int hmcx_sghmc_run(hmcx_ctx* ctx, const hmcx_sampler_args* a) {
+int hmcx_sghmc_run(hmcx_ctx* ctx, const hmcx_sampler_args* a_in) {
   HMCX_GUARD_CTX(ctx);
+  if (!a_in) return set_error(ctx, HMCX_EINVAL, "null args");
+  const hmcx_sampler_args* a = a_in;
+  hmcx_sampler_args own;
+  if (a_in->noise_mode == HMCX_NOISE_PHILOX && !a_in->n_iter && !a_in->u_accept && a_in->n_steps > 0 && a_in->C > 0) {
+    // the call draws its own Philox schedule (one pass here instead of one by the caller)
+    const size_t nsc = (size_t)a_in->n_steps * a_in->C;
+    if (!a_in->eps) return set_error(ctx, HMCX_EINVAL, "null pointer");
+    ctx->sched_L.resize(nsc);
+    ctx->sched_n.resize(nsc);
+    ctx->sched_u.resize(nsc);
+    if (hmcx_philox_schedule(a_in->seed, a_in->chain0, a_in->C, a_in->step_base, a_in->n_steps, a_in->path_length,
+                             a_in->eps, ctx->sched_L.data(), ctx->sched_n.data(), ctx->sched_u.data()))
+      return set_error(ctx, HMCX_EINVAL, "non-finite path length (step size 0?)");
+    if (a_in->out_L) std::memcpy(a_in->out_L, ctx->sched_L.data(), nsc * sizeof(double));
+    own = *a_in;
+    own.n_iter = ctx->sched_n.data();
+    own.u_accept = ctx->sched_u.data();
+    a = &own;
+  }
   int rc = check_sampler(ctx, a, true);
   if (rc) return rc;
   if (a->pW || a->pb) return set_error(ctx, HMCX_EINVAL, "sghmc: pW/pb are SGLD-only fields");
   if (a->n_steps == 0) return HMCX_OK;
-  if (a->out_trace && sghmc_p2_selected(ctx, a))   // the persistent kernel stores the trace rows itself
+  const bool p2 = sghmc_p2_selected(ctx, a);
+  if (a->out_abort && !p2) HMCX_HIP(ctx, hipMemsetAsync(a->out_abort, 0, sizeof(int32_t), ctx->stream));
+  if (a->out_trace && p2)   // the persistent kernel stores the trace rows itself
     return a->dtype == HMCX_F64 ? sghmc_run_t<double>(ctx, a) : sghmc_run_t<float>(ctx, a);
   return run_traced(ctx, a, [ctx](const hmcx_sampler_args* s) {
     return s->dtype == HMCX_F64 ? sghmc_run_t<double>(ctx, s) : sghmc_run_t<float>(ctx, s);

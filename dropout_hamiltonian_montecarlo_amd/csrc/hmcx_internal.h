@@ -19,12 +19,19 @@ struct hmcx_ctx {
   // device workspace (grows; freed only after a stream sync)
   char* ws = nullptr;
   size_t ws_cap = 0;
-  // pinned host staging for per-call schedules
-  char* stage = nullptr;
-  size_t stage_cap = 0;
+  // pinned host staging for per-call schedules: two slots used by alternate calls, so a call only
+  // waits (begin_call) for the uploads of the call before the previous one, never for the stream
+  char* stage_buf[2] = {nullptr, nullptr};
+  size_t stage_capv[2] = {0, 0};
+  hipEvent_t stage_evv[2] = {nullptr, nullptr};
+  bool stage_pend[2] = {false, false};
+  int stage_cur = 0;
   size_t stage_off = 0;
-  hipEvent_t stage_ev = nullptr;
-  bool stage_pending = false;
+  // host schedule of the calls that draw their own (PHILOX, n_iter == u_accept == NULL)
+  std::vector<double> sched_L, sched_u;
+  std::vector<int32_t> sched_n;
+  // launch attributes already applied (dynamic-LDS limit) and the occupancy they gave, per kernel
+  std::vector<std::pair<std::pair<const void*, int>, int>> occ_cache;
   // hipGraph mode: capture happens on own_stream (the legacy default stream cannot be captured)
   hipEvent_t ev_in = nullptr, ev_out = nullptr;
   std::vector<std::pair<hipGraphExec_t, hipEvent_t>> graveyard;   // executed graphs awaiting release
@@ -39,6 +46,8 @@ struct hmcx_ctx {
   // deferred abort checks of persistent launches: the abort word is copied into a pinned slot and
   // checked once the launch's event has completed (next call, hmcx_synchronize), not by a per-call sync
   int* abort_host = nullptr;           // pinned [ABORT_SLOTS]
+  int* abort_dev = nullptr;            // device word: raised by a timed-out persistent launch, sticky
+                                       // until hmcx_clear_abort (later launches return at once)
   std::vector<std::pair<hipEvent_t, int>> abort_pend;
   unsigned abort_next = 0;
 };
@@ -62,6 +71,7 @@ int timing_collect(hmcx_ctx* ctx);
 // and returns an error if any launch had aborted.
 int abort_defer(hmcx_ctx* ctx, const int* dev_flag, hipStream_t st);
 int abort_poll(hmcx_ctx* ctx, bool block);
+int abort_precheck(hmcx_ctx* ctx);
 
 #define HMCX_HIP(ctx, expr)                                                                  \
   do {                                                                                       \
@@ -171,6 +181,12 @@ template <typename T> struct AcceptArgs {
 // Copy a host array to device through the context's pinned staging buffer (stream-ordered).
 int upload(hmcx_ctx* ctx, void* dst, const void* src, size_t bytes);
 void begin_call(hmcx_ctx* ctx);
+// Several host arrays in ONE host-to-device copy: item i lands at dst + packed_offset(i) (256-B
+// aligned pieces); dst must hold packed_bytes(n, bytes).  Null / empty items are skipped.
+size_t packed_bytes(int n, const size_t* bytes);
+int upload_packed(hmcx_ctx* ctx, char* dst, int n, const void* const* src, const size_t* bytes, char** dev);
+// hipFuncSetAttribute(max dynamic LDS) once per (kernel, lds) and the occupancy it gives (cached).
+int kernel_occupancy(hmcx_ctx* ctx, const void* kfn, int threads, int lds, int* per_cu);
 
 // Optional hipGraph capture of one run call (hmcx_set_graph_mode).
 struct GraphScope {

@@ -71,7 +71,9 @@ struct Q2Args {
   int al2;                                  // row teams share an XCD (xmap): A-round stores plain
   int prefetch;                             // 1: next step's tile/labels loaded during the accept round
   int acc1;                                 // 1: accept partials polled in one batch (HMCX_P2_ACC1)
-  int* abort_flag;                          // inside the arena
+  int* abort_flag;                          // the context's sticky abort word (hmcx_clear_abort)
+  int force_abort;                          // HMCX_P2_FORCE_ABORT=<step>: the last workgroup raises the
+                                            // abort word at that step (tests the recovery path); −1 off
   double* out_A; int32_t* out_acc; double* out_ll; double* out_E;
   void* out_trace;                          // [n_steps][P] state after every step, or null
   unsigned long long* prof;                 // HMCX_PERSIST_PROF=1: per-segment s_memtime totals (workgroup 0)
@@ -456,6 +458,8 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
   const int wl = (fo0 + od) * 16 + okc;               // index in Wf
   T pw = T(0), wv = T(0), w0 = T(0), zn = T(0);
 
+  // a launch behind a timed-out one (sticky abort word) leaves everything untouched
+  if (__hip_atomic_load(a.abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
   if (tid == 0) ish[0] = 0;
   if (tid < 16) profacc[tid] = 0ull;
   for (int e = tid; e < BfP * 16; e += QTH) {
@@ -539,6 +543,10 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
     const T* Xg = reinterpret_cast<const T*>(a.X) + (size_t)a.row0[s] * D;
     const T* Yg = reinterpret_cast<const T*>(a.Y) + (size_t)a.row0[s] * K;
     prof.stamp(0);
+    if (s == a.force_abort && bid == G - 1) {                             // test knob: a "timed-out" member
+      if (tid == 0) __hip_atomic_store(a.abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
 
     // ---- step start: tile, labels of my rows (step 0 only: later steps' were loaded while the
     //      previous accept round travelled), momentum (hmc.py:82-87), step-start copies
@@ -897,7 +905,10 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
   }
   prof.stamp(0);
   prof.flush();
-  // ---- committed state: owners write their weights, workgroup 0 the bias
+  // ---- committed state: owners write their weights, workgroup 0 the bias — unless a member timed
+  //      out (then no workgroup can have passed the last accept round, which needs every member's
+  //      write-through partial: an aborted launch leaves W/b as they were)
+  if (__hip_atomic_load(a.abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
   if (own) reinterpret_cast<T*>(a.W)[e_own] = wv;
   if (bid == 0 && tid < K) reinterpret_cast<T*>(a.b)[tid] = bsh[tid];
 }
@@ -969,28 +980,33 @@ int sghmc_p2_t(hmcx_ctx* ctx, const hmcx_sampler_args* s, const PersistPlan2& pl
              nXS = 2L * G * (pad ? 8 : 4);
   const long ngran = nXA + nXD + nXB + nXW + nXS + 1;
   if (ngran * 16 > 0x7fffffffL) return set_error(ctx, HMCX_EUNSUPPORTED, "persistent SGHMC: arena too large");
+  int rc = abort_precheck(ctx);                  // an earlier launch's timeout, before enqueueing more
+  if (rc) return rc;
+  // the call's schedule travels in one packed host-to-device copy
+  const bool buf = s->noise_mode == HMCX_NOISE_BUFFER;
+  const void* hsrc[5] = {s->eps, s->u_accept, s->row0, s->n_iter, buf ? (const void*)s->noise_off : nullptr};
+  const size_t hbytes[5] = {n * sizeof(double), n * sizeof(double), n * sizeof(int64_t), n * sizeof(int32_t),
+                            buf ? n * sizeof(int64_t) : 0};
+  for (int i = 0; i < 5; ++i)
+    if (hbytes[i] && !hsrc[i]) return set_error(ctx, HMCX_EINVAL, "sghmc: null host schedule array");
+  const size_t sched_bytes = packed_bytes(5, hbytes);
   Workspace ws(ctx);
   char* arena;
-  double *d_eps, *d_u;
-  int64_t *d_row0, *d_noff;
-  int32_t* d_n;
+  char* sched;
   do {
     ws.reset();
     arena = reinterpret_cast<char*>(ws.take<double>((size_t)ngran * 2));
-    d_eps = ws.take<double>(n);
-    d_u = ws.take<double>(n);
-    d_row0 = ws.take<int64_t>(n);
-    d_noff = ws.take<int64_t>(n);
-    d_n = ws.take<int32_t>(n);
+    sched = ws.take<char>(sched_bytes);
   } while (ws.retry());
   if (ws.failed) return HMCX_ENOMEM;
   begin_call(ctx);
-  int rc;
-  if ((rc = upload(ctx, d_eps, s->eps, n * sizeof(double)))) return rc;
-  if ((rc = upload(ctx, d_u, s->u_accept, n * sizeof(double)))) return rc;
-  if ((rc = upload(ctx, d_row0, s->row0, n * sizeof(int64_t)))) return rc;
-  if ((rc = upload(ctx, d_n, s->n_iter, n * sizeof(int32_t)))) return rc;
-  if (s->noise_mode == HMCX_NOISE_BUFFER && (rc = upload(ctx, d_noff, s->noise_off, n * sizeof(int64_t)))) return rc;
+  char* dp[5];
+  if ((rc = upload_packed(ctx, sched, 5, hsrc, hbytes, dp))) return rc;
+  double* d_eps = reinterpret_cast<double*>(dp[0]);
+  double* d_u = reinterpret_cast<double*>(dp[1]);
+  int64_t* d_row0 = reinterpret_cast<int64_t*>(dp[2]);
+  int32_t* d_n = reinterpret_cast<int32_t*>(dp[3]);
+  int64_t* d_noff = reinterpret_cast<int64_t*>(dp[4]);
   HMCX_HIP(ctx, hipMemsetAsync(arena, 0, (size_t)ngran * 16, ctx->stream));
 
   Q2Args a{};
@@ -1014,17 +1030,22 @@ int sghmc_p2_t(hmcx_ctx* ctx, const hmcx_sampler_args* s, const PersistPlan2& pl
     static const int spread_env = getenv("HMCX_P2_SPREAD") ? atoi(getenv("HMCX_P2_SPREAD")) : 2;
     a.spread = fits ? spread_env : 0;
     a.zoff = !(getenv("HMCX_P2_ZOFF") && getenv("HMCX_P2_ZOFF")[0] == '0');
-    static const int xmap_env = getenv("HMCX_P2_XMAP") ? atoi(getenv("HMCX_P2_XMAP")) : 1;
+    // HMCX_P2_XMAP: 1 (default) row teams on one XCD; 0 identity map; 2 = deliberately MISPLACED (test
+    // knob, read per call): identity map with the row-team rounds still published into one XCD's L2,
+    // so members on other XCDs never see them — the launch times out (4 s) and aborts
+    const int xmap_env = getenv("HMCX_P2_XMAP") ? atoi(getenv("HMCX_P2_XMAP")) : 1;
     a.xmap = (xmap_env == 1 && (pl.Gr * pl.Gf) % 8 == 0) ? 1 : 0;
     static const int fl2_env = getenv("HMCX_P2_FL2") ? atoi(getenv("HMCX_P2_FL2")) : 1;
-    a.fl2 = (fl2_env == 1 && !a.xmap && pl.Gf % 8 == 0) ? 1 : 0;
+    a.fl2 = (fl2_env == 1 && !a.xmap && pl.Gf % 8 == 0 && xmap_env != 2) ? 1 : 0;
     a.al2 = (fl2_env == 1 && a.xmap && ((pl.Gr * pl.Gf) / 8) % pl.Gf == 0) ? 1 : 0;
+    if (xmap_env == 2) a.al2 = 1;
     static const int pf_env = getenv("HMCX_P2_PREFETCH") ? atoi(getenv("HMCX_P2_PREFETCH")) : 1;
     a.prefetch = pf_env == 1 ? 1 : 0;
     static const int acc1_env = getenv("HMCX_P2_ACC1") ? atoi(getenv("HMCX_P2_ACC1")) : 1;
     a.acc1 = acc1_env == 1 ? 1 : 0;
   }
-  a.abort_flag = reinterpret_cast<int*>(arena + (ngran - 1) * 16);
+  a.abort_flag = ctx->abort_dev;
+  a.force_abort = getenv("HMCX_P2_FORCE_ABORT") ? atoi(getenv("HMCX_P2_FORCE_ABORT")) : -1;
   a.out_A = s->out_A; a.out_acc = s->out_accepted; a.out_ll = s->out_ll; a.out_E = s->out_E;
   a.out_trace = s->out_trace;
   static const bool prof_on = getenv("HMCX_PERSIST_PROF") && getenv("HMCX_PERSIST_PROF")[0] == '1';
@@ -1043,19 +1064,22 @@ int sghmc_p2_t(hmcx_ctx* ctx, const hmcx_sampler_args* s, const PersistPlan2& pl
   }
   a.trace = dtrace;
   const void* kfn = KC == 10 ? (const void*)k_sghmc_p2<T, 10> : (const void*)k_sghmc_p2<T, 16>;
-  HMCX_HIP(ctx, hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.lds));
   void* kargs[] = {&a};
-  if ((rc = timing_begin(ctx, ctx->stream))) return rc;
-  // co-residency of all G workgroups is checked here (occupancy query × CUs); a plain launch then
-  // has the same residency as a cooperative one without its per-launch host cost
+  // co-residency of all G workgroups is checked here (occupancy query × CUs, cached per kernel); a
+  // plain launch then has the same residency as a cooperative one without its per-launch host cost
   int per_cu = 0;
-  HMCX_HIP(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, QTH, pl.lds));
+  if ((rc = kernel_occupancy(ctx, kfn, QTH, (int)pl.lds, &per_cu))) return rc;
   if ((long)per_cu * ctx->num_cus < G)
     return set_error(ctx, HMCX_EUNSUPPORTED, "persistent SGHMC: workgroups cannot be co-resident");
+  if ((rc = timing_begin(ctx, ctx->stream))) return rc;
   HMCX_HIP(ctx, hipLaunchKernel(kfn, dim3(G), dim3(QTH), kargs, (unsigned)pl.lds, ctx->stream));
   if ((rc = timing_end(ctx, ctx->stream))) return rc;
-  if (!dprof && !dtrace)                         // no per-call sync: checked once the launch is done
+  if (s->out_abort) {                            // the caller reads this launch's verdict itself
+    HMCX_HIP(ctx, hipMemcpyAsync(s->out_abort, ctx->abort_dev, sizeof(int), hipMemcpyDeviceToDevice, ctx->stream));
+    if (!dprof && !dtrace) return HMCX_OK;
+  } else if (!dprof && !dtrace) {                // no per-call sync: checked once the launch is done
     return abort_defer(ctx, a.abort_flag, ctx->stream);
+  }
   int flag = 0;
   HMCX_HIP(ctx, hipMemcpyAsync(&flag, a.abort_flag, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
   HMCX_HIP(ctx, hipStreamSynchronize(ctx->stream));

@@ -7,9 +7,14 @@ the ``+ε·∇U`` momentum sign and 2ε noise std (sghmc.py:31,34), no momentum 
 NaN energy difference accepted (Python ``min``).  The dead ``grad(q)`` of sghmc.py:26 is not
 executed (it has no effect and consumes no randomness).
 
-The whole trajectory of every step runs inside libhmcx (hmcx_sghmc_run): per leapfrog
-iteration one k_fwd + one k_grad launch; the host only prepares the per-step schedule.
+The whole trajectory of every step runs inside libhmcx (hmcx_sghmc_run): one chain — one
+persistent launch per call (csrc/hmcx_persist2.hip); C ≥ 16 chains — the chain-batched GEMMs
+(csrc/hmcx_batch.h); otherwise one k_fwd + one k_grad launch per leapfrog iteration.  The host only
+prepares the per-step schedule and reads back the per-step scalars.
 """
+import os
+import time
+
 import numpy as np
 import torch
 
@@ -17,6 +22,10 @@ from dropout_hamiltonian_montecarlo_amd import _native as nat
 from dropout_hamiltonian_montecarlo_amd._native import HmcxError, ptr
 
 from .sgmcmc import RunResult, sgmcmc
+
+
+_HOST_PROF = os.environ.get("HMCX_HOST_PROF") == "1"     # phase timestamps of _enqueue (tools/)
+_marks = []
 
 
 def _n_iter(path_length):
@@ -55,15 +64,14 @@ class sghmc(sgmcmc):
         off = 0
         Ls = np.empty((n_steps, C))
         if self.noise == 'philox':
-            # per-step path-length and accept uniforms of every chain, all steps in one pass
-            g = ((self.global_step + np.arange(n_steps)) & 0xFFFFFFFF)[:, None]
-            chain_ids = (self.chain + np.arange(C))[None, :]
-            uL = nat.philox_uniforms_chains(self.seed, chain_ids, g, nat.SLOT_PATH)
-            Ls[:] = np.ceil(2 * uL * self.path_length / np.asarray(eps, dtype=np.float64)[:, None])
-            if not np.all(np.isfinite(Ls)):
-                raise HmcxError("non-finite path length (step size 0?)")
-            n_iter[:] = np.maximum(0, np.ceil(Ls - 1)).astype(np.int32)
-            u[:] = nat.philox_uniforms_chains(self.seed, chain_ids, g, nat.SLOT_ACCEPT)
+            # per-step path lengths and accept uniforms of every chain: one host C call
+            Ls, n_iter, u = nat.philox_schedule(self.seed, self.chain, C, self.global_step, self.path_length, eps)
+            if self.trace is not None:
+                if C == 1:
+                    self.trace.extend({'L': float(l), 'eps': float(e)} for l, e in zip(Ls[:, 0], eps))
+                else:
+                    self.trace.extend({'L': Ls[s].copy(), 'eps': float(eps[s])} for s in range(n_steps))
+            return n_iter, u, None, noise_off
         for s in range(n_steps):
             e = eps[s]
             if self.noise == 'numpy':
@@ -89,11 +97,57 @@ class sghmc(sgmcmc):
             return self._run_mlp(state, data, rows, eps, rng, batch_size)
         return self._collect(self._enqueue(state, data, rows, eps, rng, batch_size))
 
+    _IO_SLOTS = 4          # output buffers in rotation (at most two calls are in flight in sample/bench)
+
+    def _io_slot(self, nbytes, dev):
+        """A device output buffer and its pinned host mirror, reused round-robin across calls (all
+        slots are allocated by the first call, so later calls allocate nothing)."""
+        ring = self.__dict__.setdefault('_io_ring', [])
+        if not ring:
+            ring.extend({'dev': None, 'host': None, 'ev': torch.cuda.Event(), 'busy': None}
+                        for _ in range(self._IO_SLOTS))
+        i = self.__dict__.get('_io_next', 0)
+        self._io_next = i + 1
+        slot = ring[i % self._IO_SLOTS]
+        if slot['busy'] is not None:    # an uncollected call keeps its buffers; the slot gets new ones
+            slot.update(dev=None, host=None, ev=torch.cuda.Event(), busy=None)
+        if slot['dev'] is None or slot['dev'].numel() < nbytes:
+            cap = max(1 << 16, 1 << (int(nbytes) - 1).bit_length())
+            for sl in ring:                          # busy slots grow when their turn comes
+                if sl['busy'] is None and (sl['dev'] is None or sl['dev'].numel() < cap):
+                    sl['dev'] = torch.empty(cap, dtype=torch.uint8, device=dev)
+                    sl['host'] = torch.empty(cap, dtype=torch.uint8, pin_memory=True)
+        return slot
+
+    def _call_template(self, Xd, Yd, W, b, batch_size, D, K, C):
+        """hmcx_sampler_args fields that stay fixed from call to call (cached per data/state)."""
+        key = (Xd.data_ptr(), Yd.data_ptr(), W.data_ptr(), b.data_ptr(), batch_size, C, self.path_length,
+               self.seed, self.chain)
+        tpl = self.__dict__.get('_tpl')
+        if tpl is None or tpl[0] != key:
+            a = nat.SamplerArgs()
+            a.dtype = self.model.code
+            a.B, a.D, a.K, a.C = batch_size, D, K, C
+            a.alpha = self.model.alpha
+            a.log_prior = self._log_prior()
+            a.X, a.Y = ptr(Xd), ptr(Yd)
+            a.noise_mode = nat.NOISE_BUFFER if self.noise == 'numpy' else nat.NOISE_PHILOX
+            a.seed, a.chain0 = self.seed, self.chain
+            a.path_length = self.path_length
+            a.W, a.b = ptr(W), ptr(b)
+            self._tpl = tpl = (key, a)
+        return tpl[1]
+
     def _enqueue(self, state, data, rows, eps, rng, batch_size):
         """Prepare the schedule of len(rows) steps and enqueue them (one hmcx_sghmc_run call) without
-        waiting: the returned handle is read back by _collect.  A caller may enqueue the next call
-        before collecting this one — the state stays on the device and stream order keeps the calls
-        in sequence — so the host work of one call overlaps the device work of the previous one."""
+        waiting: the outputs travel back into a pinned host buffer behind the call (stream-ordered)
+        and a HIP event marks their arrival.  _collect waits on that event only, so a caller may
+        enqueue the next call before collecting this one — the state stays on the device, stream
+        order keeps the calls in sequence, and the host work of call k+1 overlaps the device work of
+        call k."""
+        mark = _marks if _HOST_PROF else None
+        if mark is not None:
+            mark.append(('start', time.perf_counter()))
         Xd, Yd = data
         W, b = state['weights'], state['bias']
         C = self.chains
@@ -101,50 +155,83 @@ class sghmc(sgmcmc):
         P = D * K + K
         n_steps = len(rows)
         t0 = len(self.trace) if self.trace is not None else 0
-        n_iter, u, noise, noise_off = self._schedule(n_steps, eps, rng, P)
-        n_iter, u, noise_off = (np.ascontiguousarray(x.reshape(-1)) for x in (n_iter, u, noise_off))
+        nsc = n_steps * C
+        philox = self.noise == 'philox'
+        if philox:                      # the C call draws the Philox schedule itself (out_L: the L's)
+            L_out = np.empty(nsc)
+            n_iter = u = noise = noise_off = None
+        else:
+            n_iter, u, noise, noise_off = self._schedule(n_steps, eps, rng, P)
+            n_iter, u, noise_off = (np.ascontiguousarray(x.reshape(-1)) for x in (n_iter, u, noise_off))
+        if mark is not None:
+            mark.append(('schedule', time.perf_counter()))
         dev = self.model.device
         noise_d = torch.from_numpy(noise).to(dev) if noise is not None else None
-        out_f = torch.empty(4 * n_steps * C, dtype=torch.float64, device=dev)     # A, ll, E (2)
-        out_acc = torch.empty(n_steps * C, dtype=torch.int32, device=dev)
-        out_A, out_ll, out_E = out_f[:n_steps * C], out_f[n_steps * C:2 * n_steps * C], out_f[2 * n_steps * C:]
+        nbytes = 32 * nsc + 4 * nsc + 4                  # A, ll, E (2) f64 | accepted i32 | abort i32
+        slot = self._io_slot(nbytes, dev)
+        base = slot['dev'].data_ptr()
         row0 = np.asarray(rows, dtype=np.int64)
         eps_a = np.asarray(eps, dtype=np.float64)
-        a = nat.SamplerArgs()
-        a.dtype = self.model.code
-        a.B, a.D, a.K, a.C = batch_size, D, K, C
+        a = nat.SamplerArgs.from_buffer_copy(self._call_template(Xd, Yd, W, b, batch_size, D, K, C))
         a.n_steps = n_steps
-        a.alpha = self.model.alpha
-        a.log_prior = self._log_prior()
-        a.X, a.Y = ptr(Xd), ptr(Yd)
         a.row0 = row0.ctypes.data_as(nat.c_i64p)
         a.eps = eps_a.ctypes.data_as(nat.c_dblp)
-        a.n_iter = n_iter.ctypes.data_as(nat.c_i32p)
-        a.u_accept = u.ctypes.data_as(nat.c_dblp)
-        a.noise_mode = nat.NOISE_BUFFER if self.noise == 'numpy' else nat.NOISE_PHILOX
-        a.noise = ptr(noise_d)
-        a.noise_off = noise_off.ctypes.data_as(nat.c_i64p)
-        a.seed, a.chain0, a.step_base = self.seed, self.chain, self.global_step & 0xFFFFFFFF
-        a.W, a.b = ptr(W), ptr(b)
-        a.out_A, a.out_accepted, a.out_ll, a.out_E = ptr(out_A), ptr(out_acc), ptr(out_ll), ptr(out_E)
+        if philox:
+            a.out_L = L_out.ctypes.data_as(nat.c_dblp)
+        else:
+            a.n_iter = n_iter.ctypes.data_as(nat.c_i32p)
+            a.u_accept = u.ctypes.data_as(nat.c_dblp)
+            a.noise = ptr(noise_d)
+            a.noise_off = noise_off.ctypes.data_as(nat.c_i64p)
+        a.step_base = self.global_step & 0xFFFFFFFF
+        a.out_A, a.out_ll, a.out_E = base, base + 8 * nsc, base + 16 * nsc
+        a.out_accepted, a.out_abort = base + 32 * nsc, base + 36 * nsc
         out_steps = None
         if self.record_steps:
             out_steps = torch.empty((n_steps, C, P), dtype=self.model.dtype, device=dev)
             a.out_trace = ptr(out_steps)
         ctx = nat.context(dev)
+        if mark is not None:
+            mark.append(('args', time.perf_counter()))
         ctx.check(ctx.lib.hmcx_sghmc_run(ctx.h, a), "hmcx_sghmc_run")
+        if mark is not None:
+            mark.append(('c call', time.perf_counter()))
+        slot['host'][:nbytes].copy_(slot['dev'][:nbytes], non_blocking=True)
+        if mark is not None:
+            mark.append(('d2h copy', time.perf_counter()))
+        slot['ev'].record()
+        if mark is not None:
+            mark.append(('event', time.perf_counter()))
+        if philox and self.trace is not None:                 # while the launch runs
+            if C == 1:
+                self.trace.extend({'L': float(l), 'eps': float(e)} for l, e in zip(L_out, eps))
+            else:
+                Ls = L_out.reshape(n_steps, C)
+                self.trace.extend({'L': Ls[i].copy(), 'eps': float(eps[i])} for i in range(n_steps))
         self.global_step += n_steps
-        return dict(out_f=out_f, out_acc=out_acc, noise_d=noise_d, n_steps=n_steps, C=C, t0=t0, ctx=ctx,
-                    out_steps=out_steps)
+        h = dict(slot=slot, dev=slot['dev'], host=slot['host'], ev=slot['ev'], nbytes=nbytes, n_steps=n_steps,
+                 C=C, t0=t0, ctx=ctx, out_steps=out_steps,
+                 args=a, keep=(row0, eps_a, n_iter, u, noise_off, noise_d, L_out if philox else None))
+        slot['busy'] = h
+        self.__dict__.setdefault('_inflight', []).append(h)
+        return h
 
     def _collect(self, h):
-        """Read back one enqueued call (waits for it) and fill the trace entries of its steps."""
+        """Wait for one enqueued call (its own event, not the stream) and read its outputs; a call
+        whose persistent launch timed out is re-run first (_recover)."""
         n_steps, C = h['n_steps'], h['C']
-        f = h['out_f'].cpu().numpy()
-        acc = h['out_acc'].cpu().numpy().astype(bool)
-        ctx = h['ctx']
-        ctx.check(ctx.lib.hmcx_synchronize(ctx.h), "hmcx_sghmc_run")        # deferred abort check
+        slot = h['slot']
+        h['ev'].synchronize()
         nsc = n_steps * C
+        raw = h['host'][:h['nbytes']].numpy()
+        if raw[36 * nsc:36 * nsc + 4].view(np.int32)[0] and not h.get('recovered'):
+            self._recover(h)
+        raw = raw.copy()
+        if slot['busy'] is h:
+            slot['busy'] = None
+        self._inflight.remove(h)
+        f = raw[:32 * nsc].view(np.float64)
+        acc = raw[32 * nsc:36 * nsc].view(np.int32).astype(bool)
         A, ll, E = f[:nsc], f[nsc:2 * nsc], f[2 * nsc:]
         steps = h['out_steps'].cpu().numpy() if h.get('out_steps') is not None else None
         if C == 1:
@@ -158,6 +245,28 @@ class sghmc(sgmcmc):
                 t['A'] = float(res.A[s]) if C == 1 else res.A[s].copy()
                 t['accepted'] = bool(res.accepted[s]) if C == 1 else res.accepted[s].copy()
         return res
+
+    def _recover(self, h):
+        """The persistent launch of call h timed out in a hand-off (include/hmcx.h hmcx_clear_abort):
+        it, and every call enqueued after it, left W/b untouched.  Lower the abort word and re-run
+        those calls in order, in this process, on the kernel-per-phase path — same schedule, same
+        noise, so the results are those the persistent kernel would have produced.  The context
+        stays on that path afterwards (a misplacement that happened once is likely to recur)."""
+        import sys
+        ctx = h['ctx']
+        torch.cuda.synchronize()
+        ctx.clear_abort()
+        print("hmcx: persistent SGHMC hand-off timed out; re-running %d call(s) on the kernel-per-phase "
+              "path" % (len(self._inflight) - self._inflight.index(h)), file=sys.stderr)
+        ctx.set_sghmc_path(1)
+        for x in self._inflight[self._inflight.index(h):]:
+            a = x['args']
+            a.out_abort = None
+            ctx.check(ctx.lib.hmcx_sghmc_run(ctx.h, a), "hmcx_sghmc_run (recovery)")
+            x['host'][:x['nbytes']].copy_(x['dev'][:x['nbytes']])
+            x['host'][36 * x['n_steps'] * x['C']:x['nbytes']].zero_()
+            x['recovered'] = True
+        torch.cuda.synchronize()
 
     def _run_mlp(self, state, data, rows, eps, rng, batch_size):
         """MLP steps through hmcx_mlp_sghmc_run (hmcx_mlp.hip): same schedule and noise layout as the

@@ -153,7 +153,8 @@ typedef struct hmcx_sampler_args {
   const int64_t* row0;     /* host [n_steps]                                           */
   const double* eps;       /* host [n_steps]  step size used by step s                */
   const int32_t* n_iter;   /* host [n_steps*C] SGHMC leapfrog iterations max(0, L-1)   */
-  const double* u_accept;  /* host [n_steps*C] accept uniforms (SGHMC)                 */
+  const double* u_accept;  /* host [n_steps*C] accept uniforms (SGHMC); both NULL in    */
+                           /* PHILOX mode: drawn by the call (path_length, out_L)       */
   const uint8_t* want_ll;  /* host [n_steps] or NULL: SGLD computes ll(q_new) after s  */
   int noise_mode;
   const double* noise;     /* device, BUFFER mode                                      */
@@ -172,11 +173,34 @@ typedef struct hmcx_sampler_args {
   void* out_trace;         /* device [n_steps][C][D*K+K] (dtype) or NULL: the state     */
                            /* after every step (weights row-major, then bias) — the rows */
                            /* of the HDF5 backend (sghmc_multicore.py:49-51)            */
+  int32_t* out_abort;      /* device [1] or NULL (SGHMC): 0, or 1 when a persistent launch */
+                           /* timed out in a hand-off (or followed one that did) and left */
+                           /* W/b untouched — see hmcx_clear_abort.  NULL: the check is    */
+                           /* deferred to the next call / hmcx_synchronize instead.       */
+  double path_length;      /* SGHMC, PHILOX mode with n_iter == u_accept == NULL: the call */
+  double* out_L;           /* draws its own schedule (hmcx_philox_schedule, this path     */
+                           /* length); out_L (host [n_steps*C] or NULL) receives the L's  */
 } hmcx_sampler_args;
 
 /* Replaces hamiltonian/inference/{cpu,gpu}/sghmc.py:19-39 (step, with the A1 completion:
  * momentum ~ N(0,1), MH accept min(1, exp(E_cur - E_new)) from cpu/hmc.py:67-87). */
 int hmcx_sghmc_run(hmcx_ctx* ctx, const hmcx_sampler_args* a);
+
+/* Persistent-kernel hand-off timeouts (single-chain SGHMC).  A launch whose workgroups time out
+ * waiting for each other (they were not co-resident, or not placed on the XCDs the kernel assumes)
+ * writes nothing to W/b and raises the context's abort word; every later persistent launch sees the
+ * raised word and returns at once, also without touching W/b.  The caller re-runs those calls (in
+ * order, e.g. on the kernel-per-phase path: hmcx_set_sghmc_path(ctx, 1)) after hmcx_clear_abort,
+ * which lowers the word (stream-ordered) and drops the deferred checks still pending. */
+int hmcx_clear_abort(hmcx_ctx* ctx);
+
+/* Host-side Philox schedule of noise='philox' SGHMC steps (sghmc.py:25 path length, :36 accept
+ * uniform), bit-identical to the device generator: for step s < n_steps and chain c < C
+ *   L[s*C+c] = ceil(2·u_path·path_length / eps[s]),  n_iter = max(0, L − 1),  u = u_accept
+ * with u_path / u_accept = Philox(seed, chain0 + c, step_base + s, SLOT_PATH / SLOT_ACCEPT, 0).
+ * All arrays host.  Returns HMCX_EINVAL for a non-finite or oversized path length. */
+int hmcx_philox_schedule(uint64_t seed, uint32_t chain0, int C, uint32_t step_base, int n_steps,
+                         double path_length, const double* eps, double* L, int32_t* n_iter, double* u);
 
 /* Replaces hamiltonian/inference/cpu/sgld.py:31-46 (step): p = N(0,(2ε)²) − ½ε∇U; q += p.
  * With pW/pb set: hamiltonian/inference/gpu/sgld.py:11-20, p = ν⊙p_prev − ½ε∇U with

@@ -93,6 +93,22 @@ def test_philox_known_answer(nat):
     assert u == expect
 
 
+def test_philox_schedule_matches_vectorised_twin(nat):
+    """hmcx_philox_schedule (one host C call per sampler call) equals the NumPy twin of the device
+    generator, including the uint32 wrap of chain and step ids."""
+    eps = np.array([1e-3, 5e-4, 1e-3, 2e-3, 1e-3])
+    for seed, chain0, C, step0 in ((20251015, 0, 1, 0), (7, 0xFFFFFFFE, 3, 0xFFFFFFFD), (11, 64, 16, 1234567)):
+        L, n_iter, u = nat.philox_schedule(seed, chain0, C, step0, 1e-2, eps)
+        g = ((step0 + np.arange(len(eps))) & 0xFFFFFFFF)[:, None]
+        ch = ((chain0 + np.arange(C)) & 0xFFFFFFFF)[None, :]
+        uL = nat.philox_uniforms_chains(seed, ch, g, nat.SLOT_PATH)
+        np.testing.assert_array_equal(L, np.ceil(2 * uL * 1e-2 / eps[:, None]))
+        np.testing.assert_array_equal(n_iter, np.maximum(0, L - 1).astype(np.int32))
+        np.testing.assert_array_equal(u, nat.philox_uniforms_chains(seed, ch, g, nat.SLOT_ACCEPT))
+    with pytest.raises(nat.HmcxError):
+        nat.philox_schedule(1, 0, 1, 0, 1e-2, np.array([0.0]))
+
+
 def test_python_surface_imports():
     import hamiltonian.inference.gpu.sghmc as m1
     import hamiltonian.inference.gpu.sgld as m2
