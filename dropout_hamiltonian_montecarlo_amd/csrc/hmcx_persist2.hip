@@ -71,6 +71,9 @@ struct Q2Args {
   int al2;                                  // row teams share an XCD (xmap): A-round stores plain
   int prefetch;                             // 1: next step's tile/labels loaded during the accept round
   int acc1;                                 // 1: accept partials polled in one batch (HMCX_P2_ACC1)
+  int bar;                                  // 1: round B is an all-reduce by redundant reads (every feature-
+                                            // team member sums all Gr partials of the WHOLE slice and updates
+                                            // it identically) — no B-AG round (HMCX_P2_BAR, default on)
   int* abort_flag;                          // the context's sticky abort word (hmcx_clear_abort)
   int force_abort;                          // HMCX_P2_FORCE_ABORT=<step>: the last workgroup raises the
                                             // abort word at that step (tests the recovery path); −1 off
@@ -183,6 +186,70 @@ __device__ inline bool poll(__amdgpu_buffer_rsrc_t rs, int base0, int pstride, i
                             V* dst = nullptr, int dstride = 0) {
   return np <= 8 ? poll_nb<1, SUM, V, AUX>(rs, base0, pstride, np, pskip, off, valid, ep, sum, abort_flag, dst, dstride)
                  : poll_nb<2, SUM, V, AUX>(rs, base0, pstride, np, pskip, off, valid, ep, sum, abort_flag, dst, dstride);
+}
+
+// NI items per thread (item j at granule offset off[j] of every producer block, valid bit j of vmask),
+// each summed over producers p < np in producer order: NI·8·NB loads per pass in one batch.
+// false on timeout/abort.
+// `work()` runs once while the first batch of loads is in flight (independent work hidden behind the
+// round's latency).
+template <int NI, int NB, typename Work>
+__device__ inline bool polln_nb(__amdgpu_buffer_rsrc_t rs, int base0, int pstride, int np, const int* off,
+                                unsigned vmask, unsigned ep, double* sum, int* abort_flag, Work work) {
+  constexpr int N = 8 * NB, M = NI * N;
+  static_assert(M <= 64, "pending mask");
+  unsigned long long pend = 0;
+  int o[M];
+#pragma unroll
+  for (int u = 0; u < M; ++u) {
+    const int j = u / N, p = u - j * N;
+    const bool want = ((vmask >> j) & 1u) && p < np;
+    pend |= want ? 1ull << u : 0ull;
+    o[u] = (base0 + (want ? p * pstride + off[j] : 0)) * 16;
+  }
+  double val[M];
+#pragma unroll
+  for (int u = 0; u < M; ++u) val[u] = 0.0;
+  unsigned long long t0 = 0;
+  bool worked = false;
+  for (int spins = 0; pend; ++spins) {
+    gran_t v[M];
+#pragma unroll
+    for (int u = 0; u < M; ++u) v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, o[u], 0, 16 /* sc1 */);
+    if (spins == 0) work();
+    worked = true;
+#pragma unroll
+    for (int u = 0; u < M; ++u)
+      if (((pend >> u) & 1ull) && v[u].y == ep && v[u].w == ep) {
+        val[u] = decode(v[u]);
+        pend &= ~(1ull << u);
+      }
+    if (!pend) break;
+    if (spins == 0) t0 = __builtin_amdgcn_s_memrealtime();
+    if ((spins & 63) == 63 &&
+        (__builtin_amdgcn_s_memrealtime() - t0 > QTIMEOUT ||
+         __hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+      __hip_atomic_store(abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    if (HMCX_P2_SLEEP) __builtin_amdgcn_s_sleep(1);
+  }
+  if (!worked) work();
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    double acc = val[j * N];
+#pragma unroll
+    for (int p = 1; p < N; ++p)
+      if (p < np) acc += val[j * N + p];
+    sum[j] = acc;
+  }
+  return true;
+}
+template <int NI, typename Work>
+__device__ inline bool polln(__amdgpu_buffer_rsrc_t rs, int base0, int pstride, int np, const int* off, unsigned vmask,
+                             unsigned ep, double* sum, int* abort_flag, Work work) {
+  return np <= 8 ? polln_nb<NI, 1>(rs, base0, pstride, np, off, vmask, ep, sum, abort_flag, work)
+                 : polln_nb<NI, 2>(rs, base0, pstride, np, off, vmask, ep, sum, abort_flag, work);
 }
 
 // Spread gather: the (producer, item) pairs of a round are dealt over ALL threads of the workgroup
@@ -446,9 +513,12 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
   unsigned long long* profacc = reinterpret_cast<unsigned long long*>(ish + 4);   // [16]
   double* stg = reinterpret_cast<double*>(profacc + 16);                             // [QSTAGE] spread gathers
   T* zbuf = reinterpret_cast<T*>(stg + QSTAGE);                                      // [Fo·KC + 16] noise
+  T* pWs = zbuf + Fo * 16 + 16;                       // [BfP][16] momentum of the whole slice (bar)
   // friction noise by the waves that do not poll A-RS (threads from NZ0 on), when they fit
   const int NZ0 = ((nro * KC + 63) / 64) * 64;
   const bool zoff = a.zoff && !(a.spread & 1) && NZ0 + Fo * KC + K <= QTH;
+  // B all-reduce (a.bar) needs the owners' noise in LDS (zoff) to fold it into their partials
+  const bool bar = a.bar && zoff;
   const auto all_items = [](int, int) { return true; };
 
   // owned weight of this thread: feature fo0 + od, class ok (thread t = od·KC + ok)
@@ -604,7 +674,9 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
             const int e = 4 * g + q;
             if (e < feat0 * K || e >= (feat0 + nfeat) * K) continue;
             const int i = e / K - feat0, k = e - (e / K) * K;
-            Wf[i * 16 + k] = Wf[i * 16 + k] + eps * noise_at<T>(a, s, 0u, (uint32_t)e, z4);
+            const T p0 = noise_at<T>(a, s, 0u, (uint32_t)e, z4);
+            Wf[i * 16 + k] = Wf[i * 16 + k] + eps * p0;
+            if (bar) pWs[i * 16 + k] = p0;
           }
         }
         if (own) wv = wv + eps * pw;
@@ -729,6 +801,12 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
         ++ep;
         const int reg = a.oXB + (((int)(uB & 1) * Gf + f) * Gr + r) * NXB;
         if (tid < HA) put_t(a.fl2, rs, reg + tid, hv, ep);
+        // bar: the owner of an element folds its friction noise into its partial — Σ partials − 2z, so
+        // ε·(−(Σ − 2z − αw)) = ε·g + 2ε·z (sghmc.py:31,34) arrives with the all-reduce and no other
+        // member has to draw that noise
+        const auto bpart = [&](int d, int k, double v) -> double {
+          return (bar && d >= fo0 && d < fo0 + nfo && k < K) ? v - 2.0 * (double)zbuf[(d - fo0) * KC + k] : v;
+        };
         const int nkp = (Br / 4) / WPB;
         for (int item = wave; item < MTB * WPB; item += QNW) {
           const int mt = item % MTB, part = item / MTB;
@@ -738,7 +816,7 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
               const int d = mt * 16 + M::row(lane, q);
-              if (d < nfeat && lr < KC) put_t(a.fl2, rs, reg + HA + d * KC + lr, (double)c[q], ep);
+              if (d < nfeat && lr < KC) put_t(a.fl2, rs, reg + HA + d * KC + lr, bpart(d, lr, (double)c[q]), ep);
             }
           } else {
 #pragma unroll
@@ -751,13 +829,58 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
             const int i = e / KC, k = e - (e / KC) * KC;
             T v = Zp[i * 16 + k];
             for (int q = 1; q < WPB; ++q) v += Zp[(q * BfP + i) * 16 + k];
-            put_t(a.fl2, rs, reg + HA + e, (double)v, ep);
+            put_t(a.fl2, rs, reg + HA + e, bpart(i, k, (double)v), ep);
           }
         }
         const int base0 = a.oXB + ((int)(uB & 1) * Gf + f) * Gr * NXB;
         ++uB;
         tstamp(s, it, 4);
         prof.stamp(7);
+        if (bar) {
+          // all-reduce by redundant reads: items [0, HA) header, [HA, HA + nfeat·KC) the slice's gradient
+          // (noise folded in by the owners); every member sums the Gr partials of every item in producer
+          // order and applies the same update to the whole slice (momentum pWs, position Wf), so no B-AG
+          // round is needed
+          const int ni = HA + nfeat * KC;
+          bool ok = true;
+          double kl = 0.0;
+          for (int i0 = tid; i0 < ni; i0 += 2 * QTH) {
+            int off[2] = {i0, i0 + QTH};
+            const unsigned vm = 1u | (off[1] < ni ? 2u : 0u);
+            double sm[2];
+            ok = polln<2>(rs, base0, NXB, Gr, off, vm, ep, sm, a.abort_flag, []() {});
+            if (!ok) break;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              const int i = off[j];
+              if (i >= ni) continue;
+              if (i < HA) { hdr[i] = sm[j]; continue; }
+              const int m = i - HA, d = m / KC, k = m - (m / KC) * KC;
+              if (k >= K) continue;
+              const int l = d * 16 + k;
+              const T w = Wf[l];
+              const T gz = -((T)sm[j] - alpha * w);                   // softmax.py:57-58 gradient + 2z
+              const T p = ome * pWs[l] + eps * gz;                     // sghmc.py:31,34
+              pWs[l] = p;
+              if (!last) Wf[l] = w + eps * p;                          // sghmc.py:32
+              else if (d >= fo0 && d < fo0 + nfo) kl += (double)p * (double)p;
+            }
+          }
+          if (!all_ok(ok, ish)) return;
+          tstamp(s, it, 5);
+          prof.stamp(8);
+          if (tid < K) {                                                      // bias sub-step, replicated
+            const T gr = -((T)hdr[tid] - alpha * bpsh[tid]);
+            pbsh[tid] = (ome * pbsh[tid] + eps * gr) + nsc * zb;
+            bsh[tid] = bpsh[tid];
+          }
+          if (last) {
+            ll_last = hdr[KC];                                                // ll(q_new) on this batch
+            kin1 = kl;
+            break;
+          }
+          continue;
+        }
         // threads [0, nfo·KC): owned gradient element; threads [nfo·KC, nfo·KC + HA): header
         const int ng = nfo * KC;
         double sum = 0.0;
@@ -834,6 +957,7 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
       }
     }
 
+    if (bar && n > 0 && own) wv = Wf[wl];            // the slice lives in LDS (last write: barrier-ed)
     // ===== accept (hmc.py:67-71): all-gather of the kinetic / log-likelihood partials
     prof.stamp(10);
     const double kin1w = wsum(kin1, dsh);
@@ -923,6 +1047,7 @@ static size_t p2_lds(const PersistPlan2& p, int K, size_t ts) {
                    4 * (size_t)p.Ro * 16 + 64);
   t = (t + 15) & ~(size_t)15;
   t += 8 * ((size_t)p.Ro + 32) + 16 + 16 * 8 + 8 * (size_t)QSTAGE + ts * ((size_t)p.Fo * 16 + 16);
+  t += ts * ((size_t)p.BfP * 16);                                            // pWs (bar)
   (void)K;
   return t;
 }
@@ -1043,6 +1168,8 @@ int sghmc_p2_t(hmcx_ctx* ctx, const hmcx_sampler_args* s, const PersistPlan2& pl
     a.prefetch = pf_env == 1 ? 1 : 0;
     static const int acc1_env = getenv("HMCX_P2_ACC1") ? atoi(getenv("HMCX_P2_ACC1")) : 1;
     a.acc1 = acc1_env == 1 ? 1 : 0;
+    static const int bar_env = getenv("HMCX_P2_BAR") ? atoi(getenv("HMCX_P2_BAR")) : 1;
+    a.bar = bar_env == 1 ? 1 : 0;
   }
   a.abort_flag = ctx->abort_dev;
   a.force_abort = getenv("HMCX_P2_FORCE_ABORT") ? atoi(getenv("HMCX_P2_FORCE_ABORT")) : -1;
