@@ -1155,10 +1155,16 @@ int sghmc_p2_t(hmcx_ctx* ctx, const hmcx_sampler_args* s, const PersistPlan2& pl
     static const int spread_env = getenv("HMCX_P2_SPREAD") ? atoi(getenv("HMCX_P2_SPREAD")) : 2;
     a.spread = fits ? spread_env : 0;
     a.zoff = !(getenv("HMCX_P2_ZOFF") && getenv("HMCX_P2_ZOFF")[0] == '0');
-    // HMCX_P2_XMAP: 1 (default) row teams on one XCD; 0 identity map; 2 = deliberately MISPLACED (test
-    // knob, read per call): identity map with the row-team rounds still published into one XCD's L2,
-    // so members on other XCDs never see them — the launch times out (4 s) and aborts
-    const int xmap_env = getenv("HMCX_P2_XMAP") ? atoi(getenv("HMCX_P2_XMAP")) : 1;
+    static const int bar_env = getenv("HMCX_P2_BAR") ? atoi(getenv("HMCX_P2_BAR")) : 1;
+    a.bar = bar_env == 1 ? 1 : 0;
+    // HMCX_P2_XMAP: which team shares an XCD (workgroups are dealt to the XCDs round-robin).  0 = identity
+    // map: each FEATURE team on one XCD, its B rounds kept in that XCD's L2 (default with the B all-
+    // reduce: its redundant reads, 8x the bytes of the other rounds, then stay off the fabric — same
+    // speed, 11.1 -> 4.5 MB of fabric traffic per leapfrog); 1 = each ROW team on one XCD (default
+    // without it); 2 = deliberately MISPLACED (test knob, read per call): identity map with the row-team
+    // rounds published into one XCD's L2, so members on other XCDs never see them — the launch times
+    // out (4 s) and aborts
+    const int xmap_env = getenv("HMCX_P2_XMAP") ? atoi(getenv("HMCX_P2_XMAP")) : (a.bar ? 0 : 1);
     a.xmap = (xmap_env == 1 && (pl.Gr * pl.Gf) % 8 == 0) ? 1 : 0;
     static const int fl2_env = getenv("HMCX_P2_FL2") ? atoi(getenv("HMCX_P2_FL2")) : 1;
     a.fl2 = (fl2_env == 1 && !a.xmap && pl.Gf % 8 == 0 && xmap_env != 2) ? 1 : 0;
@@ -1168,8 +1174,6 @@ int sghmc_p2_t(hmcx_ctx* ctx, const hmcx_sampler_args* s, const PersistPlan2& pl
     a.prefetch = pf_env == 1 ? 1 : 0;
     static const int acc1_env = getenv("HMCX_P2_ACC1") ? atoi(getenv("HMCX_P2_ACC1")) : 1;
     a.acc1 = acc1_env == 1 ? 1 : 0;
-    static const int bar_env = getenv("HMCX_P2_BAR") ? atoi(getenv("HMCX_P2_BAR")) : 1;
-    a.bar = bar_env == 1 ? 1 : 0;
   }
   a.abort_flag = ctx->abort_dev;
   a.force_abort = getenv("HMCX_P2_FORCE_ABORT") ? atoi(getenv("HMCX_P2_FORCE_ABORT")) : -1;
