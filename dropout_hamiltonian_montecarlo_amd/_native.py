@@ -26,16 +26,18 @@ c_u8p = ctypes.POINTER(ctypes.c_uint8)
 
 
 class SamplerArgs(ctypes.Structure):
+    # host-array fields are plain addresses here (same layout as the typed pointers of include/hmcx.h):
+    # assigning addr(ndarray) costs far less than ndarray.ctypes.data_as on the per-call path
     _fields_ = [("dtype", c_int), ("B", c_int), ("D", c_int), ("K", c_int), ("C", c_int),
                 ("n_steps", c_int), ("alpha", c_double), ("log_prior", c_double),
-                ("X", c_void_p), ("Y", c_void_p), ("row0", c_i64p), ("eps", c_dblp),
-                ("n_iter", c_i32p), ("u_accept", c_dblp), ("want_ll", c_u8p),
-                ("noise_mode", c_int), ("noise", c_void_p), ("noise_off", c_i64p),
+                ("X", c_void_p), ("Y", c_void_p), ("row0", c_void_p), ("eps", c_void_p),
+                ("n_iter", c_void_p), ("u_accept", c_void_p), ("want_ll", c_void_p),
+                ("noise_mode", c_int), ("noise", c_void_p), ("noise_off", c_void_p),
                 ("seed", ctypes.c_uint64), ("chain0", ctypes.c_uint32), ("step_base", ctypes.c_uint32),
                 ("W", c_void_p), ("b", c_void_p), ("out_A", c_void_p), ("out_accepted", c_void_p),
                 ("out_ll", c_void_p), ("out_E", c_void_p), ("pW", c_void_p), ("pb", c_void_p),
                 ("out_trace", c_void_p), ("out_abort", c_void_p), ("path_length", c_double),
-                ("out_L", c_dblp)]
+                ("out_L", c_void_p)]
 
 
 class MvnArgs(ctypes.Structure):
@@ -185,9 +187,17 @@ class Context:
             raise HmcxError("hmcx_create failed (%d)" % rc)
         self.h = h
 
+    _bound = None
+
     def bind_stream(self):
-        s = torch.cuda.current_stream(self.device)
-        self.lib.hmcx_set_stream(self.h, c_void_p(s.cuda_stream))
+        """Run on torch's current stream of this device (set again only when it has changed)."""
+        try:
+            raw = torch._C._cuda_getCurrentRawStream(self.device.index)
+        except AttributeError:
+            raw = torch.cuda.current_stream(self.device).cuda_stream
+        if raw != self._bound:
+            self.lib.hmcx_set_stream(self.h, c_void_p(raw))
+            self._bound = raw
 
     def check(self, rc, what):
         if rc != 0:
@@ -233,13 +243,16 @@ def context(device=None):
     """Context for `device` (default: torch's current device)."""
     if device is None:
         device = torch.cuda.current_device() if torch.cuda.is_available() else 0
-    idx = device if isinstance(device, int) else (torch.device(device).index or 0)
-    with _lock:
-        ctx = _ctxs.get(idx)
+    idx = device if isinstance(device, int) else (
+        device.index or 0 if isinstance(device, torch.device) else torch.device(device).index or 0)
+    ctx = _ctxs.get(idx)
     if ctx is None:
-        ctx = Context(idx)
         with _lock:
-            _ctxs[idx] = ctx
+            ctx = _ctxs.get(idx)
+        if ctx is None:
+            ctx = Context(idx)
+            with _lock:
+                _ctxs[idx] = ctx
     ctx.bind_stream()
     return ctx
 
@@ -258,6 +271,11 @@ def _release_contexts():
 
 def ptr(t):
     return c_void_p(t.data_ptr()) if t is not None else c_void_p()
+
+
+def addr(a):
+    """Address of a host ndarray's data (None for None)."""
+    return a.__array_interface__['data'][0] if a is not None else None
 
 
 def dtype_code(dt):

@@ -170,19 +170,23 @@ class sghmc(sgmcmc):
         nbytes = 32 * nsc + 4 * nsc + 4                  # A, ll, E (2) f64 | accepted i32 | abort i32
         slot = self._io_slot(nbytes, dev)
         base = slot['dev'].data_ptr()
+        if mark is not None:
+            mark.append(('io slot', time.perf_counter()))
         row0 = np.asarray(rows, dtype=np.int64)
         eps_a = np.asarray(eps, dtype=np.float64)
         a = nat.SamplerArgs.from_buffer_copy(self._call_template(Xd, Yd, W, b, batch_size, D, K, C))
+        if mark is not None:
+            mark.append(('template', time.perf_counter()))
         a.n_steps = n_steps
-        a.row0 = row0.ctypes.data_as(nat.c_i64p)
-        a.eps = eps_a.ctypes.data_as(nat.c_dblp)
+        a.row0 = nat.addr(row0)
+        a.eps = nat.addr(eps_a)
         if philox:
-            a.out_L = L_out.ctypes.data_as(nat.c_dblp)
+            a.out_L = nat.addr(L_out)
         else:
-            a.n_iter = n_iter.ctypes.data_as(nat.c_i32p)
-            a.u_accept = u.ctypes.data_as(nat.c_dblp)
+            a.n_iter = nat.addr(n_iter)
+            a.u_accept = nat.addr(u)
             a.noise = ptr(noise_d)
-            a.noise_off = noise_off.ctypes.data_as(nat.c_i64p)
+            a.noise_off = nat.addr(noise_off)
         a.step_base = self.global_step & 0xFFFFFFFF
         a.out_A, a.out_ll, a.out_E = base, base + 8 * nsc, base + 16 * nsc
         a.out_accepted, a.out_abort = base + 32 * nsc, base + 36 * nsc
@@ -190,9 +194,11 @@ class sghmc(sgmcmc):
         if self.record_steps:
             out_steps = torch.empty((n_steps, C, P), dtype=self.model.dtype, device=dev)
             a.out_trace = ptr(out_steps)
-        ctx = nat.context(dev)
         if mark is not None:
             mark.append(('args', time.perf_counter()))
+        ctx = nat.context(dev)
+        if mark is not None:
+            mark.append(('context', time.perf_counter()))
         ctx.check(ctx.lib.hmcx_sghmc_run(ctx.h, a), "hmcx_sghmc_run")
         if mark is not None:
             mark.append(('c call', time.perf_counter()))

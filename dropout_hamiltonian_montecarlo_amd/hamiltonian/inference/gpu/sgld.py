@@ -71,12 +71,12 @@ class sgld(sgmcmc):
         a.alpha = self.model.alpha
         a.log_prior = self._log_prior()
         a.X, a.Y = ptr(Xd), ptr(Yd)
-        a.row0 = row0.ctypes.data_as(nat.c_i64p)
-        a.eps = eps_a.ctypes.data_as(nat.c_dblp)
-        a.want_ll = want.ctypes.data_as(nat.c_u8p)
+        a.row0 = nat.addr(row0)
+        a.eps = nat.addr(eps_a)
+        a.want_ll = nat.addr(want)
         a.noise_mode = nat.NOISE_BUFFER if self.noise == 'numpy' else nat.NOISE_PHILOX
         a.noise = ptr(noise_d)
-        a.noise_off = noise_off.ctypes.data_as(nat.c_i64p)
+        a.noise_off = nat.addr(noise_off)
         a.seed, a.chain0, a.step_base = self.seed, self.chain, self.global_step & 0xFFFFFFFF
         a.W, a.b = ptr(W), ptr(b)
         if self.variant == 'gpu':

@@ -93,12 +93,12 @@ def test_abort_word_reported_through_c_abi(monkeypatch):
         a.dtype, a.B, a.D, a.K, a.C, a.n_steps = m.code, c["B"], c["D"], c["K"], 1, 3
         a.alpha, a.log_prior = m.alpha, s._log_prior()
         a.X, a.Y = nat.ptr(data[0]), nat.ptr(data[1])
-        a.row0 = rows.ctypes.data_as(nat.c_i64p)
-        a.eps = eps.ctypes.data_as(nat.c_dblp)
-        a.n_iter = n_iter.ctypes.data_as(nat.c_i32p)
-        a.u_accept = u.ctypes.data_as(nat.c_dblp)
+        a.row0 = nat.addr(rows)
+        a.eps = nat.addr(eps)
+        a.n_iter = nat.addr(n_iter)
+        a.u_accept = nat.addr(u)
         a.noise_mode = nat.NOISE_PHILOX
-        a.noise_off = noff.reshape(-1).ctypes.data_as(nat.c_i64p)
+        a.noise_off = nat.addr(noff.reshape(-1))
         a.seed, a.chain0, a.step_base = 3, 0, 0
         a.W, a.b = nat.ptr(st["weights"]), nat.ptr(st["bias"])
         a.out_A, a.out_ll, a.out_E = out.data_ptr(), out.data_ptr() + 64, out.data_ptr() + 128
