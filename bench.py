@@ -11,7 +11,8 @@ Workload (BASELINE config 2 at N=1, config 4 at N=8): synthetic MNIST-shaped dat
 (X = rand(60000, 784), one-hot labels over 10 classes), batch 500, α = 0.01, ε = 1e-3,
 λ = 1e-2 (E[L] ≈ 10.5), zero start, one chain per GPU, float64 (the reference's dtype),
 device Philox noise.  Ranks run independent chains (no communication while sampling); after the
-timed region one all-gather (RCCL) moves the per-chain log-likelihood traces to rank 0 for R̂/ESS.
+timed region an untimed diagnostics run returns every step's state, and one all-gather (RCCL) moves
+each chain's per-parameter Welford mean / M2 and thinned trace to rank 0 for R̂ / split-R̂ / ESS.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
@@ -32,6 +33,7 @@ D, K, B, N_DATA = 784, 10, 500, 60000
 P = D * K + K
 ALPHA, EPS, LAMBDA = 0.01, 1e-3, 1e-2
 FLOP_PER_LEAPFROG = 4.0 * B * D * K          # X·W and Xᵀ·diff: 15.68 MFLOP
+DIAG_STEPS, DIAG_THIN = 240, 4               # untimed diagnostics run after the timed region
 MFMA_PEAK_TFLOPS = {"f64": 78.6, "f32": 157.3}   # dense MFMA, MI355X spec (f32: MI355X_MICROARCH.md)
 
 
@@ -306,8 +308,9 @@ def main():
     X, Y = synthetic_data(0)
     model = softmax({"alpha": ALPHA}, dtype=dtype, device=dev)
     model.ctx.set_sghmc_path({"auto": 0, "kernels": 1, "persistent": 2}[args.path])
+    chain0, _ = parallel.chain_block(world, rank, world)     # one chain per rank: Philox key chain0
     s = sghmc(model, {"weights": np.zeros((D, K)), "bias": np.zeros(K)}, path_length=LAMBDA, step_size=EPS,
-              noise="philox", seed=20251015, chain=rank)
+              noise="philox", seed=20251015, chain=chain0)
     s.out = io.StringIO()
     data = s._upload_data(X, Y)                      # dataset resident in HBM before timing
     state = s._init_state()
@@ -373,7 +376,23 @@ def main():
     lf_total = parallel.allreduce_sum(lf_local, device=dev)
     value = lf_total / t_max * P
 
-    # cross-chain diagnostics: one RCCL all-gather of the per-chain ll traces (untimed)
+    # cross-chain diagnostics (untimed, after the timed region): DIAG_STEPS more steps of the same
+    # chain return the state after every step (out_trace); per-parameter Welford mean / M2 and a
+    # thinned trace of every chain travel in ONE all-gather (RCCL over xGMI); rank 0 reports R̂,
+    # split-R̂ and ESS per parameter.  The timed steps' log-likelihood trace is gathered too.
+    s.record_steps = True
+    wf = parallel.Welford((1, P))
+    thin = []
+    done = 0
+    while done < DIAG_STEPS:
+        n = min(CHUNK, DIAG_STEPS - done)
+        st = run(n, args.warmup + args.steps + done).steps        # [n, 1, P]
+        wf.update(st.transpose(1, 0, 2))
+        thin.append(st[DIAG_THIN - 1::DIAG_THIN, 0])
+        done += n
+    s.record_steps = False
+    n_draws, means, M2, tr = parallel.gather_summaries(wf, np.concatenate(thin)[None], device=dev)
+    diag_par = parallel.summary_diagnostics(n_draws, means, M2, tr)
     trace = np.concatenate(lls)[None, :, None]       # [1 chain, T, 1]
     allt = parallel.gather_traces(trace, device=dev)
     diag = parallel.chain_diagnostics(allt) if allt.shape[1] >= 4 else {"rhat": np.nan, "ess": np.nan}
@@ -428,7 +447,10 @@ def main():
                      else "kernel-per-phase sequence of each call (%d call(s) of <= %d steps)" % (n_calls, CHUNK),
                      "launch_ms": launch_ms, "flop_per_launch": flop_per_launch, "calls": n_calls,
                      "leapfrogs_per_launch": lf_local / n_calls},
-        "diagnostics": {"rhat_ll": float(np.ravel(diag["rhat"])[0]), "ess_ll": float(np.ravel(diag["ess"])[0]),
+        "diagnostics": {"per_parameter": diag_par,
+                        "source": "%d untimed steps after the timed region, state after every step; Welford "
+                                  "mean/M2 per parameter and every %dth draw, one all_gather" % (DIAG_STEPS, DIAG_THIN),
+                        "rhat_ll": float(np.ravel(diag["rhat"])[0]), "ess_ll": float(np.ravel(diag["ess"])[0]),
                         "gather": "torch.distributed all_gather (%s)" % (parallel.backend_name() if world > 1 else "local")},
         "cpu_baseline": None,
         "chain_batched": batched,

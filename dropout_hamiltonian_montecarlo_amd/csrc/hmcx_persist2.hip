@@ -79,6 +79,7 @@ struct Q2Args {
                                             // abort word at that step (tests the recovery path); −1 off
   double* out_A; int32_t* out_acc; double* out_ll; double* out_E;
   void* out_trace;                          // [n_steps][P] state after every step, or null
+  void* out_mom;                            // [P] momentum returned by the last step, or null
   unsigned long long* prof;                 // HMCX_PERSIST_PROF=1: per-segment s_memtime totals (workgroup 0)
   unsigned long long* trace;                // HMCX_P2_TRACE=1: [G][P2TR_IT][8] s_memrealtime stamps (step 0)
 };
@@ -505,7 +506,8 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
   T* pbsh = bsh + 16;                                 // [16] pb
   T* b0sh = pbsh + 16;                                // [16] b at step start
   T* bpsh = b0sh + 16;                                // [16] b'
-  size_t off = ((size_t)(reinterpret_cast<char*>(bpsh + 16) - smem) + 15) & ~(size_t)15;
+  T* pb0sh = bpsh + 16;                               // [16] pb drawn at step start
+  size_t off = ((size_t)(reinterpret_cast<char*>(pb0sh + 16) - smem) + 15) & ~(size_t)15;
   double* rowll = reinterpret_cast<double*>(smem + off);  // [Ro] ll of my rows
   double* hdr = rowll + Ro;                               // [16] all-row colsum, ll
   double* dsh = hdr + 16;                                 // [16] reductions
@@ -623,9 +625,11 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
     if (s == 0 || !a.prefetch) load_step_rows<T>(Xs, Yo, Xg, Yg, Br, BfP, BFP, nrow, nfeat, row0, feat0, D, K, Ro, nro, ro0);
     for (int e = tid; e < BfP * 16; e += QTH) Wf0[e] = Wf[e];
     pw = own ? noise1<T>(a, s, 0u, (uint32_t)e_own) : T(0);
+    const T pw0 = pw;
     w0 = wv;
     if (tid < 16) {
       pbsh[tid] = tid < K ? noise1<T>(a, s, 0u, (uint32_t)(D * K + tid)) : T(0);
+      pb0sh[tid] = pbsh[tid];
       b0sh[tid] = bsh[tid];
     }
     const double kin0 = wsum((double)pw * (double)pw, dsh);
@@ -1014,6 +1018,12 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
       wv = w0;
       if (tid < 16) bsh[tid] = b0sh[tid];
     }
+    if (a.out_mom && s == a.n_steps - 1) {                                 // sghmc.py:36-39 returned p
+      T* mo = reinterpret_cast<T*>(a.out_mom);
+      const bool keep_new = acc && n > 0;
+      if (own) mo[e_own] = keep_new ? (bar ? pWs[wl] : pw) : pw0;
+      if (bid == 0 && tid < K) mo[D * K + tid] = keep_new ? pbsh[tid] : pb0sh[tid];
+    }
     if (a.out_trace) {                                                     // sghmc_multicore.py:49-51 row
       T* tr = reinterpret_cast<T*>(a.out_trace) + (size_t)s * a.P;
       if (own) tr[e_own] = wv;
@@ -1045,6 +1055,7 @@ static size_t p2_lds(const PersistPlan2& p, int K, size_t ts) {
   const int ZPN = std::max(WPA * p.Br, WPB * p.BfP) * 16;
   size_t t = ts * ((size_t)p.Br * p.BFP + 2 * (size_t)p.BfP * 16 + (size_t)p.Gf * p.Ro * 16 + ZPN +
                    4 * (size_t)p.Ro * 16 + 64);
+  t += ts * 16;                                                              // pb0sh
   t = (t + 15) & ~(size_t)15;
   t += 8 * ((size_t)p.Ro + 32) + 16 + 16 * 8 + 8 * (size_t)QSTAGE + ts * ((size_t)p.Fo * 16 + 16);
   t += ts * ((size_t)p.BfP * 16);                                            // pWs (bar)
@@ -1179,6 +1190,7 @@ int sghmc_p2_t(hmcx_ctx* ctx, const hmcx_sampler_args* s, const PersistPlan2& pl
   a.force_abort = getenv("HMCX_P2_FORCE_ABORT") ? atoi(getenv("HMCX_P2_FORCE_ABORT")) : -1;
   a.out_A = s->out_A; a.out_acc = s->out_accepted; a.out_ll = s->out_ll; a.out_E = s->out_E;
   a.out_trace = s->out_trace;
+  a.out_mom = s->out_mom;
   static const bool prof_on = getenv("HMCX_PERSIST_PROF") && getenv("HMCX_PERSIST_PROF")[0] == '1';
   unsigned long long* dprof = nullptr;
   if (prof_on) {

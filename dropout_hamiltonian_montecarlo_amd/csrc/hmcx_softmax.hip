@@ -627,6 +627,27 @@ __global__ __launch_bounds__(64) void k_sghmc_accept(AcceptArgs<T> a) {
   }
 }
 
+// Momentum returned by the call's last step (sghmc.py:36-39): p_new (pW/pb after the last iteration)
+// when accepted with at least one iteration, else the momentum drawn at step start (slot 0, as
+// k_sghmc_init draws it).  out [C][D·K + K] (weights row-major, then bias).
+template <typename T>
+__global__ void k_mom_out(InitArgs<T> a, const int32_t* acc, const T* pW, const T* pb, T* out) {
+  const int c = blockIdx.y, K = a.K;
+  const long long P = (long long)a.D * K + K, DK = (long long)a.D * K;
+  const bool keep_new = acc[c] && a.n_iter[c] >= 1;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < P; e += (long long)gridDim.x * blockDim.x) {
+    T v;
+    if (keep_new) {
+      v = e < DK ? pW[(size_t)(e / K) * a.N + c * K + e % K] : pb[c * K + (e - DK)];
+    } else if (a.noise_mode == HMCX_NOISE_BUFFER) {
+      v = (T)a.noise[a.noff[c] + e];
+    } else {
+      v = philox_normal_t<T>(a.seed, a.chain0 + c, a.step, 0u, (uint32_t)e);
+    }
+    out[(size_t)c * P + e] = v;
+  }
+}
+
 __global__ void k_fix_acc(const int32_t* n_iter, const double* u, int32_t* acc, int n) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c < n && n_iter[c] <= 0) acc[c] = u[c] < 1.0;
@@ -1372,7 +1393,10 @@ int sghmc_run_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
     return set_error(ctx, HMCX_EUNSUPPORTED, "persistent SGHMC needs C == 1");
   }
   static const bool no_batch = getenv("HMCX_NO_BATCH") && getenv("HMCX_NO_BATCH")[0] == '1';
-  if (C >= 16 && K == BKC && D % 2 == 0 && !no_batch) return sghmc_batch_t<T>(ctx, s);   // chain-batched GEMMs
+  if (C >= 16 && K == BKC && D % 2 == 0 && !no_batch) {                                // chain-batched GEMMs
+    if (s->out_mom) return set_error(ctx, HMCX_EUNSUPPORTED, "out_mom: single-chain / C < 16 paths only");
+    return sghmc_batch_t<T>(ctx, s);
+  }
   const Tiling t = make_tiling(B, D, K, C);
   const size_t nsc = (size_t)s->n_steps * C;
   Workspace ws(ctx);
@@ -1477,6 +1501,18 @@ int sghmc_run_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
   hipLaunchKernelGGL(k_fix_acc, dim3((unsigned)((nsc + 255) / 256)), dim3(256), 0, st, d_niter, d_u,
                      s->out_accepted, (int)nsc);
   HMCX_HIP(ctx, hipGetLastError());
+  if (s->out_mom) {
+    const int last = s->n_steps - 1;
+    InitArgs<T> ma{};
+    ma.D = D; ma.K = K; ma.C = C; ma.N = N;
+    ma.n_iter = d_niter + (size_t)last * C;
+    ma.noise_mode = s->noise_mode; ma.noise = s->noise; ma.noff = d_noff + (size_t)last * C;
+    ma.seed = s->seed; ma.chain0 = s->chain0; ma.step = s->step_base + (uint32_t)last;
+    const unsigned gx = (unsigned)std::min<long long>(((long long)D * K + K + 255) / 256, 1024);
+    hipLaunchKernelGGL((k_mom_out<T>), dim3(gx, C), dim3(256), 0, st, ma, s->out_accepted + (size_t)last * C,
+                       (const T*)pW, (const T*)pb, (T*)s->out_mom);
+    HMCX_HIP(ctx, hipGetLastError());
+  }
   if ((rc = gs.finish())) return rc;
   return timing_end(ctx, ctx->stream);
 }

@@ -194,6 +194,10 @@ class sghmc(sgmcmc):
         if self.record_steps:
             out_steps = torch.empty((n_steps, C, P), dtype=self.model.dtype, device=dev)
             a.out_trace = ptr(out_steps)
+        out_mom = None
+        if self.__dict__.get('_want_mom'):
+            out_mom = torch.empty((C, P), dtype=self.model.dtype, device=dev)
+            a.out_mom = ptr(out_mom)
         if mark is not None:
             mark.append(('args', time.perf_counter()))
         ctx = nat.context(dev)
@@ -216,7 +220,7 @@ class sghmc(sgmcmc):
                 self.trace.extend({'L': Ls[i].copy(), 'eps': float(eps[i])} for i in range(n_steps))
         self.global_step += n_steps
         h = dict(slot=slot, dev=slot['dev'], host=slot['host'], ev=slot['ev'], nbytes=nbytes, n_steps=n_steps,
-                 C=C, t0=t0, ctx=ctx, out_steps=out_steps,
+                 C=C, t0=t0, ctx=ctx, out_steps=out_steps, out_mom=out_mom,
                  args=a, keep=(row0, eps_a, n_iter, u, noise_off, noise_d, L_out if philox else None))
         slot['busy'] = h
         self.__dict__.setdefault('_inflight', []).append(h)
@@ -245,6 +249,7 @@ class sghmc(sgmcmc):
         else:
             res = RunResult(A.reshape(n_steps, C), acc.reshape(n_steps, C), ll.reshape(n_steps, C),
                             E.reshape(n_steps, C, 2), steps=steps)
+        res.mom = h.get('out_mom')
         if self.trace is not None:
             for s in range(n_steps):
                 t = self.trace[h['t0'] + s]
@@ -338,10 +343,10 @@ class sghmc(sgmcmc):
 
     # ------------------------------------------------------------------ single step (API parity)
     def step(self, state, momentum, rng, **args):                         # sghmc.py:19-39
-        """One SGHMC step on the given minibatch; returns (q, None, acceptprob).
-
-        q is a dict of device tensors.  The final momentum stays on the device (the reference
-        returns it but ``sample`` discards it; draw_momentum redraws it every step)."""
+        """One SGHMC step on the given minibatch; returns (q, p, acceptprob) like the reference:
+        q and p are dicts of device tensors — p is the final momentum when the proposal was
+        accepted, else the momentum drawn at the start of the step (sghmc.py:36-39; the argument
+        `momentum` is ignored there too, the step draws its own)."""
         if self.chains != 1:
             raise HmcxError("step() is the reference's single-chain API; use sample() for chains > 1")
         X, y = args['X_train'], args['y_train']
@@ -349,5 +354,13 @@ class sghmc(sgmcmc):
         st = {var: torch.as_tensor(np.asarray(state[var]) if not isinstance(state[var], torch.Tensor)
                                    else state[var]).to(self.model.device, self.model.dtype).contiguous().clone()
               for var in self.start}
-        res = self._run(st, data, [0], [self.step_size], rng, data[0].shape[0])
-        return st, None, float(res.A[0])
+        self._want_mom = True
+        try:
+            res = self._run(st, data, [0], [self.step_size], rng, data[0].shape[0])
+        finally:
+            self._want_mom = False
+        W = st['weights']
+        D, K = W.shape
+        mom = res.mom.reshape(-1)
+        p = {'weights': mom[:D * K].reshape(D, K), 'bias': mom[D * K:]}
+        return st, p, float(res.A[0])

@@ -40,6 +40,7 @@ class RunResult:
     def __init__(self, A, accepted, ll, E=None, nlp=None, steps=None):
         self.A, self.accepted, self.ll, self.E, self.nlp = A, accepted, ll, E, nlp
         self.steps = steps      # [n_steps, C, P] state after every step (record_steps), else None
+        self.mom = None         # device [C, P] momentum returned by the last step (sghmc.step), else None
 
 
 class sgmcmc:

@@ -180,6 +180,9 @@ typedef struct hmcx_sampler_args {
   double path_length;      /* SGHMC, PHILOX mode with n_iter == u_accept == NULL: the call */
   double* out_L;           /* draws its own schedule (hmcx_philox_schedule, this path     */
                            /* length); out_L (host [n_steps*C] or NULL) receives the L's  */
+  void* out_mom;           /* SGHMC, C < 16, or NULL: device [C][D*K+K] (dtype), the       */
+                           /* momentum the call's LAST step returns (sghmc.py:36-39): the */
+                           /* final p_new if accepted, else the drawn p                   */
 } hmcx_sampler_args;
 
 /* Replaces hamiltonian/inference/{cpu,gpu}/sghmc.py:19-39 (step, with the A1 completion:

@@ -303,3 +303,36 @@ def test_sgld_gpu_variant_step_api():
     for v in start:
         np.testing.assert_allclose(qg[v].cpu().numpy(), qo[v], rtol=1e-10, atol=1e-14)
         np.testing.assert_allclose(pg[v].cpu().numpy(), po[v], rtol=1e-10, atol=1e-14)
+
+
+@pytest.mark.parametrize("path", [1, 2])
+def test_sghmc_step_api_returns_momentum(path):
+    """sghmc.step(state, momentum, rng) returns (q, p, acceptprob) like cpu/sghmc.py:19-39 (A1
+    completion): p is the final momentum of an accepted proposal, else the freshly drawn one.  The
+    hot config (ε = 0.05) rejects some proposals; both cases must match the oracle's step."""
+    softmax, sghmc, _ = _gpu_classes()
+    c = gi.TRAJ_CONFIGS["sghmc_hot"]
+    X, Y = gi.dataset(c["data_seed"], c["N"], c["D"], c["K"])
+    Xb, Yb = X[:c["B"]], Y[:c["B"]]
+    start = {"weights": np.zeros((c["D"], c["K"])), "bias": np.zeros(c["K"])}
+    o = osm.sghmc(om.softmax({"alpha": c["alpha"]}), start, path_length=c["path_length"], step_size=c["step_size"])
+    o.trace = []
+    m = softmax({"alpha": c["alpha"]}, dtype=torch.float64, device="cuda:0")
+    m.ctx.set_sghmc_path(path)
+    try:
+        g = sghmc(m, start, path_length=c["path_length"], step_size=c["step_size"])
+        r1, r2 = np.random.RandomState(5), np.random.RandomState(5)
+        qo, qg = dict(start), dict(start)
+        for i in range(8):
+            np.random.seed(100 + i)
+            qo, po, Ao = o.step(qo, None, r1, X_train=Xb, y_train=Yb)
+            np.random.seed(100 + i)
+            qg, pg, Ag = g.step(qg, None, r2, X_train=Xb, y_train=Yb)
+            assert abs(Ag - Ao) <= 1e-9 * max(1.0, abs(Ao))
+            for v in start:
+                np.testing.assert_allclose(qg[v].cpu().numpy(), qo[v], rtol=1e-9, atol=1e-12)
+                np.testing.assert_allclose(pg[v].cpu().numpy(), po[v], rtol=1e-9, atol=1e-12)
+        acc = [t["accepted"] for t in o.trace]
+        assert any(acc) and not all(acc), acc            # both branches exercised
+    finally:
+        m.ctx.set_sghmc_path(0)

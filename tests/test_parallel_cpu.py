@@ -34,10 +34,35 @@ def test_rhat_ess_known_answers():
 
 
 def test_chain_sharding():
-    from dropout_hamiltonian_montecarlo_amd.parallel import chains_of_rank
+    from dropout_hamiltonian_montecarlo_amd.parallel import chain_block, chains_of_rank
     assert chains_of_rank(8, 0, 8) == [0]
-    assert chains_of_rank(8, 1, 2) == [1, 3, 5, 7]
+    assert chains_of_rank(8, 1, 2) == [4, 5, 6, 7]
     assert sorted(sum((chains_of_rank(10, r, 4) for r in range(4)), [])) == list(range(10))
+    # contiguous blocks: sampler(chain=chain0, chains=c) keys chain0 + c — disjoint across ranks
+    assert [chain_block(10, r, 4) for r in range(4)] == [(0, 3), (3, 3), (6, 2), (8, 2)]
+    for r in range(4):
+        c0, c = chain_block(10, r, 4)
+        assert chains_of_rank(10, r, 4) == list(range(c0, c0 + c))
+
+
+def test_welford_matches_two_pass():
+    from dropout_hamiltonian_montecarlo_amd.parallel import Welford, rhat_from_moments
+    from dropout_hamiltonian_montecarlo_amd import diagnostics as dg
+    rs = np.random.RandomState(3)
+    x = rs.normal(size=(3, 301, 7)) * np.arange(1, 8) + np.arange(3)[:, None, None]
+    w = Welford((3, 7))
+    for a, b in ((0, 1), (1, 50), (50, 51), (51, 301)):      # uneven batches, single draws
+        w.update(x[:, a] if b - a == 1 else x[:, a:b])
+    assert w.n == 301
+    np.testing.assert_allclose(w.mean, x.mean(axis=1), rtol=1e-13, atol=1e-13)
+    np.testing.assert_allclose(w.M2, ((x - x.mean(axis=1, keepdims=True)) ** 2).sum(axis=1), rtol=1e-12)
+    # classic R̂ from the moments = the direct computation on the draws
+    means, var = x.mean(axis=1), x.var(axis=1, ddof=1)
+    n = x.shape[1]
+    direct = np.sqrt(((n - 1) / n * var.mean(axis=0) + means.var(axis=0, ddof=1)) / var.mean(axis=0))
+    np.testing.assert_allclose(rhat_from_moments(n, w.mean, w.M2), direct, rtol=1e-12)
+    assert np.all(rhat_from_moments(n, w.mean, w.M2) > 1.0)
+    assert dg.split_rhat(x).shape == (7,)
 
 
 WORKER = r'''
@@ -57,6 +82,18 @@ assert parallel.allreduce_sum(rank + 1) == world * (world + 1) / 2
 assert parallel.allreduce_max(rank) == world - 1
 d = parallel.chain_diagnostics(allt)
 assert d["rhat"].shape == (3,) and np.all(d["rhat"] > 1.0)
+# per-parameter summaries: Welford over the local draws + a thinned trace, one all-gather
+w = parallel.Welford((2, 3)).update(local_tr)
+n, means, M2, tr = parallel.gather_summaries(w, local_tr[:, ::4], device=None)
+assert n == 64 and means.shape == (2 * world, 3) and tr.shape == (2 * world, 16, 3)
+np.testing.assert_allclose(means, allt.mean(axis=1), rtol=1e-13)
+np.testing.assert_allclose(parallel.rhat_from_moments(n, means, M2),
+                           np.sqrt(((n - 1) / n * allt.var(axis=1, ddof=1).mean(axis=0)
+                                    + allt.mean(axis=1).var(axis=0, ddof=1)) / allt.var(axis=1, ddof=1).mean(axis=0)),
+                           rtol=1e-12)
+np.testing.assert_allclose(parallel.diagnostics.split_rhat(tr), parallel.diagnostics.split_rhat(allt[:, ::4]))
+s = parallel.summary_diagnostics(n, means, M2, tr)
+assert s["chains"] == 2 * world and s["params"] == 3 and s["rhat"]["min"] > 1.0
 parallel.barrier()
 print("ok", rank)
 '''
