@@ -30,6 +30,7 @@
 // 784-256-256-10, B = 500 (layer 1 runs once, after W1 moved).
 #include "hmcx_common.h"
 #include "hmcx_internal.h"
+#include <type_traits>
 #include <algorithm>
 #include <vector>
 
@@ -260,7 +261,7 @@ __device__ inline void load_chunk(T (&x)[4][2], const T* P, int ld, int r0, int 
 // mean): gz = (softmax − onehot)/M replaces z in LDS and goes to gz[m][ldg]; lpart[blk] = Σ −log p[y].
 template <typename T>
 __device__ inline void ce_rows(T* zt, int zs, double* rowl, int m0, int M, int N, const int32_t* y, T* gz, int ldg,
-                               double* lpart, int blk) {
+                               double* lpart, int blk, bool writer = true) {
   const int t = threadIdx.x;
   if (t < 32) {
     T* zr = zt + t * zs;
@@ -279,7 +280,7 @@ __device__ inline void ce_rows(T* zt, int zs, double* rowl, int m0, int M, int N
         if (k == lab) g -= T(1);
         g = g / (T)M;
         zr[k] = g;
-        gz[(size_t)m * ldg + k] = g;
+        if (writer) gz[(size_t)m * ldg + k] = g;
       }
     } else {
       for (int k = 0; k < N; ++k) zr[k] = T(0);
@@ -287,7 +288,7 @@ __device__ inline void ce_rows(T* zt, int zs, double* rowl, int m0, int M, int N
     rowl[t] = l;
   }
   __syncthreads();
-  if (t == 0) {
+  if (t == 0 && writer) {
     double s = 0.0;
     for (int r = 0; r < 32; ++r) s += rowl[r];
     lpart[blk] = s;
@@ -298,37 +299,47 @@ __device__ inline void ce_rows(T* zt, int zs, double* rowl, int m0, int M, int N
 // hold zeros):  ga2 = ((gz·W3)·m2)·[h2>0]·m1 and its column sums (b2 partial), column sums of gz
 // (b3 partial), and gzᵀ·d3 over the block's rows (W3 partial).  Threads own a column j and a row
 // group (rows ≡ g mod R, R = blockDim / n_mid); W3 is staged in LDS scratch `scr` when it fits.
+// Columns [jlo, jhi) of n_mid only (the workgroup's slice: the layer-3 kernel runs one workgroup per
+// (row block, column slice)); `first` marks the slice that also writes the b3 partial.
 template <typename T>
-__device__ inline void l3_backward(const MMArgs<T>& a, const T* zt, int zs, int m0, int blk, T* scr, int scr_n) {
-  const int N = a.N, nm = a.n_mid;
+__device__ inline void l3_backward(const MMArgs<T>& a, const T* zt, int zs, int m0, int blk, T* scr, int scr_n,
+                                   int jlo, int jhi, bool first) {
+  const int N = a.N, nm = a.n_mid, nj = jhi - jlo;
   const int rows = min(32, a.M - m0);
   const int tid = threadIdx.x, nt = blockDim.x;
-  if (a.ga2) {
+  if (a.ga2 && nj > 0) {
     const bool wl = N * nm + nt <= scr_n;                      // W3 in LDS (+ nt values for the combine)
     T* w3 = scr + nt;
-    if (wl) {                                                  // 8 loads in flight per thread
-      const int nw = N * nm;
+    if (wl) {                                                  // the slice's columns, 8 loads in flight
+      const int nw = N * nj;
       for (int e0 = tid; e0 < nw; e0 += 8 * nt) {
         T v[8];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) v[q] = a.W3[min(e0 + q * nt, nw - 1)];
+        for (int q = 0; q < 8; ++q) {
+          const int e = min(e0 + q * nt, nw - 1), o = e / nj;
+          v[q] = a.W3[(size_t)o * nm + jlo + (e - o * nj)];
+        }
 #pragma unroll
         for (int q = 0; q < 8; ++q)
-          if (e0 + q * nt < nw) w3[e0 + q * nt] = v[q];
+          if (e0 + q * nt < nw) {
+            const int e = e0 + q * nt, o = e / nj;
+            w3[o * nm + jlo + (e - o * nj)] = v[q];
+          }
       }
       __syncthreads();
     }
-    const int R = max(1, nt / nm), cols = nt / R;
-    constexpr int RB = 16;                                     // rows per pass (one pass at R = 2)
+    const int R = max(1, nt / nj), cols = nt / R;
 #pragma unroll 1
-    for (int jb = 0; jb < nm; jb += cols) {
+    for (int jb = jlo; jb < jhi; jb += cols) {
       const int j = jb + tid % cols, g = tid / cols;
-      const bool act = g < R && j < nm;
+      const bool act = g < R && j < jhi;
       T cs = T(0);
-      if (act) {
+      // RB rows per pass (rows g, g + R, …): their h2 / mask loads go out first, then RB independent
+      // dot products; RB = 32 / R so that one pass covers the 32-row block
+      auto rows_pass = [&](auto rbc) {
+        constexpr int RB = decltype(rbc)::value;
 #pragma unroll 1
         for (int r0 = g; r0 < rows; r0 += RB * R) {
-          // RB rows per pass: their h2 / mask loads go out first, then RB independent dot products
           T hv[RB], m1v[RB], m2v[RB], acc8[RB];
 #pragma unroll
           for (int c = 0; c < RB; ++c) {
@@ -357,6 +368,12 @@ __device__ inline void l3_backward(const MMArgs<T>& a, const T* zt, int zs, int 
             }
           }
         }
+      };
+      if (act) {
+        if (R <= 2) rows_pass(std::integral_constant<int, 16>{});
+        else if (R <= 4) rows_pass(std::integral_constant<int, 8>{});
+        else if (R <= 8) rows_pass(std::integral_constant<int, 4>{});
+        else rows_pass(std::integral_constant<int, 2>{});
       }
       if (a.pb2) {
         scr[tid] = cs;
@@ -370,7 +387,7 @@ __device__ inline void l3_backward(const MMArgs<T>& a, const T* zt, int zs, int 
       }
     }
   }
-  if (a.pb3) {
+  if (a.pb3 && first) {
     for (int j = tid; j < N; j += nt) {
       T cs = T(0);
       for (int r = 0; r < rows; ++r) cs += zt[r * zs + j];
@@ -379,7 +396,7 @@ __device__ inline void l3_backward(const MMArgs<T>& a, const T* zt, int zs, int 
   }
   if (a.pw3) {
 #pragma unroll 1
-    for (int j = tid; j < nm; j += nt) {                       // one column of d3 per thread, all rows
+    for (int j = jlo + tid; j < jhi; j += nt) {                // one column of d3 per thread, all rows
       T dv[32];
 #pragma unroll
       for (int r = 0; r < 32; ++r) dv[r] = a.d3[(size_t)(m0 + min(r, rows - 1)) * nm + j];
@@ -416,7 +433,8 @@ __global__ __launch_bounds__(MM_NT) void k_mm(MMArgs<T> a) {
   __shared__ double rowl[32];
   run_pending(a.pend);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lg = lane >> 4;
-  const int m0 = blockIdx.x * 32, n0 = blockIdx.y * 32;
+  // MM_L3CE: blockIdx.y is the n_mid column slice of the layer-3 backward (N = n_out ≤ 32: one tile)
+  const int m0 = blockIdx.x * 32, n0 = EPI == MM_L3CE ? 0 : blockIdx.y * 32;
   const int Kq = ((a.K + 16 * MM_NW - 1) / (16 * MM_NW)) * 16;   // k range per wave (multiple of 16)
   const int kb = wave * Kq, ke = min(a.K, kb + Kq);
   typename M::acc_t acc[2][2];
@@ -484,9 +502,12 @@ __global__ __launch_bounds__(MM_NT) void k_mm(MMArgs<T> a) {
   }
   if constexpr (EPI == MM_L3CE) {
     __syncthreads();
-    ce_rows<T>(&red[0][0][0], 33, rowl, m0, a.M, a.N, a.y, a.C, a.ldc, a.lpart, blockIdx.x);
+    const bool first = blockIdx.y == 0;
+    ce_rows<T>(&red[0][0][0], 33, rowl, m0, a.M, a.N, a.y, a.C, a.ldc, a.lpart, blockIdx.x, first);
     __syncthreads();
-    l3_backward<T>(a, &red[0][0][0], 33, m0, blockIdx.x, &red[1][0][0], (MM_NW - 1) * 32 * 33);
+    const int cw = (a.n_mid + gridDim.y - 1) / gridDim.y;
+    const int jlo = min(a.n_mid, (int)blockIdx.y * cw), jhi = min(a.n_mid, jlo + cw);
+    l3_backward<T>(a, &red[0][0][0], 33, m0, blockIdx.x, &red[1][0][0], (MM_NW - 1) * 32 * 33, jlo, jhi, first);
   }
   if constexpr (EPI == MM_GA1) {
     if (a.colpart) {
@@ -517,7 +538,7 @@ __global__ __launch_bounds__(MM_NT) void k_l3_wide(MMArgs<T> a, const T* z) {
   __syncthreads();
   ce_rows<T>(zt, zs, rowl, m0, a.M, N, a.y, a.C, a.ldc, a.lpart, blockIdx.x);
   __syncthreads();
-  l3_backward<T>(a, zt, zs, m0, blockIdx.x, scr, MM_NT);
+  l3_backward<T>(a, zt, zs, m0, blockIdx.x, scr, MM_NT, 0, a.n_mid, true);
 }
 
 // Keep flags of F forwards (blockIdx.y = forward f, Philox slot MASK_SLOT0 + f), 3·mn per forward.
@@ -712,6 +733,7 @@ hipError_t mm(MlpNet<T>& net, MMArgs<T>& a) {
   a.pend = net.pend;
   net.pend.mode = UPD_NONE;
   dim3 grid((a.M + 31) / 32, (a.N + 31) / 32), blk(MM_NT);
+  if (EPI == MM_L3CE) grid.y = (unsigned)std::max(1, std::min(8, a.n_mid / 32));   // n_mid column slices
   const bool h1ok = AOP != OP_H1 || net.vec_masks;
   const bool kvec = a.K % (int)(16 / sizeof(T)) == 0;       // vectors never straddle the K end
   const bool av = !TA && h1ok && kvec && vec_ok(a.A, a.lda, sizeof(T));
