@@ -33,6 +33,11 @@ constexpr int BCH = 32;           // depth of one staged k-chunk
 constexpr int BXP = BCH + 2;      // 34: k_bfwd X chunk
 constexpr int BXPG = 48;          // k_bgrad X chunk [row][32 features]
 constexpr int BWP = BNT + 16;     // 176: W / diff chunk [k][160 columns]
+// Epilogue tiles read by the MFMA fragment layout (row = 4·lg + q, column = 16·j + lr): the noise tile
+// and the p² partials.  A row pitch of BNT = 160 elements is ≡ 0 (mod 64) dwords for doubles, so the
+// lane groups lg = 0 / 1 of a half-wave hit the same banks; BNP ≡ 4 (mod 8) elements puts them 32
+// dwords apart (doubles) / 16 apart (floats).
+constexpr int BNP = BNT + 4;      // 164
 
 // XCD-grouped tile order: the 1-D grid holds 8·nX·ceil(nCT/8) blocks; blocks b, b+8, b+16, ... share
 // one XCD (round-robin dispatch), so every x tile of chain tile ct lands on XCD ct mod 8 and the
@@ -324,15 +329,17 @@ __device__ inline void gen_tile_noise(const BGradArgs<T>& a, const int* chs, int
                                       FMap fmap) {
   const int tid = threadIdx.x;
   if constexpr (sizeof(T) == 8) {
+    // one Philox block per element pair (k, k+1); lane order: chain slot and pair fastest, so the
+    // lanes of a wave write consecutive 16-byte pairs of one feature row of Nz
     constexpr int NP = BKC / 2;
     for (int t = tid; t < BCT * nfl * NP; t += 256) {
-      const int cs = t / (nfl * NP), r = t - cs * (nfl * NP), fl = r / NP, kk = r - fl * NP;
+      const int fl = t / (BCT * NP), r = t - fl * (BCT * NP), cs = r / NP, kk = r - cs * NP;
       const int ch = chs[cs], fi = fmap(fl);
       if (ch < 0 || fi >= nfeat) continue;
       double z0, z1;
       philox_pair_d(a.seed, a.chain0 + ch, a.step, a.slot, (uint32_t)((d0 + fi) * NP + kk), z0, z1);
-      Nz[fl * BNT + cs * BKC + 2 * kk] = z0;
-      Nz[fl * BNT + cs * BKC + 2 * kk + 1] = z1;
+      Nz[fl * BNP + cs * BKC + 2 * kk] = z0;
+      Nz[fl * BNP + cs * BKC + 2 * kk + 1] = z1;
     }
   } else {                                        // nfl == tile width, fmap = identity
     const int e0 = d0 * BKC, ne = min(nfl, nfeat) * BKC;
@@ -345,7 +352,7 @@ __device__ inline void gen_tile_noise(const BGradArgs<T>& a, const int* chs, int
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int e = 4 * g + q - e0;
-        if (e >= 0 && e < ne) Nz[(e / BKC) * BNT + cs * BKC + (e % BKC)] = z4[q];
+        if (e >= 0 && e < ne) Nz[(e / BKC) * BNP + cs * BKC + (e % BKC)] = z4[q];
       }
     }
   }
@@ -394,7 +401,7 @@ __device__ inline void bias_substep(const BGradArgs<T>& a, const int* chs, T* pb
 template <typename T>
 __global__ __launch_bounds__(256) void k_bgrad(BGradArgs<T> a) {
   using M = mfma16<T>;
-  constexpr int XSN = BCH * BXPG > 8 * BNT * 8 / (int)sizeof(T) ? BCH * BXPG : 8 * BNT * 8 / (int)sizeof(T);
+  constexpr int XSN = BCH * BXPG > 8 * BNP * 8 / (int)sizeof(T) ? BCH * BXPG : 8 * BNP * 8 / (int)sizeof(T);
   __shared__ __attribute__((aligned(16))) T Xs[XSN];   // [row][feature]; later the per-lane-group p² sums
   __shared__ __attribute__((aligned(16))) T Ds[BCH * BWP];   // [row][column]; later the friction noise
   __shared__ int chs[BCT];
@@ -490,7 +497,7 @@ __global__ __launch_bounds__(256) void k_bgrad(BGradArgs<T> a) {
         const T gr = -(acc[j][q] - a.alpha * w);
         const T z = a.noise_mode == HMCX_NOISE_BUFFER
                         ? (T)a.noise[a.noff[ch] + (int64_t)a.slot * a.P + (uint32_t)(d * BKC + k)]
-                        : Nz[fi * BNT + col];
+                        : Nz[fi * BNP + col];
         const T p = (a.one_minus_eps * pv[j][q] + a.eps * gr) + a.noise_scale * z;
         Pg[idx] = p;
         const int n = a.n_iter[ch];
@@ -498,7 +505,7 @@ __global__ __launch_bounds__(256) void k_bgrad(BGradArgs<T> a) {
         else p2s += (double)(p * p);
       }
     }
-    kp[(mt * 4 + lg) * BNT + col] = p2s;
+    kp[(mt * 4 + lg) * BNP + col] = p2s;
   }
   __syncthreads();
   if (tid < BCT) {                                   // Σ pW² per chain ending at this iteration
@@ -506,7 +513,7 @@ __global__ __launch_bounds__(256) void k_bgrad(BGradArgs<T> a) {
     if (ch >= 0 && a.iter == a.n_iter[ch] - 1) {
       double v = 0.0;
       for (int k = 0; k < BKC; ++k)
-        for (int g = 0; g < 8; ++g) v += kp[g * BNT + tid * BKC + k];
+        for (int g = 0; g < 8; ++g) v += kp[g * BNP + tid * BKC + k];
       a.kin_part[(size_t)bx * a.C + ch] = v;
     }
   }
@@ -523,9 +530,9 @@ template <typename T>
 __global__ __launch_bounds__(256) void k_bgrad2(BGradArgs<T> a) {
   using M = mfma16<T>;
   typedef typename StageMap<T>::v2 v2;
-  constexpr int XSN = BCH * BXP2 > 8 * BNT * 8 / (int)sizeof(T) ? BCH * BXP2 : 8 * BNT * 8 / (int)sizeof(T);
+  constexpr int XSN = BCH * BXP2 > 8 * BNP * 8 / (int)sizeof(T) ? BCH * BXP2 : 8 * BNP * 8 / (int)sizeof(T);
   __shared__ __attribute__((aligned(16))) T Xs[XSN];   // [row][feature]; later the per-lane-group p² sums
-  constexpr int NZN = sizeof(T) == 8 ? 32 * BNT : BRW2 * BNT;   // noise rows of one pass
+  constexpr int NZN = sizeof(T) == 8 ? 32 * BNP : BRW2 * BNP;   // noise rows of one pass
   constexpr int DSN = BCH * BWP > NZN ? BCH * BWP : NZN;
   __shared__ __attribute__((aligned(16))) T Ds[DSN];   // [row][column]; later the friction noise
   __shared__ int chs[BCT];
@@ -648,7 +655,7 @@ __global__ __launch_bounds__(256) void k_bgrad2(BGradArgs<T> a) {
             const int nzr = NPASS == 2 ? mt * 16 + M::row(lane, q) : fi;
             const T z = a.noise_mode == HMCX_NOISE_BUFFER
                             ? (T)a.noise[a.noff[ch] + (int64_t)a.slot * a.P + (uint32_t)(d * BKC + k)]
-                            : Nz[nzr * BNT + col];
+                            : Nz[nzr * BNP + col];
             const T p = (a.one_minus_eps * pv[ii * 4 + q] + a.eps * gr) + a.noise_scale * z;
             Pg[idx] = p;
             if (!last) Wg[idx] = w + a.eps * p;
@@ -658,14 +665,14 @@ __global__ __launch_bounds__(256) void k_bgrad2(BGradArgs<T> a) {
     }
   }
 #pragma unroll
-  for (int j = 0; j < 5; ++j) kp[(mt * 4 + lg) * BNT + (nh * 5 + j) * 16 + lr] = p2s[j];
+  for (int j = 0; j < 5; ++j) kp[(mt * 4 + lg) * BNP + (nh * 5 + j) * 16 + lr] = p2s[j];
   __syncthreads();
   if (tid < BCT) {                                   // Σ pW² per chain ending at this iteration
     const int ch = chs[tid];
     if (ch >= 0 && a.iter == a.n_iter[ch] - 1) {
       double v = 0.0;
       for (int k = 0; k < BKC; ++k)
-        for (int g = 0; g < 8; ++g) v += kp[g * BNT + tid * BKC + k];
+        for (int g = 0; g < 8; ++g) v += kp[g * BNP + tid * BKC + k];
       a.kin_part[(size_t)bx * a.C + ch] = v;
       if (bx == 0)
         for (int b2 = a.nX; b2 < a.nDB_all; ++b2) a.kin_part[(size_t)b2 * a.C + ch] = 0.0;

@@ -37,14 +37,14 @@ for C in Cs:
     a.B, a.D, a.K, a.C, a.n_steps = B, D, K, C, steps
     a.alpha, a.log_prior = 0.01, 0.0
     a.X, a.Y = nat.ptr(X), nat.ptr(Y)
-    a.row0 = row0.ctypes.data_as(nat.c_i64p)
-    a.eps = epsa.ctypes.data_as(nat.c_dblp)
+    a.row0 = nat.addr(row0)
+    a.eps = nat.addr(epsa)
     n_iter_f = np.ascontiguousarray(n_iter.reshape(-1))
     u_f = np.ascontiguousarray(u.reshape(-1))
-    a.n_iter = n_iter_f.ctypes.data_as(nat.c_i32p)
-    a.u_accept = u_f.ctypes.data_as(nat.c_dblp)
+    a.n_iter = nat.addr(n_iter_f)
+    a.u_accept = nat.addr(u_f)
     a.noise_mode = nat.NOISE_PHILOX
-    a.noise_off = noff.ctypes.data_as(nat.c_i64p)
+    a.noise_off = nat.addr(noff)
     a.seed, a.chain0, a.step_base = 7, 0, 0
     a.W, a.b = nat.ptr(W), nat.ptr(b)
     a.out_A, a.out_accepted, a.out_ll = nat.ptr(out_A), nat.ptr(out_acc), nat.ptr(out_ll)

@@ -33,11 +33,11 @@ a.dtype = nat.dtype_code(dtype)
 a.B, a.D, a.K, a.C, a.n_steps = B, D, K, C, steps
 a.alpha, a.log_prior = 0.01, 0.0
 a.X, a.Y = nat.ptr(X), nat.ptr(Y)
-a.row0 = row0.ctypes.data_as(nat.c_i64p)
-a.eps = epsa.ctypes.data_as(nat.c_dblp)
-a.want_ll = want.ctypes.data_as(nat.c_u8p)
+a.row0 = nat.addr(row0)
+a.eps = nat.addr(epsa)
+a.want_ll = nat.addr(want)
 a.noise_mode = nat.NOISE_PHILOX
-a.noise_off = noff.ctypes.data_as(nat.c_i64p)
+a.noise_off = nat.addr(noff)
 a.seed, a.chain0, a.step_base = 3, 0, 0
 a.W, a.b = nat.ptr(W), nat.ptr(b)
 a.out_ll = nat.ptr(out_ll)
