@@ -332,7 +332,7 @@ __device__ inline void gen_tile_noise(const BGradArgs<T>& a, const int* chs, int
     // one Philox block per element pair (k, k+1); lane order: chain slot and pair fastest, so the
     // lanes of a wave write consecutive 16-byte pairs of one feature row of Nz
     constexpr int NP = BKC / 2;
-    for (int t = tid; t < BCT * nfl * NP; t += 256) {
+    for (int t = tid; t < BCT * nfl * NP; t += blockDim.x) {
       const int fl = t / (BCT * NP), r = t - fl * (BCT * NP), cs = r / NP, kk = r - cs * NP;
       const int ch = chs[cs], fi = fmap(fl);
       if (ch < 0 || fi >= nfeat) continue;
@@ -344,7 +344,7 @@ __device__ inline void gen_tile_noise(const BGradArgs<T>& a, const int* chs, int
   } else {                                        // nfl == tile width, fmap = identity
     const int e0 = d0 * BKC, ne = min(nfl, nfeat) * BKC;
     const int g0 = e0 >> 2, ng = ((e0 + ne + 3) >> 2) - g0;
-    for (int t = tid; t < BCT * ng; t += 256) {
+    for (int t = tid; t < BCT * ng; t += blockDim.x) {
       const int cs = t / ng, g = g0 + (t - cs * ng), ch = chs[cs];
       if (ch < 0) continue;
       float z4[4];
@@ -520,61 +520,87 @@ __global__ __launch_bounds__(256) void k_bgrad(BGradArgs<T> a) {
   if (bx == 0) bias_substep(a, chs, pbs);
 }
 
-// k_bgrad with 64-feature tiles (two m-tiles per wave: 10 MFMAs per 7 LDS operand reads instead of
-// 5 per 6), used when many chains are active.  LDS: X chunk [32 rows][64 features] and the diff
-// chunk as in k_bgrad; the friction noise is generated after the k loop into the diff chunk's
-// space and the kinetic partials use the X chunk's space, so two workgroups fit per CU.
-constexpr int BRW2 = 64;
-constexpr int BXP2 = BRW2 + 16;   // 80 ≡ 16 (mod 32)
-template <typename T>
-__global__ __launch_bounds__(256) void k_bgrad2(BGradArgs<T> a) {
+// k_bgrad with wide feature tiles: NW waves, FT = 16·NW features × 16 chains (two m-tiles per wave:
+// 10 MFMAs per 7 LDS operand reads instead of 5 per 6), used when many chains are active.  Built with
+// NW = 4: 64 features, 66 KB of LDS, two workgroups per CU.  (NW = 8 — 128 features, 122 KB, one
+// 8-wave workgroup per CU, 7 feature tiles instead of 13 re-reading each diff slice — measured
+// slower: 247 vs 231 ms per 24-step call at 2048 chains)
+// LDS (dynamic): X chunk [32 rows][FT features] (later the per-lane-group p² sums) and the diff chunk
+// [32 rows][160] (later the friction noise of one pass: f64 chains in two passes of FT/2 features —
+// m-tile i = pass, local feature fl = mt·16 + row — f32 chains in one).
+template <typename T, int NW> struct BGW {
+  static constexpr int NT = 64 * NW, FT = 16 * NW, XP = FT + 16;     // XP ≡ 16 (mod 32)
+  static constexpr int NXV = BCH * FT / 2 / NT;                        // X 2-vectors per thread (4)
+  static constexpr int NDV = BCH * BNT / 2 / NT;                       // diff 2-vectors per thread
+  static constexpr int NMT = NW / 2;                                   // feature groups of 32
+  static constexpr int NPASS = sizeof(T) == 8 ? 2 : 1;
+  static constexpr int NZR = FT / NPASS;                               // noise rows per pass
+  static constexpr int XSN = BCH * XP > 2 * NW * BNP * 8 / (int)sizeof(T) ? BCH * XP : 2 * NW * BNP * 8 / (int)sizeof(T);
+  static constexpr int DSN = BCH * BWP > NZR * BNP ? BCH * BWP : NZR * BNP;
+  static constexpr size_t lds() { return (size_t)(XSN + DSN + BNT) * sizeof(T) + BCT * sizeof(int); }
+};
+constexpr int BRW2 = 64;          // k_bgradw<T, 4> feature tile
+
+template <typename T, int NW>
+__global__ __launch_bounds__(64 * NW) void k_bgradw(BGradArgs<T> a) {
   using M = mfma16<T>;
+  using G = BGW<T, NW>;
   typedef typename StageMap<T>::v2 v2;
-  constexpr int XSN = BCH * BXP2 > 8 * BNP * 8 / (int)sizeof(T) ? BCH * BXP2 : 8 * BNP * 8 / (int)sizeof(T);
-  __shared__ __attribute__((aligned(16))) T Xs[XSN];   // [row][feature]; later the per-lane-group p² sums
-  constexpr int NZN = sizeof(T) == 8 ? 32 * BNP : BRW2 * BNP;   // noise rows of one pass
-  constexpr int DSN = BCH * BWP > NZN ? BCH * BWP : NZN;
-  __shared__ __attribute__((aligned(16))) T Ds[DSN];   // [row][column]; later the friction noise
-  __shared__ int chs[BCT];
-  __shared__ T pbs[BNT];
+  extern __shared__ __attribute__((aligned(16))) unsigned char bgw_smem[];
+  T* Xs = reinterpret_cast<T*>(bgw_smem);                // [row][feature]; later the p² sums
+  T* Ds = Xs + G::XSN;                                   // [row][column]; later the friction noise
+  T* pbs = Ds + G::DSN;
+  int* chs = reinterpret_cast<int*>(pbs + BNT);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lg = lane >> 4;
   int bx, by;
   if (!xcd_tile(a.nX, a.nCT, bx, by)) return;
-  const int d0 = bx * BRW2, rank0 = by * BCT;
-  const int nfeat = min(BRW2, a.D - d0);
+  const int d0 = bx * G::FT, rank0 = by * BCT;
+  const int nfeat = min(G::FT, a.D - d0);
   const int D = a.D, N = a.N, B = a.B;
   if (tid < BCT) chs[tid] = rank0 + tid < a.c_act ? a.perm[rank0 + tid] : -1;
   __syncthreads();
 
-  const StageCM scm(tid, chs, (size_t)B * BKC);      // diff chunk [32 rows][16 chains × 10]
-  int xr[4], xc[4];                                  // X part: [32 rows][64 features], 4 vectors each
+  // diff chunk [32 rows][16 chains × 10]: 2560 vectors, NDV per thread (StageCM's map, stride NT)
+  int wr[G::NDV], wls[G::NDV];
+  size_t wsrc[G::NDV];
+  bool wok[G::NDV];
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int j = tid + 256 * u;
-    xr[u] = j >> 5;
-    xc[u] = (j & 31) * 2;
+  for (int u = 0; u < G::NDV; ++u) {
+    const int j = tid + G::NT * u;
+    const int row = j / 80, rem = j - row * 80, cs = rem / 5, k2 = (rem - cs * 5) * 2, ch = chs[cs];
+    wr[u] = row;
+    wok[u] = ch >= 0;
+    wsrc[u] = (size_t)(ch >= 0 ? ch : 0) * ((size_t)B * BKC) + k2;
+    wls[u] = cs * BKC + k2;
   }
-  v2 xv[4], dv[10];
+  int xr[G::NXV], xc[G::NXV];                            // X chunk [32 rows][FT features]
+#pragma unroll
+  for (int u = 0; u < G::NXV; ++u) {
+    const int j = tid + G::NT * u;
+    xr[u] = j / (G::FT / 2);
+    xc[u] = (j - xr[u] * (G::FT / 2)) * 2;
+  }
+  v2 xv[G::NXV], dv[G::NDV];
   auto fetch = [&](int r0) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < G::NXV; ++u) {
       const int r = r0 + xr[u];
       xv[u] = ld2<T>(a.X + (size_t)min(r, B - 1) * D + d0 + xc[u], r < B, nfeat - xc[u]);
     }
 #pragma unroll
-    for (int u = 0; u < 10; ++u) {
-      const int r = r0 + scm.wr[u];
-      dv[u] = ld2<T>(a.diff + scm.wsrc[u] + (size_t)min(r, B - 1) * BKC, scm.wok[u] && r < B, 2);
+    for (int u = 0; u < G::NDV; ++u) {
+      const int r = r0 + wr[u];
+      dv[u] = ld2<T>(a.diff + wsrc[u] + (size_t)min(r, B - 1) * BKC, wok[u] && r < B, 2);
     }
   };
   auto stash = [&]() {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) st2<T>(Xs + xr[u] * BXP2 + xc[u], xv[u]);
+    for (int u = 0; u < G::NXV; ++u) st2<T>(Xs + xr[u] * G::XP + xc[u], xv[u]);
 #pragma unroll
-    for (int u = 0; u < 10; ++u) st2<T>(Ds + scm.wr[u] * BWP + scm.wls[u], dv[u]);
+    for (int u = 0; u < G::NDV; ++u) st2<T>(Ds + wr[u] * BWP + wls[u], dv[u]);
   };
 
-  const int mt = wave & 1, nh = wave >> 1;           // wave: features mt·32 .. +32, columns nh·80 .. +80
+  const int mt = wave % G::NMT, nh = wave / G::NMT;     // wave: features mt·32 .. +32, columns nh·80 .. +80
   typename M::acc_t acc[2][5];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -591,7 +617,7 @@ __global__ __launch_bounds__(256) void k_bgrad2(BGradArgs<T> a) {
     for (int ks = 0; ks < nks; ++ks) {
       T av[2], bv[5];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) av[i] = Xs[(ks * 4 + lg) * BXP2 + mt * 32 + i * 16 + lr];
+      for (int i = 0; i < 2; ++i) av[i] = Xs[(ks * 4 + lg) * G::XP + mt * 32 + i * 16 + lr];
 #pragma unroll
       for (int j = 0; j < 5; ++j) bv[j] = Ds[(ks * 4 + lg) * BWP + (nh * 5 + j) * 16 + lr];
 #pragma unroll
@@ -601,30 +627,26 @@ __global__ __launch_bounds__(256) void k_bgrad2(BGradArgs<T> a) {
     }
   }
   __syncthreads();
-  // ---- epilogue on the accumulators: softmax.py:57-58 gradient, sghmc.py:31,34 momentum, :32 drift.
-  // The friction noise of the tile goes into the diff chunk's space first: f32 chains in one pass
-  // ([64 features][160] floats); f64 chains in two passes of 32 features (m-tile i = pass: local
-  // feature fl = mt·16 + row), [32][160] doubles each, so two workgroups still fit per CU.
-  constexpr int NPASS = sizeof(T) == 8 ? 2 : 1;
+  // ---- epilogue on the accumulators: softmax.py:57-58 gradient, sghmc.py:31,34 momentum, :32 drift
   T* Nz = Ds;
-  double* kp = reinterpret_cast<double*>(Xs);        // [mt·4 + lg][160] Σ p² over the lane's rows
+  double* kp = reinterpret_cast<double*>(Xs);        // [mt·4 + lg][BNP] Σ p² over the lane's rows
   // The elements of one column (the pass's m-tiles × 4 rows) are loaded together (W and pW never
   // alias): one HBM round trip per column instead of one per element.
   T* __restrict__ Wg = a.W;
   T* __restrict__ Pg = a.pW;
   double p2s[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-  for (int h = 0; h < NPASS; ++h) {
+  for (int h = 0; h < G::NPASS; ++h) {
     if (a.noise_mode != HMCX_NOISE_BUFFER) {
       if (h) __syncthreads();                      // pass 0's noise has been read
-      if constexpr (NPASS == 2)
-        gen_tile_noise(a, chs, d0, nfeat, Nz, 32, [h](int fl) { return (fl >> 4) * 32 + h * 16 + (fl & 15); });
+      if constexpr (G::NPASS == 2)
+        gen_tile_noise(a, chs, d0, nfeat, Nz, G::NZR, [h](int fl) { return (fl >> 4) * 32 + h * 16 + (fl & 15); });
       else
-        gen_tile_noise(a, chs, d0, nfeat, Nz, BRW2, [](int fl) { return fl; });
+        gen_tile_noise(a, chs, d0, nfeat, Nz, G::FT, [](int fl) { return fl; });
       __syncthreads();
     }
-    constexpr int NI = 2 / NPASS;                    // m-tiles of this pass
-    const int i0 = NPASS == 2 ? h : 0;
+    constexpr int NI = 2 / G::NPASS;                 // m-tiles of this pass
+    const int i0 = G::NPASS == 2 ? h : 0;
 #pragma unroll
     for (int j = 0; j < 5; ++j) {
       const int col = (nh * 5 + j) * 16 + lr;
@@ -652,7 +674,7 @@ __global__ __launch_bounds__(256) void k_bgrad2(BGradArgs<T> a) {
             const size_t idx = ((size_t)ch * D + d) * BKC + k;
             const T w = wv[ii * 4 + q];
             const T gr = -(acc[i][j][q] - a.alpha * w);
-            const int nzr = NPASS == 2 ? mt * 16 + M::row(lane, q) : fi;
+            const int nzr = G::NPASS == 2 ? mt * 16 + M::row(lane, q) : fi;
             const T z = a.noise_mode == HMCX_NOISE_BUFFER
                             ? (T)a.noise[a.noff[ch] + (int64_t)a.slot * a.P + (uint32_t)(d * BKC + k)]
                             : Nz[nzr * BNP + col];
@@ -672,7 +694,7 @@ __global__ __launch_bounds__(256) void k_bgrad2(BGradArgs<T> a) {
     if (ch >= 0 && a.iter == a.n_iter[ch] - 1) {
       double v = 0.0;
       for (int k = 0; k < BKC; ++k)
-        for (int g = 0; g < 8; ++g) v += kp[g * BNP + tid * BKC + k];
+        for (int g = 0; g < 4 * G::NMT; ++g) v += kp[g * BNP + tid * BKC + k];
       a.kin_part[(size_t)bx * a.C + ch] = v;
       if (bx == 0)
         for (int b2 = a.nX; b2 < a.nDB_all; ++b2) a.kin_part[(size_t)b2 * a.C + ch] = 0.0;

@@ -1234,7 +1234,14 @@ int sghmc_batch_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
   const bool big = C >= 512;
   const int RT = big ? 64 : 32;
   const int nRB = (B + RT - 1) / RT, nDB = (D + BRW - 1) / BRW, nDB16 = (D + 15) / 16;
-  const int nDB2 = (D + BRW2 - 1) / BRW2;            // k_bgrad2 feature tiles
+  const int nDB2 = (D + BRW2 - 1) / BRW2;            // k_bgradw<T, 4> feature tiles
+  // dynamic LDS of the wide gradient kernel (set once per kernel)
+  const size_t lds4 = BGW<T, 4>::lds();
+  static bool bgw_attr = false;
+  if (!bgw_attr) {
+    HMCX_HIP(ctx, hipFuncSetAttribute((const void*)k_bgradw<T, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds4));
+    bgw_attr = true;
+  }
   const size_t nsc = (size_t)s->n_steps * C;
   // host: chain order per step (path length descending, stable) and active counts per iteration
   std::vector<int32_t> perm(nsc);
@@ -1342,7 +1349,7 @@ int sghmc_batch_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
       g.nCT = ctiles;
       if (nDB2 * ctiles >= 2 * ctx->num_cus) {
         g.nX = nDB2;
-        hipLaunchKernelGGL((k_bgrad2<T>), dim3(xcd_grid(g.nX, g.nCT)), dim3(256), 0, st, g);
+        hipLaunchKernelGGL((k_bgradw<T, 4>), dim3(xcd_grid(g.nX, g.nCT)), dim3(256), lds4, st, g);
       } else {
         g.nX = nDB;
         hipLaunchKernelGGL((k_bgrad<T>), dim3(xcd_grid(g.nX, g.nCT)), dim3(256), 0, st, g);
