@@ -138,10 +138,18 @@ class mlp:
         return np.float64(self.loss_device(par, masks=masks, **args).item())
 
     def log_prior(self, par, **args):                                     # mlp.py:40-45
+        """−Σ_var ½·alpha·Σθ²/dim, with Σθ² a float64 device reduction (hmcx_sumsq)."""
+        ctx = context(self.device)
+        ss = torch.empty(len(par), dtype=torch.float64, device=self.device)
+        keep = []
+        for i, var in enumerate(par.keys()):
+            v = self._dev(par[var]).contiguous()
+            keep.append(v)
+            ctx.check(ctx.lib.hmcx_sumsq(ctx.h, self.code, ptr(v), v.numel(), ptr(ss[i:i + 1])), "hmcx_sumsq")
+        sums = ss.cpu().numpy()
         K = 0.0
-        for var in par.keys():
-            v = self._dev(par[var]).to(torch.float64)
-            K -= 0.5 * self.alpha * float(torch.sum(v * v)) / v.numel()
+        for v, s2 in zip(keep, sums):
+            K -= 0.5 * self.alpha * float(s2) / v.numel()
         return K
 
     def negative_log_posterior(self, par, masks=None, **args):           # mlp.py:80-82

@@ -248,3 +248,16 @@ def test_sghmc_mlp_config3_f64_trajectory_matches_oracle():
     np.testing.assert_allclose([t["A"] for t in s.trace], [t["A"] for t in o.trace], rtol=1e-8, atol=1e-12)
     for k in start:
         np.testing.assert_allclose(post_g[k], post_r[k], rtol=1e-8, atol=1e-10)
+
+
+@pytest.mark.parametrize("dtype,rtol", [(torch.float64, 1e-13), (torch.float32, 1e-6)])
+def test_mlp_log_prior_device_reduction(dtype, rtol):
+    """mlp.log_prior (mlp.py:40-45, −Σ_var ½·alpha·Σθ²/dim) with Σθ² from hmcx_sumsq against the
+    NumPy restatement."""
+    mlp, _ = _mlp_cls()
+    rs = np.random.RandomState(9)
+    par = {k: rs.normal(0, 0.3, s) for k, s in om.mlp_param_shapes(30, 24, 7).items()}
+    m = mlp({"alpha": 0.05}, 30, 24, 7, dtype=dtype, device="cuda:0")
+    ref = om.mlp({"alpha": 0.05}, 30, 24, 7).log_prior({k: v.astype(np.float32 if dtype == torch.float32 else np.float64)
+                                                         for k, v in par.items()})
+    assert abs(m.log_prior(par) - ref) <= rtol * abs(ref)
