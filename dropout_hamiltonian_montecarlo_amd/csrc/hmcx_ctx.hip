@@ -444,6 +444,7 @@ int hmcx_destroy(hmcx_ctx* ctx) {
   for (auto e : ctx->ev_pool) (void)hipEventDestroy(e);
   if (ctx->abort_host) (void)hipHostFree(ctx->abort_host);
   if (ctx->abort_dev) (void)hipFree(ctx->abort_dev);
+  if (ctx->mlp_gx) (void)hipFree(ctx->mlp_gx);
   for (auto& g : ctx->graveyard) {
     (void)hipGraphExecDestroy(g.first);
     (void)hipEventDestroy(g.second);

@@ -27,6 +27,10 @@ struct hmcx_ctx {
   bool stage_pend[2] = {false, false};
   int stage_cur = 0;
   size_t stage_off = 0;
+  // MLP fused layer-2/3 launches (hmcx_mlp.hip, MM_L23): granule arena (zeroed once) and epoch counter
+  char* mlp_gx = nullptr;
+  size_t mlp_gx_bytes = 0;
+  unsigned mlp_epoch = 0;
   // host schedule of the calls that draw their own (PHILOX, n_iter == u_accept == NULL)
   std::vector<double> sched_L, sched_u;
   std::vector<int32_t> sched_n;

@@ -147,7 +147,7 @@ __device__ inline void run_pending(const Pending<T>& pd) {
 template <typename T>
 __global__ __launch_bounds__(256) void k_pending(Pending<T> pd) { run_pending(pd); }
 
-enum MMEpi { MM_STORE = 0, MM_L2 = 1, MM_L3CE = 2, MM_GA1 = 3, MM_UPD = 4 };
+enum MMEpi { MM_STORE = 0, MM_L2 = 1, MM_L3CE = 2, MM_GA1 = 3, MM_UPD = 4, MM_L23 = 5 };
 enum MMOp { OP_PLAIN = 0, OP_H1 = 1 };
 
 template <typename T> struct MMArgs {
@@ -167,6 +167,10 @@ template <typename T> struct MMArgs {
   T* ga2; T* pb2; T* pb3; T* pw3;
   int upd_mode; Upd<T> u;            // MM_UPD
   Pending<T> pend;                   // run first, by the whole grid
+  // MM_L23 (layer 2 + layer 3 in one launch): the 32 × n_out logit partials of the column-slice
+  // workgroups of one row block meet in a tagged-granule arena (see k_mm)
+  char* gx; int gx_bytes; unsigned ep; int* abort_flag;
+  int N3; const T* bias3; T* gz;     // n_out, b3 and the gz output of the fused layer 3
 };
 
 template <typename T, int OP>
@@ -303,8 +307,8 @@ __device__ inline void ce_rows(T* zt, int zs, double* rowl, int m0, int M, int N
 // (row block, column slice)); `first` marks the slice that also writes the b3 partial.
 template <typename T>
 __device__ inline void l3_backward(const MMArgs<T>& a, const T* zt, int zs, int m0, int blk, T* scr, int scr_n,
-                                   int jlo, int jhi, bool first) {
-  const int N = a.N, nm = a.n_mid, nj = jhi - jlo;
+                                   int jlo, int jhi, bool first, int n_out = -1) {
+  const int N = n_out >= 0 ? n_out : a.N, nm = a.n_mid, nj = jhi - jlo;
   const int rows = min(32, a.M - m0);
   const int tid = threadIdx.x, nt = blockDim.x;
   if (a.ga2 && nj > 0) {
@@ -426,6 +430,47 @@ __device__ inline void mm_epilogue(const MMArgs<T>& a, int m, int n, T v) {
   }
 }
 
+// Granule poll of one item over `np` producers (stride `pstride` granules): sum in producer order.
+// Bounded (2 s of s_memrealtime): on timeout the context's abort word is raised and the item reads
+// 0 — the host reports the launch as failed (abort_defer), it never returns a stale value silently.
+__device__ inline bool l23_poll(__amdgpu_buffer_rsrc_t rs, int g0, int pstride, int np, unsigned ep, int* abort_flag,
+                                double* sum) {
+  typedef unsigned int g4 __attribute__((ext_vector_type(4)));
+  constexpr int NPMAX = 16;
+  unsigned pend = (np >= 32) ? 0xffffffffu : ((1u << np) - 1u);
+  double val[NPMAX];
+#pragma unroll
+  for (int p = 0; p < NPMAX; ++p) val[p] = 0.0;
+  unsigned long long t0 = 0;
+  for (int spins = 0; pend; ++spins) {
+    g4 v[NPMAX];
+#pragma unroll
+    for (int p = 0; p < NPMAX; ++p)
+      v[p] = __builtin_amdgcn_raw_buffer_load_b128(rs, (g0 + (p < np ? p : 0) * pstride) * 16, 0, 16 /* sc1 */);
+#pragma unroll
+    for (int p = 0; p < NPMAX; ++p)
+      if (((pend >> p) & 1u) && v[p].y == ep && v[p].w == ep) {
+        val[p] = __builtin_bit_cast(double, (unsigned long long)v[p].x | ((unsigned long long)v[p].z << 32));
+        pend &= ~(1u << p);
+      }
+    if (!pend) break;
+    if (spins == 0) t0 = __builtin_amdgcn_s_memrealtime();
+    if ((spins & 63) == 63 && (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull ||
+                               __hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+      __hip_atomic_store(abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *sum = 0.0;
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  double acc = val[0];
+#pragma unroll
+  for (int p = 1; p < NPMAX; ++p)
+    if (p < np) acc += val[p];
+  *sum = acc;
+  return true;
+}
+
 template <typename T, int EPI, int AOP, int BOP, int TA, int TB, int AV, int BV>
 __global__ __launch_bounds__(MM_NT) void k_mm(MMArgs<T> a) {
   using M = mfma16<T>;
@@ -496,6 +541,23 @@ __global__ __launch_bounds__(MM_NT) void k_mm(MMArgs<T> a) {
         a.C[i] = g;
       }
       red[0][mm][nn] = g;
+    } else if constexpr (EPI == MM_L23) {                      // mlp.py:30-31; the tile stays in LDS
+      T d = T(0), h = T(0), m1 = T(0), m2 = T(0);
+      if (m < a.M && n < a.N) {
+        const size_t i = (size_t)m * a.ldc + n;
+        m1 = mval(a.ms, 1, i);
+        m2 = mval(a.ms, 2, i);
+        const T t = (v + a.bias[n]) * m1;
+        h = t > T(0) ? t : T(0);
+        a.C[i] = h;
+        d = h * m2;
+        a.C2[i] = d;
+      }
+      // planes of this element only (each (mm, nn) has one thread): d3, h2, m1, m2 of the tile
+      red[0][mm][nn] = d;
+      red[3][mm][nn] = h;
+      red[4][mm][nn] = m1;
+      red[5][mm][nn] = m2;
     } else {
       if (m < a.M && n < a.N) mm_epilogue<T, EPI>(a, m, n, v);
     }
@@ -508,6 +570,86 @@ __global__ __launch_bounds__(MM_NT) void k_mm(MMArgs<T> a) {
     const int cw = (a.n_mid + gridDim.y - 1) / gridDim.y;
     const int jlo = min(a.n_mid, (int)blockIdx.y * cw), jhi = min(a.n_mid, jlo + cw);
     l3_backward<T>(a, &red[0][0][0], 33, m0, blockIdx.x, &red[1][0][0], (MM_NW - 1) * 32 * 33, jlo, jhi, first);
+  }
+  if constexpr (EPI == MM_L23) {
+    // Layer 3 of this row block, in the same launch: z = d3·W3ᵀ + b3 (mlp.py:31) needs all n_mid
+    // columns, which the S = gridDim.y column-slice workgroups of the block hold.  Each publishes
+    // its 32 × n_out partial (own 32 columns, k order within the slice) as 16-byte granules
+    // {lo32, ep, hi32, ep} with write-through (sc1) stores; every member reads all S partials of
+    // every (row, class) and sums them in slice order — the all-reduce by redundant reads of
+    // hmcx_persist2.hip — then runs the cross-entropy of the block (slice 0 writes loss and gz) and
+    // the layer-3 backward of its own columns.  The epoch is new per launch and the arena only ever
+    // holds granules of earlier launches, so no stale value can match.
+    __syncthreads();                                             // the reduction has read every red[w]
+    const int No = a.N3, S = gridDim.y, s = blockIdx.y, rb = blockIdx.x;
+    T* d3t = &red[0][0][0];                                      // [32][33] d3 of the tile
+    T* w3s = &red[1][0][0];                                      // [n_out][32] W3 columns of the slice
+    T* zt = &red[2][0][0];                                       // [32][33] logits, then gz
+    for (int e = tid; e < No * 32; e += MM_NT) {
+      const int o = e >> 5, c = e & 31;
+      w3s[e] = n0 + c < a.N ? a.W3[(size_t)o * a.n_mid + n0 + c] : T(0);
+    }
+    __syncthreads();
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(a.gx, 0, a.gx_bytes, 0x00020000);
+    const int items = 32 * No;
+    const int base_rb = rb * S * items;
+    if (tid < items) {
+      const int r = tid / No, o = tid - r * No;
+      T zp = T(0);
+#pragma unroll 8
+      for (int c = 0; c < 32; ++c) zp += d3t[r * 33 + c] * w3s[o * 32 + c];
+      const unsigned long long x = __builtin_bit_cast(unsigned long long, (double)zp);
+      typedef unsigned int g4 __attribute__((ext_vector_type(4)));
+      const g4 w = {(unsigned)x, a.ep, (unsigned)(x >> 32), a.ep};
+      __builtin_amdgcn_raw_buffer_store_b128(w, rs, (base_rb + s * items + tid) * 16, 0, 16 /* sc1 */);
+    }
+    bool ok = true;
+    if (tid < items) {
+      const int r = tid / No, o = tid - r * No;
+      double sum = 0.0;
+      ok = l23_poll(rs, base_rb + tid, items, S, a.ep, a.abort_flag, &sum);
+      zt[r * 33 + o] = (m0 + r < a.M) ? (T)sum + a.bias3[o] : T(0);
+    }
+    __syncthreads();
+    const bool first = s == 0;
+    ce_rows<T>(zt, 33, rowl, m0, a.M, No, a.y, a.gz, No, a.lpart, rb, first);
+    __syncthreads();
+    // layer-3 backward of the slice's columns, all operands in LDS (gz in zt, W3 slice in w3s, the
+    // tile's h2 / d3 / masks): ga2 = ((gz·W3)·m2)·[h2 > 0]·m1 and its column sums (b2 partial),
+    // gzᵀ·d3 (W3 partial), column sums of gz (b3 partial, slice 0)
+    const int rows = min(32, a.M - m0), nm = a.n_mid;
+    T* gat = &red[6][0][0];                                      // [32][33] ga2 of the tile
+    for (int e = tid; e < 1024; e += MM_NT) {
+      const int r = e >> 5, c = e & 31;
+      T g = T(0);
+      for (int o = 0; o < No; ++o) g += zt[r * 33 + o] * w3s[o * 32 + c];
+      T t = g * red[5][r][c];
+      t = t * (red[3][r][c] > T(0) ? T(1) : T(0));
+      t = t * red[4][r][c];
+      const bool ok2 = r < rows && n0 + c < nm;
+      gat[r * 33 + c] = ok2 ? t : T(0);
+      if (ok2 && a.ga2) a.ga2[(size_t)(m0 + r) * nm + n0 + c] = t;
+    }
+    __syncthreads();
+    if (a.pb2 && tid < 32 && n0 + tid < nm) {
+      T cs = T(0);
+      for (int r = 0; r < rows; ++r) cs += gat[r * 33 + tid];
+      a.pb2[(size_t)rb * nm + n0 + tid] = cs;
+    }
+    if (a.pw3)
+      for (int e = tid; e < No * 32; e += MM_NT) {
+        const int o = e >> 5, c = e & 31;
+        if (n0 + c >= nm) continue;
+        T acc = T(0);
+        for (int r = 0; r < 32; ++r) acc += zt[r * 33 + o] * d3t[r * 33 + c];   // rows past M: gz = 0
+        a.pw3[(size_t)rb * No * nm + (size_t)o * nm + n0 + c] = acc;
+      }
+    if (a.pb3 && first && tid < No) {
+      T cs = T(0);
+      for (int r = 0; r < rows; ++r) cs += zt[r * 33 + tid];
+      a.pb3[(size_t)rb * No + tid] = cs;
+    }
+    (void)ok;
   }
   if constexpr (EPI == MM_GA1) {
     if (a.colpart) {
@@ -710,6 +852,8 @@ struct MlpNet {
   bool xw_valid = false;
   bool vec_masks = true;                 // masks may be read as 4-/2-element vectors
   Pending<T> pend{};                     // consumed by the next launch
+  // fused layer 2 + layer 3 (MM_L23): granule arena and epoch counter of the context
+  char* gx = nullptr; int gx_bytes = 0; unsigned* epoch = nullptr; int* abort_flag = nullptr; bool fuse = false;
   int nvar(int v) const {
     switch (v) {
       case 0: return n_mid * n_in;  case 1: return n_mid;
@@ -766,6 +910,21 @@ hipError_t mlp_forward(MlpNet<T>& net, T* const* q, const MaskSrc<T>& ms, double
     mm_set<T>(a, B, nm, net.n_in, net.X, net.n_in, 0, q[0], net.n_in, 1, net.xw, nm);
     if ((e = mm<T, MM_STORE, 0, 1>(net, a))) return e;
     net.xw_valid = true;
+  }
+  if (net.fuse && lpart && !logits && net.n_out <= 32) {
+    // h2, d3 and layer 3 (cross-entropy, layer-3 backward) in one launch (MM_L23)
+    MMArgs<T> a{};
+    mm_set<T>(a, B, nm, nm, net.xw, nm, 0, q[2], nm, 1, net.h2, nm);
+    a.bias = q[3]; a.b1 = q[1]; a.ms = ms; a.C2 = net.d3;
+    a.N3 = net.n_out; a.bias3 = q[5]; a.gz = net.gz; a.y = net.y; a.lpart = lpart;
+    a.W3 = q[4]; a.h2 = net.h2; a.d3 = net.d3; a.n_mid = nm;
+    a.ga2 = w.ga2 ? net.ga2 : nullptr;
+    a.pb2 = w.pb2 ? net.pb2 : nullptr;
+    a.pb3 = w.pb3 ? net.pb3 : nullptr;
+    a.pw3 = w.pw3 ? net.pw3 : nullptr;
+    a.gx = net.gx; a.gx_bytes = net.gx_bytes; a.ep = ++*net.epoch; a.abort_flag = net.abort_flag;
+    if (a.ep == 0) a.ep = ++*net.epoch;                       // 0 is the arena's initial content
+    return mm<T, MM_L23, 0, 1, OP_H1>(net, a);
   }
   {                                                           // h2, d3 from h1 = max((xw + b1)·m0, 0)
     MMArgs<T> a{};
@@ -848,6 +1007,36 @@ hipError_t flush_pending(MlpNet<T>& net) {
   return hipGetLastError();
 }
 
+// Fused layer 2 + layer 3 (MM_L23) when n_out ≤ 32, at most 16 column slices, and the whole grid
+// fits on the chip at once (its slice workgroups wait for each other); HMCX_MLP_FUSE=0 turns it off.
+template <typename T>
+int net_fuse(hmcx_ctx* ctx, MlpNet<T>& net) {
+  static const bool off = getenv("HMCX_MLP_FUSE") && getenv("HMCX_MLP_FUSE")[0] == '0';
+  const int S = (net.n_mid + 31) / 32;
+  if (off || net.n_out > 32 || S > 16) return HMCX_OK;
+  int per_cu = 0;
+  const void* kfn = (const void*)k_mm<T, MM_L23, OP_H1, OP_PLAIN, 0, 1, 1, 1>;
+  HMCX_HIP(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, MM_NT, 0));
+  if ((long)per_cu * ctx->num_cus < (long)net.nlb * S) return HMCX_OK;
+  const size_t need = (size_t)net.nlb * S * 32 * net.n_out * 16;
+  if (need > 0x7fffffff) return HMCX_OK;
+  if (ctx->mlp_gx_bytes < need) {
+    HMCX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (ctx->mlp_gx) (void)hipFree(ctx->mlp_gx);
+    ctx->mlp_gx = nullptr;
+    ctx->mlp_gx_bytes = 0;
+    HMCX_HIP(ctx, hipMalloc((void**)&ctx->mlp_gx, need));
+    HMCX_HIP(ctx, hipMemset(ctx->mlp_gx, 0, need));          // epoch 0 never matches a launch
+    ctx->mlp_gx_bytes = need;
+  }
+  net.gx = ctx->mlp_gx;
+  net.gx_bytes = (int)ctx->mlp_gx_bytes;
+  net.epoch = &ctx->mlp_epoch;
+  net.abort_flag = ctx->abort_dev;
+  net.fuse = true;
+  return HMCX_OK;
+}
+
 template <typename T>
 void mlp_workspace(Workspace& ws, MlpNet<T>& net) {
   const size_t mn = (size_t)net.B * net.n_mid;
@@ -878,6 +1067,7 @@ int mlp_grad_t(hmcx_ctx* ctx, const void* X, const int32_t* y, int B, int n_in, 
   MlpNet<T> net{};
   net_init(net, B, n_in, n_mid, n_out, ctx->stream);
   net.X = (const T*)X; net.y = y;
+  if (int rc = net_fuse<T>(ctx, net)) return rc;
   Workspace ws(ctx);
   double* lpart;
   do { ws.reset(); mlp_workspace<T>(ws, net); lpart = ws.take<double>(net.nlb); } while (ws.retry());
@@ -912,6 +1102,7 @@ int mlp_loss_t(hmcx_ctx* ctx, const void* X, const int32_t* y, int B, int n_in, 
   MlpNet<T> net{};
   net_init(net, B, n_in, n_mid, n_out, ctx->stream);
   net.X = (const T*)X; net.y = y;
+  if (int rc = net_fuse<T>(ctx, net)) return rc;
   Workspace ws(ctx);
   double* lpart;
   do { ws.reset(); mlp_workspace<T>(ws, net); lpart = ws.take<double>(net.nlb); } while (ws.retry());
@@ -937,6 +1128,7 @@ template <typename T>
 int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
   MlpNet<T> net{};
   net_init(net, s->B, s->n_in, s->n_mid, s->n_out, ctx->stream);
+  if (int rc0 = net_fuse<T>(ctx, net)) return rc0;
   const int mn = s->B * s->n_mid, n3 = 3 * mn;
   int off_v[6], dim[6], P = 0;                                // element offset of each variable in `order`
   {
