@@ -112,6 +112,23 @@ int abort_defer(hmcx_ctx* ctx, const int* dev_flag, hipStream_t st) {
   return HMCX_OK;          // checked before the next launch (abort_precheck) or by hmcx_synchronize
 }
 
+int gx_reserve(hmcx_ctx* ctx, size_t bytes) {
+  if (ctx->gx_bytes >= bytes) return HMCX_OK;
+  HMCX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (ctx->gx_arena) (void)hipFree(ctx->gx_arena);
+  ctx->gx_arena = nullptr;
+  ctx->gx_bytes = 0;
+  HMCX_HIP(ctx, hipMalloc((void**)&ctx->gx_arena, bytes));
+  HMCX_HIP(ctx, hipMemset(ctx->gx_arena, 0, bytes));          // epoch 0 never matches a launch
+  ctx->gx_bytes = bytes;
+  return HMCX_OK;
+}
+
+unsigned gx_next_epoch(hmcx_ctx* ctx) {
+  if (++ctx->gx_epoch == 0) ++ctx->gx_epoch;
+  return ctx->gx_epoch;
+}
+
 void begin_call(hmcx_ctx* ctx) {
   ctx->stage_cur ^= 1;
   const int c = ctx->stage_cur;
@@ -444,7 +461,7 @@ int hmcx_destroy(hmcx_ctx* ctx) {
   for (auto e : ctx->ev_pool) (void)hipEventDestroy(e);
   if (ctx->abort_host) (void)hipHostFree(ctx->abort_host);
   if (ctx->abort_dev) (void)hipFree(ctx->abort_dev);
-  if (ctx->mlp_gx) (void)hipFree(ctx->mlp_gx);
+  if (ctx->gx_arena) (void)hipFree(ctx->gx_arena);
   for (auto& g : ctx->graveyard) {
     (void)hipGraphExecDestroy(g.first);
     (void)hipEventDestroy(g.second);

@@ -27,10 +27,11 @@ struct hmcx_ctx {
   bool stage_pend[2] = {false, false};
   int stage_cur = 0;
   size_t stage_off = 0;
-  // MLP fused layer-2/3 launches (hmcx_mlp.hip, MM_L23): granule arena (zeroed once) and epoch counter
-  char* mlp_gx = nullptr;
-  size_t mlp_gx_bytes = 0;
-  unsigned mlp_epoch = 0;
+  // tagged-granule arena of the fused launches (MLP MM_L23, wide SGLD forward+softmax): zeroed once,
+  // one epoch per launch from a single counter, so no launch can match another's granules
+  char* gx_arena = nullptr;
+  size_t gx_bytes = 0;
+  unsigned gx_epoch = 0;
   // host schedule of the calls that draw their own (PHILOX, n_iter == u_accept == NULL)
   std::vector<double> sched_L, sched_u;
   std::vector<int32_t> sched_n;
@@ -76,6 +77,10 @@ int timing_collect(hmcx_ctx* ctx);
 int abort_defer(hmcx_ctx* ctx, const int* dev_flag, hipStream_t st);
 int abort_poll(hmcx_ctx* ctx, bool block);
 int abort_precheck(hmcx_ctx* ctx);
+// Grow the fused launches' granule arena to `bytes` (zeroed; stream-synchronising when it grows) and
+// return the next launch epoch (never 0).
+int gx_reserve(hmcx_ctx* ctx, size_t bytes);
+unsigned gx_next_epoch(hmcx_ctx* ctx);
 
 #define HMCX_HIP(ctx, expr)                                                                  \
   do {                                                                                       \

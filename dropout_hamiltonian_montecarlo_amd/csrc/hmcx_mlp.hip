@@ -30,6 +30,7 @@
 // 784-256-256-10, B = 500 (layer 1 runs once, after W1 moved).
 #include "hmcx_common.h"
 #include "hmcx_internal.h"
+#include "hmcx_granule.h"
 #include <type_traits>
 #include <algorithm>
 #include <vector>
@@ -430,47 +431,6 @@ __device__ inline void mm_epilogue(const MMArgs<T>& a, int m, int n, T v) {
   }
 }
 
-// Granule poll of one item over `np` producers (stride `pstride` granules): sum in producer order.
-// Bounded (2 s of s_memrealtime): on timeout the context's abort word is raised and the item reads
-// 0 — the host reports the launch as failed (abort_defer), it never returns a stale value silently.
-__device__ inline bool l23_poll(__amdgpu_buffer_rsrc_t rs, int g0, int pstride, int np, unsigned ep, int* abort_flag,
-                                double* sum) {
-  typedef unsigned int g4 __attribute__((ext_vector_type(4)));
-  constexpr int NPMAX = 16;
-  unsigned pend = (np >= 32) ? 0xffffffffu : ((1u << np) - 1u);
-  double val[NPMAX];
-#pragma unroll
-  for (int p = 0; p < NPMAX; ++p) val[p] = 0.0;
-  unsigned long long t0 = 0;
-  for (int spins = 0; pend; ++spins) {
-    g4 v[NPMAX];
-#pragma unroll
-    for (int p = 0; p < NPMAX; ++p)
-      v[p] = __builtin_amdgcn_raw_buffer_load_b128(rs, (g0 + (p < np ? p : 0) * pstride) * 16, 0, 16 /* sc1 */);
-#pragma unroll
-    for (int p = 0; p < NPMAX; ++p)
-      if (((pend >> p) & 1u) && v[p].y == ep && v[p].w == ep) {
-        val[p] = __builtin_bit_cast(double, (unsigned long long)v[p].x | ((unsigned long long)v[p].z << 32));
-        pend &= ~(1u << p);
-      }
-    if (!pend) break;
-    if (spins == 0) t0 = __builtin_amdgcn_s_memrealtime();
-    if ((spins & 63) == 63 && (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull ||
-                               __hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
-      __hip_atomic_store(abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      *sum = 0.0;
-      return false;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-  double acc = val[0];
-#pragma unroll
-  for (int p = 1; p < NPMAX; ++p)
-    if (p < np) acc += val[p];
-  *sum = acc;
-  return true;
-}
-
 template <typename T, int EPI, int AOP, int BOP, int TA, int TB, int AV, int BV>
 __global__ __launch_bounds__(MM_NT) void k_mm(MMArgs<T> a) {
   using M = mfma16<T>;
@@ -590,7 +550,7 @@ __global__ __launch_bounds__(MM_NT) void k_mm(MMArgs<T> a) {
       w3s[e] = n0 + c < a.N ? a.W3[(size_t)o * a.n_mid + n0 + c] : T(0);
     }
     __syncthreads();
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(a.gx, 0, a.gx_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs = gx_rsrc(a.gx, a.gx_bytes);
     const int items = 32 * No;
     const int base_rb = rb * S * items;
     if (tid < items) {
@@ -598,16 +558,13 @@ __global__ __launch_bounds__(MM_NT) void k_mm(MMArgs<T> a) {
       T zp = T(0);
 #pragma unroll 8
       for (int c = 0; c < 32; ++c) zp += d3t[r * 33 + c] * w3s[o * 32 + c];
-      const unsigned long long x = __builtin_bit_cast(unsigned long long, (double)zp);
-      typedef unsigned int g4 __attribute__((ext_vector_type(4)));
-      const g4 w = {(unsigned)x, a.ep, (unsigned)(x >> 32), a.ep};
-      __builtin_amdgcn_raw_buffer_store_b128(w, rs, (base_rb + s * items + tid) * 16, 0, 16 /* sc1 */);
+      gx_put(rs, base_rb + s * items + tid, (double)zp, a.ep);
     }
     bool ok = true;
     if (tid < items) {
       const int r = tid / No, o = tid - r * No;
       double sum = 0.0;
-      ok = l23_poll(rs, base_rb + tid, items, S, a.ep, a.abort_flag, &sum);
+      ok = gx_poll_sum(rs, base_rb + tid, items, S, a.ep, a.abort_flag, &sum);
       zt[r * 33 + o] = (m0 + r < a.M) ? (T)sum + a.bias3[o] : T(0);
     }
     __syncthreads();
@@ -853,7 +810,7 @@ struct MlpNet {
   bool vec_masks = true;                 // masks may be read as 4-/2-element vectors
   Pending<T> pend{};                     // consumed by the next launch
   // fused layer 2 + layer 3 (MM_L23): granule arena and epoch counter of the context
-  char* gx = nullptr; int gx_bytes = 0; unsigned* epoch = nullptr; int* abort_flag = nullptr; bool fuse = false;
+  char* gx = nullptr; int gx_bytes = 0; hmcx_ctx* ctx = nullptr; int* abort_flag = nullptr; bool fuse = false;
   int nvar(int v) const {
     switch (v) {
       case 0: return n_mid * n_in;  case 1: return n_mid;
@@ -922,8 +879,7 @@ hipError_t mlp_forward(MlpNet<T>& net, T* const* q, const MaskSrc<T>& ms, double
     a.pb2 = w.pb2 ? net.pb2 : nullptr;
     a.pb3 = w.pb3 ? net.pb3 : nullptr;
     a.pw3 = w.pw3 ? net.pw3 : nullptr;
-    a.gx = net.gx; a.gx_bytes = net.gx_bytes; a.ep = ++*net.epoch; a.abort_flag = net.abort_flag;
-    if (a.ep == 0) a.ep = ++*net.epoch;                       // 0 is the arena's initial content
+    a.gx = net.gx; a.gx_bytes = net.gx_bytes; a.ep = gx_next_epoch(net.ctx); a.abort_flag = net.abort_flag;
     return mm<T, MM_L23, 0, 1, OP_H1>(net, a);
   }
   {                                                           // h2, d3 from h1 = max((xw + b1)·m0, 0)
@@ -1020,18 +976,10 @@ int net_fuse(hmcx_ctx* ctx, MlpNet<T>& net) {
   if ((long)per_cu * ctx->num_cus < (long)net.nlb * S) return HMCX_OK;
   const size_t need = (size_t)net.nlb * S * 32 * net.n_out * 16;
   if (need > 0x7fffffff) return HMCX_OK;
-  if (ctx->mlp_gx_bytes < need) {
-    HMCX_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    if (ctx->mlp_gx) (void)hipFree(ctx->mlp_gx);
-    ctx->mlp_gx = nullptr;
-    ctx->mlp_gx_bytes = 0;
-    HMCX_HIP(ctx, hipMalloc((void**)&ctx->mlp_gx, need));
-    HMCX_HIP(ctx, hipMemset(ctx->mlp_gx, 0, need));          // epoch 0 never matches a launch
-    ctx->mlp_gx_bytes = need;
-  }
-  net.gx = ctx->mlp_gx;
-  net.gx_bytes = (int)ctx->mlp_gx_bytes;
-  net.epoch = &ctx->mlp_epoch;
+  if (int rc = gx_reserve(ctx, need)) return rc;
+  net.gx = ctx->gx_arena;
+  net.gx_bytes = (int)ctx->gx_bytes;
+  net.ctx = ctx;
   net.abort_flag = ctx->abort_dev;
   net.fuse = true;
   return HMCX_OK;
@@ -1259,7 +1207,8 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
     HMCX_HIP(ctx, hipGetLastError());
   }
   if ((rc = gs.finish())) return rc;
-  return timing_end(ctx, ctx->stream);
+  if ((rc = timing_end(ctx, ctx->stream))) return rc;
+  return net.fuse ? abort_defer(ctx, ctx->abort_dev, ctx->stream) : HMCX_OK;   // a timed-out exchange
 }
 
 template int mlp_masks_t<float>(hmcx_ctx*, int, int, uint64_t, uint32_t, uint32_t, uint32_t, void*);
