@@ -124,9 +124,24 @@ int gx_reserve(hmcx_ctx* ctx, size_t bytes) {
   return HMCX_OK;
 }
 
+// Epochs are unique over the arena's life: a launch polls only for epochs no earlier launch wrote,
+// so the arena needs no clearing between launches.  When the 32-bit counter would wrap, the arena is
+// cleared on the stream (behind every earlier user) and the count restarts at 1.
+int gx_epochs(hmcx_ctx* ctx, unsigned count, unsigned* first) {
+  if (count == 0) count = 1;
+  if ((uint64_t)ctx->gx_epoch + count > 0xffffffffull) {
+    if (ctx->gx_arena) HMCX_HIP(ctx, hipMemsetAsync(ctx->gx_arena, 0, ctx->gx_bytes, ctx->stream));
+    ctx->gx_epoch = 0;
+  }
+  *first = ctx->gx_epoch + 1;
+  ctx->gx_epoch += count;
+  return HMCX_OK;
+}
+
 unsigned gx_next_epoch(hmcx_ctx* ctx) {
-  if (++ctx->gx_epoch == 0) ++ctx->gx_epoch;
-  return ctx->gx_epoch;
+  unsigned ep = 1;
+  (void)gx_epochs(ctx, 1, &ep);
+  return ep;
 }
 
 void begin_call(hmcx_ctx* ctx) {

@@ -81,6 +81,7 @@ int abort_precheck(hmcx_ctx* ctx);
 // return the next launch epoch (never 0).
 int gx_reserve(hmcx_ctx* ctx, size_t bytes);
 unsigned gx_next_epoch(hmcx_ctx* ctx);
+int gx_epochs(hmcx_ctx* ctx, unsigned count, unsigned* first);   // count consecutive epochs
 
 #define HMCX_HIP(ctx, expr)                                                                  \
   do {                                                                                       \

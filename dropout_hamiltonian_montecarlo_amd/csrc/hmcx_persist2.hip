@@ -63,6 +63,7 @@ struct Q2Args {
   int oXA, oXD, oXB, oXW, oXS;              // region offsets in granules
   int arena_bytes;
   int pad;                                  // line-aligned producer blocks (HMCX_P2_PAD, default on)
+  unsigned ep0;                             // first round epoch of this launch (unique in the arena's life)
   int zoff;                                 // noise off the A-RS pollers (HMCX_P2_ZOFF, default on)
   int spread;                               // rounds with spread gathers, bits A-RS, A-AG, B-RS, B-AG
                                             // (HMCX_P2_SPREAD=<mask>; default A-AG, where it measured faster)
@@ -550,7 +551,7 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
   auto tstamp = [&](int s_, int it_, int slot) {
     if (trb && tid == 0 && s_ == 0 && it_ >= 0 && it_ < P2TR_IT) trb[it_ * 8 + slot] = __builtin_amdgcn_s_memrealtime();
   };
-  unsigned ep = 0;                                    // round epoch (same sequence in every workgroup)
+  unsigned ep = a.ep0 - 1;                            // round epoch (same sequence in every workgroup)
   unsigned uA = 0, uD = 0, uB = 0, uW = 0, uS = 0;    // per-region use counters (buffer parity)
 
   // ---- phase A: partial logits X[R_r,F_f]·W[F_f] → XA(par, r, f) [nrow][KC], then A-RS consume:
@@ -1126,12 +1127,18 @@ int sghmc_p2_t(hmcx_ctx* ctx, const hmcx_sampler_args* s, const PersistPlan2& pl
   for (int i = 0; i < 5; ++i)
     if (hbytes[i] && !hsrc[i]) return set_error(ctx, HMCX_EINVAL, "sghmc: null host schedule array");
   const size_t sched_bytes = packed_bytes(5, hbytes);
+  // the exchange arena is the context's granule arena: every launch polls for epochs of its own,
+  // never written before, so it is not cleared per call
+  if ((rc = gx_reserve(ctx, (size_t)ngran * 16))) return rc;
+  char* arena = ctx->gx_arena;
+  unsigned rounds = 0;                           // ≤ 5 epochs per leapfrog iteration (it = -1 … L-1, accept)
+  for (size_t i = 0; i < n; ++i) rounds += 5u * (unsigned)(std::max(s->n_iter[i], 0) + 2);
+  unsigned ep0 = 1;
+  if ((rc = gx_epochs(ctx, rounds, &ep0))) return rc;
   Workspace ws(ctx);
-  char* arena;
   char* sched;
   do {
     ws.reset();
-    arena = reinterpret_cast<char*>(ws.take<double>((size_t)ngran * 2));
     sched = ws.take<char>(sched_bytes);
   } while (ws.retry());
   if (ws.failed) return HMCX_ENOMEM;
@@ -1143,7 +1150,6 @@ int sghmc_p2_t(hmcx_ctx* ctx, const hmcx_sampler_args* s, const PersistPlan2& pl
   int64_t* d_row0 = reinterpret_cast<int64_t*>(dp[2]);
   int32_t* d_n = reinterpret_cast<int32_t*>(dp[3]);
   int64_t* d_noff = reinterpret_cast<int64_t*>(dp[4]);
-  HMCX_HIP(ctx, hipMemsetAsync(arena, 0, (size_t)ngran * 16, ctx->stream));
 
   Q2Args a{};
   a.B = s->B; a.D = s->D; a.K = K; a.P = s->D * K + K; a.n_steps = s->n_steps;
@@ -1158,6 +1164,7 @@ int sghmc_p2_t(hmcx_ctx* ctx, const hmcx_sampler_args* s, const PersistPlan2& pl
   a.oXA = 0; a.oXD = (int)nXA; a.oXB = (int)(nXA + nXD); a.oXW = (int)(nXA + nXD + nXB);
   a.oXS = (int)(nXA + nXD + nXB + nXW);
   a.arena_bytes = (int)(ngran * 16);
+  a.ep0 = ep0;
   a.pad = pad;
   {
     const int HA = KC + 1;
