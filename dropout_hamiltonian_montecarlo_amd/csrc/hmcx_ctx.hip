@@ -510,7 +510,8 @@ int hmcx_clear_abort(hmcx_ctx* ctx) {
 
 int hmcx_set_sghmc_path(hmcx_ctx* ctx, int path) {
   HMCX_GUARD_CTX(ctx);
-  if (path < 0 || path > 2) return set_error(ctx, HMCX_EINVAL, "path must be 0 (auto), 1 (kernels), 2 (persistent)");
+  if (path < 0 || path > 3)
+    return set_error(ctx, HMCX_EINVAL, "path must be 0 (auto), 1 (kernels), 2 (persistent 2-D), 3 (row space)");
   ctx->sghmc_path = path;
   return HMCX_OK;
 }

@@ -32,6 +32,7 @@ struct hmcx_ctx {
   char* gx_arena = nullptr;
   size_t gx_bytes = 0;
   unsigned gx_epoch = 0;
+  std::vector<int64_t> rs_poff, rs_nzo;   // row-space SGHMC: per-step projection / noise offsets
   // host schedule of the calls that draw their own (PHILOX, n_iter == u_accept == NULL)
   std::vector<double> sched_L, sched_u;
   std::vector<int32_t> sched_n;

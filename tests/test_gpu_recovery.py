@@ -1,4 +1,5 @@
-"""In-process recovery of the persistent single-chain SGHMC kernel (csrc/hmcx_persist2.hip).
+"""In-process recovery of the persistent single-chain SGHMC kernels (csrc/hmcx_persist2.hip,
+csrc/hmcx_rowspace.hip).
 
 A launch whose workgroups time out in a hand-off writes nothing to W/b and raises the context's
 sticky abort word, so every launch queued behind it returns untouched too (include/hmcx.h
@@ -36,15 +37,15 @@ def _restore_path():
     nat.context(torch.device("cuda:0")).set_sghmc_path(0)
 
 
-@pytest.mark.parametrize("name", ["sghmc_small", "sghmc_mnist"])
-def test_forced_abort_is_recovered_in_process(name, monkeypatch, capfd):
+@pytest.mark.parametrize("name,path", [("sghmc_small", 2), ("sghmc_mnist", 2), ("sghmc_mnist", 3)])
+def test_forced_abort_is_recovered_in_process(name, path, monkeypatch, capfd):
     """HMCX_P2_FORCE_ABORT=1: in every persistent launch the last workgroup gives up at step 1
     (the other workgroups then abort in their polls) — the first epoch's call and the one already
     queued behind it (sample() pipelines epoch calls) are both re-run."""
     c = gi.TRAJ_CONFIGS[name]
     monkeypatch.setenv("HMCX_P2_FORCE_ABORT", "1")
     try:
-        got = _run_gpu(c, path=2)
+        got = _run_gpu(c, path=path)
     finally:
         _restore_path()
     err = capfd.readouterr().err

@@ -54,12 +54,13 @@ def _run_gpu(c, dtype=torch.float64, noise="numpy", seed=0, path=0):
     return post, logp, s.trace, s.out.getvalue()
 
 
-_PATHS = [(n, p) for n in sorted(gi.TRAJ_CONFIGS) for p in ((1, 2) if gi.TRAJ_CONFIGS[n]["kind"] == "sghmc" else (0,))]
+_PATHS = [(n, p) for n in sorted(gi.TRAJ_CONFIGS) for p in ((1, 2, 3) if gi.TRAJ_CONFIGS[n]["kind"] == "sghmc" else (0,))]
 
 
 @pytest.mark.parametrize("name,path", _PATHS)
 def test_trajectory_f64_vs_oracle_and_golden(name, path, golden_dir):
-    """path 1 = kernel-per-phase, 2 = persistent single-launch kernel (both must agree with NumPy)."""
+    """path 1 = kernel-per-phase, 2 = persistent 2-D kernel, 3 = row-space persistent kernel (all must
+    agree with NumPy)."""
     c = gi.TRAJ_CONFIGS[name]
     post_r, logp_r, tr_r, log_r = _run_oracle(c)
     post_g, logp_g, tr_g, log_g = _run_gpu(c, path=path)
@@ -103,7 +104,7 @@ def test_trajectory_f32(name, path):
     np.testing.assert_allclose(logp_g, logp_r, rtol=1e-4)
 
 
-@pytest.mark.parametrize("path", [1, 2])
+@pytest.mark.parametrize("path", [1, 2, 3])
 def test_philox_mode_runs_and_is_deterministic(path):
     c = dict(gi.TRAJ_CONFIGS["sghmc_mnist"])
     p1, l1, t1, _ = _run_gpu(c, noise="philox", seed=11, path=path)
@@ -115,13 +116,16 @@ def test_philox_mode_runs_and_is_deterministic(path):
     assert np.all(np.isfinite(l1))
 
 
-def test_philox_paths_agree():
-    """Both SGHMC implementations consume the same Philox streams: same trajectory (f64)."""
+@pytest.mark.parametrize("path", [2, 3])
+def test_philox_paths_agree(path):
+    """Every SGHMC implementation consumes the same Philox streams: same trajectory (f64)."""
     c = dict(gi.TRAJ_CONFIGS["sghmc_mnist"])
     p1, l1, t1, _ = _run_gpu(c, noise="philox", seed=5, path=1)
-    p2, l2, t2, _ = _run_gpu(c, noise="philox", seed=5, path=2)
+    p2, l2, t2, _ = _run_gpu(c, noise="philox", seed=5, path=path)
     assert [t["accepted"] for t in t1] == [t["accepted"] for t in t2]
+    assert [t["L"] for t in t1] == [t["L"] for t in t2]
     np.testing.assert_allclose(p1["weights"], p2["weights"], rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(p1["bias"], p2["bias"], rtol=1e-9, atol=1e-12)
 
 
 def test_philox_noise_statistics():
@@ -179,7 +183,7 @@ def test_hmc_generic_softmax_vs_golden(golden_dir):
     np.testing.assert_allclose(loss, d["loss"], rtol=1e-10)
 
 
-@pytest.mark.parametrize("path", [1, 2])
+@pytest.mark.parametrize("path", [1, 2, 3])
 def test_full_size_mnist_shape_properties(path):
     """BASELINE config 2 size (N=60000 would be slow for the oracle; use N=5000, B=500, D=784):
     every step accepted or rejected consistently with its own A and u; logp finite; the state
@@ -305,7 +309,7 @@ def test_sgld_gpu_variant_step_api():
         np.testing.assert_allclose(pg[v].cpu().numpy(), po[v], rtol=1e-10, atol=1e-14)
 
 
-@pytest.mark.parametrize("path", [1, 2])
+@pytest.mark.parametrize("path", [1, 2, 3])
 def test_sghmc_step_api_returns_momentum(path):
     """sghmc.step(state, momentum, rng) returns (q, p, acceptprob) like cpu/sghmc.py:19-39 (A1
     completion): p is the final momentum of an accepted proposal, else the freshly drawn one.  The
