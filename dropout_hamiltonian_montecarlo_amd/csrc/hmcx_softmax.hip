@@ -1153,46 +1153,75 @@ int hmc_run_t(hmcx_ctx* ctx, const hmcx_hmc_args* s) {
 
 // k_sghmc_init for the chain-batched path: same arithmetic, but the working copy Wwork and the
 // momentum pW are chain-major [C][D][K] (each chain's block contiguous, so every tile of the batched
-// kernels owns whole cache lines); W stays in the caller's [D][C·K] layout.
+// kernels owns whole cache lines); W stays in the caller's [D][C·K] layout.  One workgroup per
+// (16 features, 16 chains): 16 lanes per chain, each taking element pairs (k, k+1) of one feature —
+// one Box–Muller per pair (both normals of the Philox block are used), the chain-major writes
+// contiguous per chain, the kinetic partial summed over the chain's 16 lanes (fixed DPP order).
+template <typename T>
+__device__ inline void philox_pair_t(uint64_t seed, uint32_t chain, uint32_t step, uint32_t slot, uint32_t e, T& z0,
+                                     T& z1) {   // elements e, e + 1 (e even) of philox_normal_t<T>
+  if constexpr (sizeof(T) == sizeof(double)) {
+    double a, b;
+    philox_pair_d(seed, chain, step, slot, e >> 1, a, b);
+    z0 = (T)a; z1 = (T)b;
+  } else {
+    u32x4 c = {{e >> 2, slot, step, chain}};
+    u32x4 r = philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+    float a, b;
+    if (e & 2u) box_muller(r.v[2], r.v[3], a, b);
+    else box_muller(r.v[0], r.v[1], a, b);
+    z0 = (T)a; z1 = (T)b;
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void k_binit(InitArgs<T> a) {
-  __shared__ double ksh[256];
-  const int c = blockIdx.y, tid = threadIdx.x;
-  const int K = a.K;
-  const int d0 = blockIdx.x * 16;
-  const bool take = a.prev_acc && a.prev_acc[c];
-  const bool drift = a.n_iter[c] >= 1;
+  const int tid = threadIdx.x, K = a.K, KP = K / 2;                 // K even (batched path: K = 10)
+  const int cl = tid >> 4, j = tid & 15;
+  const int c = blockIdx.y * 16 + cl, d0 = blockIdx.x * 16;
+  const bool cv = c < a.C;
+  const int cc = cv ? c : a.C - 1;
+  const bool take = cv && a.prev_acc && a.prev_acc[cc];
+  const bool drift = cv && a.n_iter[cc] >= 1;
   double kin = 0.0;
-  for (int e = tid; e < 16 * K; e += 256) {
-    const int i = e / K, k = e - (e / K) * K, d = d0 + i;
-    if (d >= a.D) continue;
+  for (int r = j; r < 16 * KP; r += 16) {                            // pair r: feature r / KP, classes 2·(r % KP) + {0, 1}
+    const int dl = r / KP, k = 2 * (r - dl * KP), d = d0 + dl;
+    if (!cv || d >= a.D) continue;
     const size_t w = (size_t)d * a.N + c * K + k;
     const size_t wc = ((size_t)c * a.D + d) * K + k;
-    double z;
-    if (a.noise_mode == HMCX_NOISE_BUFFER) z = a.noise[a.noff[c] + d * K + k];
-    else z = (double)philox_normal_t<T>(a.seed, a.chain0 + c, a.step, 0u, (uint32_t)(d * K + k));
-    const T p = (T)z;                                                     // hmc.py:86 N(0,1)
-    T q = a.W[w];
-    if (take) { q = a.Wwork[wc]; a.W[w] = q; }                            // commit (sghmc.py:37)
-    a.pW[wc] = p;
-    a.Wwork[wc] = drift ? q + a.eps * p : q;                              // sghmc.py:32 (iteration 0)
-    kin += (double)p * (double)p;
+    T p0, p1;
+    if (a.noise_mode == HMCX_NOISE_BUFFER) {
+      p0 = (T)a.noise[a.noff[c] + d * K + k];
+      p1 = (T)a.noise[a.noff[c] + d * K + k + 1];
+    } else {
+      philox_pair_t<T>(a.seed, a.chain0 + c, a.step, 0u, (uint32_t)(d * K + k), p0, p1);   // hmc.py:86
+    }
+    T q0, q1;
+    if (take) {                                                       // commit (sghmc.py:37)
+      q0 = a.Wwork[wc]; q1 = a.Wwork[wc + 1];
+      a.W[w] = q0; a.W[w + 1] = q1;
+    } else {
+      q0 = a.W[w]; q1 = a.W[w + 1];
+    }
+    a.pW[wc] = p0; a.pW[wc + 1] = p1;
+    a.Wwork[wc] = drift ? q0 + a.eps * p0 : q0;                       // sghmc.py:32 (iteration 0)
+    a.Wwork[wc + 1] = drift ? q1 + a.eps * p1 : q1;
+    kin += (double)p0 * (double)p0;
+    kin += (double)p1 * (double)p1;
   }
-  ksh[tid] = kin;
-  __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
-    if (tid < s) ksh[tid] += ksh[tid + s];
-    __syncthreads();
-  }
-  if (tid == 0) a.kin0_part[(size_t)blockIdx.x * a.C + c] = ksh[0];
-  if (blockIdx.x == 0) {
-    __syncthreads();
+  // the chain's 16 lanes (one DPP row): symmetric pairs, every lane ends with the same bits
+  kin += __shfl_xor(kin, 1, 16);
+  kin += __shfl_xor(kin, 2, 16);
+  kin += __shfl_xor(kin, 4, 16);
+  kin += __shfl_xor(kin, 8, 16);
+  if (j == 0 && cv) a.kin0_part[(size_t)blockIdx.x * a.C + c] = kin;
+  if (blockIdx.x == 0 && cv) {                                        // the bias of chain c
     double kb = 0.0;
-    if (tid < K) {
-      const int col = c * K + tid;
+    if (j < K) {
+      const int col = c * K + j;
       double z;
-      if (a.noise_mode == HMCX_NOISE_BUFFER) z = a.noise[a.noff[c] + a.D * K + tid];
-      else z = (double)philox_normal_t<T>(a.seed, a.chain0 + c, a.step, 0u, (uint32_t)(a.D * K + tid));
+      if (a.noise_mode == HMCX_NOISE_BUFFER) z = a.noise[a.noff[c] + a.D * K + j];
+      else z = (double)philox_normal_t<T>(a.seed, a.chain0 + c, a.step, 0u, (uint32_t)(a.D * K + j));
       const T p = (T)z;
       T q = a.b[col];
       if (take) { q = a.bwork[col]; a.b[col] = q; }
@@ -1200,13 +1229,11 @@ __global__ __launch_bounds__(256) void k_binit(InitArgs<T> a) {
       a.bwork[col] = q;
       kb = (double)p * (double)p;
     }
-    ksh[tid] = kb;
-    __syncthreads();
-    for (int s = 128; s > 0; s >>= 1) {
-      if (tid < s) ksh[tid] += ksh[tid + s];
-      __syncthreads();
-    }
-    if (tid == 0) a.kin0b[c] = ksh[0];
+    kb += __shfl_xor(kb, 1, 16);
+    kb += __shfl_xor(kb, 2, 16);
+    kb += __shfl_xor(kb, 4, 16);
+    kb += __shfl_xor(kb, 8, 16);
+    if (j == 0) a.kin0b[c] = kb;
   }
 }
 
@@ -1310,7 +1337,7 @@ int sghmc_batch_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
     ia.W = (T*)s->W; ia.b = (T*)s->b;
     ia.Wwork = Wwork; ia.bwork = bwork; ia.pW = pW; ia.pb = pb;
     ia.kin0_part = k0p; ia.kin0b = k0b;
-    hipLaunchKernelGGL((k_binit<T>), dim3(nDB16, C), dim3(256), 0, st, ia);
+    hipLaunchKernelGGL((k_binit<T>), dim3(nDB16, (C + 15) / 16), dim3(256), 0, st, ia);
     HMCX_HIP(ctx, hipGetLastError());
 
     BFwdArgs<T> f{};
