@@ -37,7 +37,7 @@ class SamplerArgs(ctypes.Structure):
                 ("W", c_void_p), ("b", c_void_p), ("out_A", c_void_p), ("out_accepted", c_void_p),
                 ("out_ll", c_void_p), ("out_E", c_void_p), ("pW", c_void_p), ("pb", c_void_p),
                 ("out_trace", c_void_p), ("out_abort", c_void_p), ("path_length", c_double),
-                ("out_L", c_void_p), ("out_mom", c_void_p)]
+                ("out_L", c_void_p), ("out_mom", c_void_p), ("out_host", c_void_p)]
 
 
 class MvnArgs(ctypes.Structure):

@@ -814,12 +814,24 @@ int hmcx_sghmc_run(hmcx_ctx* ctx, const hmcx_sampler_args* a_in) {
   if (a->pW || a->pb) return set_error(ctx, HMCX_EINVAL, "sghmc: pW/pb are SGLD-only fields");
   if (a->n_steps == 0) return HMCX_OK;
   const bool p2 = sghmc_p2_selected(ctx, a);
+  // the 2-D persistent path fills out_host itself (no device abort copy); the others are copied here
+  const bool host_by_kernel = p2 && !(a->dtype == HMCX_F64 && sghmc_rs_selected(ctx, a));
   if (a->out_abort && !p2) HMCX_HIP(ctx, hipMemsetAsync(a->out_abort, 0, sizeof(int32_t), ctx->stream));
   if (a->out_trace && p2)   // the persistent kernel stores the trace rows itself
-    return a->dtype == HMCX_F64 ? sghmc_run_t<double>(ctx, a) : sghmc_run_t<float>(ctx, a);
-  return run_traced(ctx, a, [ctx](const hmcx_sampler_args* s) {
-    return s->dtype == HMCX_F64 ? sghmc_run_t<double>(ctx, s) : sghmc_run_t<float>(ctx, s);
-  });
+    rc = a->dtype == HMCX_F64 ? sghmc_run_t<double>(ctx, a) : sghmc_run_t<float>(ctx, a);
+  else
+    rc = run_traced(ctx, a, [ctx](const hmcx_sampler_args* s) {
+      return s->dtype == HMCX_F64 ? sghmc_run_t<double>(ctx, s) : sghmc_run_t<float>(ctx, s);
+    });
+  if (rc || !a->out_host || host_by_kernel) return rc;
+  const size_t nsc = (size_t)a->n_steps * a->C;
+  char* h = reinterpret_cast<char*>(a->out_host);
+  HMCX_HIP(ctx, hipMemcpyAsync(h, a->out_A, 36 * nsc, hipMemcpyDeviceToHost, ctx->stream));
+  if (a->out_abort)
+    HMCX_HIP(ctx, hipMemcpyAsync(h + 36 * nsc, a->out_abort, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+  else
+    reinterpret_cast<int32_t*>(h + 36 * nsc)[0] = 0;
+  return HMCX_OK;
 }
 
 int hmcx_sgld_run(hmcx_ctx* ctx, const hmcx_sampler_args* a) {

@@ -221,6 +221,7 @@ template <typename T> int sghmc_run_t(hmcx_ctx*, const hmcx_sampler_args*);
 template <typename T> int hmc_run_t(hmcx_ctx*, const hmcx_hmc_args*);
 template <typename T> int axpy_t(hmcx_ctx*, int, int64_t, double, const void*, void*);
 bool sghmc_p2_selected(hmcx_ctx*, const hmcx_sampler_args*);   // hmcx_softmax.hip
+bool sghmc_rs_selected(hmcx_ctx*, const hmcx_sampler_args*);   // hmcx_rowspace.hip
 template <typename T> int sgld_run_t(hmcx_ctx*, const hmcx_sampler_args*);
 bool sgld_wide_eligible(const hmcx_sampler_args*);       // hmcx_wide.hip: one chain, K ≤ 64
 template <typename T> int sgld_wide_t(hmcx_ctx*, const hmcx_sampler_args*);

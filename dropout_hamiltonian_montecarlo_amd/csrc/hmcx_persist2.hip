@@ -965,6 +965,12 @@ int sghmc_p2_t(hmcx_ctx* ctx, const hmcx_sampler_args* s, const PersistPlan2& pl
   if ((rc = timing_begin(ctx, ctx->stream))) return rc;
   HMCX_HIP(ctx, hipLaunchKernel(kfn, dim3(G), dim3(QTH), kargs, (unsigned)pl.lds, ctx->stream));
   if ((rc = timing_end(ctx, ctx->stream))) return rc;
+  if (s->out_host) {                             // outputs and this launch's verdict, one copy each
+    char* h = reinterpret_cast<char*>(s->out_host);
+    HMCX_HIP(ctx, hipMemcpyAsync(h, s->out_A, 36 * n, hipMemcpyDeviceToHost, ctx->stream));
+    HMCX_HIP(ctx, hipMemcpyAsync(h + 36 * n, ctx->abort_dev, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    if (!dprof && !dtrace) return HMCX_OK;
+  }
   if (s->out_abort) {                            // the caller reads this launch's verdict itself
     HMCX_HIP(ctx, hipMemcpyAsync(s->out_abort, ctx->abort_dev, sizeof(int), hipMemcpyDeviceToDevice, ctx->stream));
     if (!dprof && !dtrace) return HMCX_OK;

@@ -140,8 +140,8 @@ class sghmc(sgmcmc):
 
     def _enqueue(self, state, data, rows, eps, rng, batch_size):
         """Prepare the schedule of len(rows) steps and enqueue them (one hmcx_sghmc_run call) without
-        waiting: the outputs travel back into a pinned host buffer behind the call (stream-ordered)
-        and a HIP event marks their arrival.  _collect waits on that event only, so a caller may
+        waiting: the call copies its outputs into a pinned host buffer behind its kernels (out_host,
+        stream-ordered) and a HIP event marks their arrival.  _collect waits on that event only, so a caller may
         enqueue the next call before collecting this one — the state stays on the device, stream
         order keeps the calls in sequence, and the host work of call k+1 overlaps the device work of
         call k."""
@@ -190,6 +190,7 @@ class sghmc(sgmcmc):
         a.step_base = self.global_step & 0xFFFFFFFF
         a.out_A, a.out_ll, a.out_E = base, base + 8 * nsc, base + 16 * nsc
         a.out_accepted, a.out_abort = base + 32 * nsc, base + 36 * nsc
+        a.out_host = slot['host'].data_ptr()          # outputs + abort word land here (include/hmcx.h)
         out_steps = None
         if self.record_steps:
             out_steps = torch.empty((n_steps, C, P), dtype=self.model.dtype, device=dev)
@@ -206,9 +207,6 @@ class sghmc(sgmcmc):
         ctx.check(ctx.lib.hmcx_sghmc_run(ctx.h, a), "hmcx_sghmc_run")
         if mark is not None:
             mark.append(('c call', time.perf_counter()))
-        slot['host'][:nbytes].copy_(slot['dev'][:nbytes], non_blocking=True)
-        if mark is not None:
-            mark.append(('d2h copy', time.perf_counter()))
         slot['ev'].record()
         if mark is not None:
             mark.append(('event', time.perf_counter()))

@@ -183,6 +183,12 @@ typedef struct hmcx_sampler_args {
   void* out_mom;           /* SGHMC, C < 16, or NULL: device [C][D*K+K] (dtype), the       */
                            /* momentum the call's LAST step returns (sghmc.py:36-39): the */
                            /* final p_new if accepted, else the drawn p                   */
+  void* out_host;          /* SGHMC or NULL: pinned host block that receives the call's     */
+                           /* outputs once the launch has finished: [n_steps*C f64 A]      */
+                           /* [.. f64 ll][2*n_steps*C f64 E][n_steps*C i32 accepted][i32   */
+                           /* abort].  out_A/out_ll/out_E/out_accepted must then be that    */
+                           /* layout in one device block; the call copies it behind its     */
+                           /* kernels (one copy of the block, one of the abort word).       */
 } hmcx_sampler_args;
 
 /* Replaces hamiltonian/inference/{cpu,gpu}/sghmc.py:19-39 (step, with the A1 completion:
