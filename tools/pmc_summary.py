@@ -7,8 +7,9 @@
 HBM/fabric bytes per launch = 2·FETCH_SIZE + WRITE_SIZE (kB units; MI355X_MICROARCH.md HBM section:
 FETCH_SIZE counts half the bytes of 16-byte-per-lane reads, WRITE_SIZE is exact for 16-byte stores;
 both include Infinity-Cache hits).  The bench JSON of the profiled run says how many timed calls it
-made (roofline.calls) and how many leapfrogs they ran: the last `calls` dispatches of the kernel are
-the timed launches, and their bytes ÷ their leapfrogs is the per-leapfrog figure bench.py scales.
+made (roofline.calls) and how many leapfrogs they ran: the timed launches are the `calls` dispatches
+after the warm-up ones (bench.py runs warm-up, timed, then the untimed diagnostics calls), and their
+bytes ÷ their leapfrogs is the per-leapfrog figure bench.py scales.
 """
 import csv
 import glob
@@ -39,8 +40,10 @@ def main():
     calls = int(b["roofline"]["calls"])
     lf = float(b["leapfrogs"])
     steps = int(b["steps"])
-    fm = sum(fetch[-calls:]) / calls
-    wm = sum(write[-calls:]) / calls
+    chunk = 120                                         # bench.py: one call per epoch of 60000 / 500 rows
+    w0 = -(-int(b["warmup"]) // chunk)                  # warm-up dispatches before the timed ones
+    fm = sum(fetch[w0:w0 + calls]) / calls
+    wm = sum(write[w0:w0 + calls]) / calls
     per_launch_bytes = (2.0 * fm + wm) * 1024.0
     lf_per_launch = lf / calls
     alg = 500 * 784 * 8 * steps / calls
