@@ -172,25 +172,46 @@ class sghmc(sgmcmc):
         base = slot['dev'].data_ptr()
         if mark is not None:
             mark.append(('io slot', time.perf_counter()))
-        row0 = np.asarray(rows, dtype=np.int64)
-        eps_a = np.asarray(eps, dtype=np.float64)
-        a = nat.SamplerArgs.from_buffer_copy(self._call_template(Xd, Yd, W, b, batch_size, D, K, C))
+        fast = philox and not self.record_steps and not self.__dict__.get('_want_mom')
+        if fast:
+            # the slot keeps its argument struct and host schedule arrays between calls of the same
+            # shape: a call only refills the step rows / sizes and the step id
+            key = (Xd.data_ptr(), Yd.data_ptr(), W.data_ptr(), b.data_ptr(), batch_size, C, n_steps, base,
+                   slot['host'].data_ptr(), self.path_length, self.seed, self.chain)
+            ac = slot.get('acache')
+            if ac is None or ac[0] != key:
+                a = nat.SamplerArgs.from_buffer_copy(self._call_template(Xd, Yd, W, b, batch_size, D, K, C))
+                r0b, epb, Lb = np.empty(n_steps, np.int64), np.empty(n_steps), np.empty(nsc)
+                a.n_steps = n_steps
+                a.row0, a.eps, a.out_L = nat.addr(r0b), nat.addr(epb), nat.addr(Lb)
+                a.out_A, a.out_ll, a.out_E = base, base + 8 * nsc, base + 16 * nsc
+                a.out_accepted = base + 32 * nsc
+                a.out_host = slot['host'].data_ptr()
+                slot['acache'] = ac = (key, a, r0b, epb, Lb)
+            _, a, row0, eps_a, L_out = ac
+            row0[:] = rows
+            eps_a[:] = eps
+            a.out_abort = base + 36 * nsc
+        else:
+            row0 = np.asarray(rows, dtype=np.int64)
+            eps_a = np.asarray(eps, dtype=np.float64)
+            a = nat.SamplerArgs.from_buffer_copy(self._call_template(Xd, Yd, W, b, batch_size, D, K, C))
+            a.n_steps = n_steps
+            a.row0 = nat.addr(row0)
+            a.eps = nat.addr(eps_a)
+            if philox:
+                a.out_L = nat.addr(L_out)
+            else:
+                a.n_iter = nat.addr(n_iter)
+                a.u_accept = nat.addr(u)
+                a.noise = ptr(noise_d)
+                a.noise_off = nat.addr(noise_off)
+            a.out_A, a.out_ll, a.out_E = base, base + 8 * nsc, base + 16 * nsc
+            a.out_accepted, a.out_abort = base + 32 * nsc, base + 36 * nsc
+            a.out_host = slot['host'].data_ptr()      # outputs + abort word land here (include/hmcx.h)
         if mark is not None:
             mark.append(('template', time.perf_counter()))
-        a.n_steps = n_steps
-        a.row0 = nat.addr(row0)
-        a.eps = nat.addr(eps_a)
-        if philox:
-            a.out_L = nat.addr(L_out)
-        else:
-            a.n_iter = nat.addr(n_iter)
-            a.u_accept = nat.addr(u)
-            a.noise = ptr(noise_d)
-            a.noise_off = nat.addr(noise_off)
         a.step_base = self.global_step & 0xFFFFFFFF
-        a.out_A, a.out_ll, a.out_E = base, base + 8 * nsc, base + 16 * nsc
-        a.out_accepted, a.out_abort = base + 32 * nsc, base + 36 * nsc
-        a.out_host = slot['host'].data_ptr()          # outputs + abort word land here (include/hmcx.h)
         out_steps = None
         if self.record_steps:
             out_steps = torch.empty((n_steps, C, P), dtype=self.model.dtype, device=dev)
