@@ -19,6 +19,14 @@ constexpr unsigned long long QTIMEOUT = 400000000ull;   // s_memrealtime ticks (
 typedef unsigned int gran_t __attribute__((ext_vector_type(4)));
 __host__ __device__ inline int p2_pad(int n, int pad) { return pad ? (n + 7) & ~7 : n; }
 
+// The thread index as a value the compiler cannot see through: index arithmetic derived from it is
+// recomputed where it is used instead of being hoisted out of the step loop and kept live (the
+// hoisted offsets of every gather and load batch exceeded the register file and spilled).
+__device__ inline int opaque(int x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+
 // ---------------------------------------------------------------- granule transport
 __device__ inline __amdgpu_buffer_rsrc_t arena_rsrc(char* base, int bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(base, 0, bytes, 0x00020000);
@@ -178,9 +186,10 @@ __device__ inline bool gather_u(__amdgpu_buffer_rsrc_t rs, int base0, int pstrid
                                 Want want, unsigned ep, int* abort_flag, double* stage) {
   unsigned pend = 0;
   int o[U], qi[U];
+  const int t0i = opaque((int)threadIdx.x);
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    const int q = threadIdx.x + u * QTH;
+    const int q = t0i + u * QTH;
     const int p = q / nitems, i = q - p * nitems;
     const bool w = q < np * nitems && want(p, i);
     pend |= w ? 1u << u : 0u;
@@ -210,6 +219,56 @@ __device__ inline bool gather_u(__amdgpu_buffer_rsrc_t rs, int base0, int pstrid
   }
   return true;
 }
+// gather_u with the destination chosen per pair: store(q, v) for pair q = p·nitems + i (e.g. straight
+// into the consumer's LDS layout, saving a staging copy and its barrier).
+template <int U, typename Off, typename Store>
+__device__ inline bool gather_st_u(__amdgpu_buffer_rsrc_t rs, int base0, int pstride, int np, int nitems, Off ioff,
+                                   unsigned ep, int* abort_flag, Store store) {
+  unsigned pend = 0;
+  int o[U], qi[U];
+  const int t0i = opaque((int)threadIdx.x);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int q = t0i + u * QTH;
+    const int p = q / nitems, i = q - p * nitems;
+    const bool w = q < np * nitems;
+    pend |= w ? 1u << u : 0u;
+    o[u] = (base0 + (w ? p * pstride + ioff(i) : 0)) * 16;
+    qi[u] = q;
+  }
+  unsigned long long t0 = 0;
+  for (int spins = 0; pend; ++spins) {
+    gran_t v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, o[u], 0, 16 /* sc1 */);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (((pend >> u) & 1u) && v[u].y == ep && v[u].w == ep) {
+        store(qi[u], decode(v[u]));
+        pend &= ~(1u << u);
+      }
+    if (!pend) break;
+    if (spins == 0) t0 = __builtin_amdgcn_s_memrealtime();
+    if ((spins & 63) == 63 &&
+        (__builtin_amdgcn_s_memrealtime() - t0 > QTIMEOUT ||
+         __hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+      __hip_atomic_store(abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    if (HMCX_P2_SLEEP) __builtin_amdgcn_s_sleep(1);
+  }
+  return true;
+}
+template <typename Off, typename Store>
+__device__ inline bool gather_st(__amdgpu_buffer_rsrc_t rs, int base0, int pstride, int np, int nitems, Off ioff,
+                                 unsigned ep, int* abort_flag, Store store) {
+  const int u = (np * nitems + QTH - 1) / QTH;
+  if (u <= 1) return gather_st_u<1>(rs, base0, pstride, np, nitems, ioff, ep, abort_flag, store);
+  if (u == 2) return gather_st_u<2>(rs, base0, pstride, np, nitems, ioff, ep, abort_flag, store);
+  if (u == 3) return gather_st_u<3>(rs, base0, pstride, np, nitems, ioff, ep, abort_flag, store);
+  return gather_st_u<4>(rs, base0, pstride, np, nitems, ioff, ep, abort_flag, store);
+}
+
 template <typename Off, typename Want>
 __device__ inline bool gather(__amdgpu_buffer_rsrc_t rs, int base0, int pstride, int np, int nitems, Off ioff,
                               Want want, unsigned ep, int* abort_flag, double* stage) {

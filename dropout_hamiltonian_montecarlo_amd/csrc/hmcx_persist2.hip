@@ -298,6 +298,7 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
   // ---- phase A: partial logits X[R_r,F_f]·W[F_f] → XA(par, r, f) [nrow][KC], then A-RS consume:
   //      Zo[ii][k] = Σ_f' partials of my rows (f' order)
   auto roundA = [&]() -> bool {
+    const int tid = opaque((int)threadIdx.x), lane = tid & 63, wave = tid >> 6, lr = lane & 15;   // not hoisted (registers)
     ++ep;
     const int reg = a.oXA + (((int)(uA & 1) * Gr + r) * Gf + f) * Br * KC;
     const int nkp = WPA == 1 ? (nfeat + 3) / 4 : (BfP / 4) / WPA;   // zero-padded tail skipped
@@ -328,6 +329,7 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
     return true;
   };
   auto consumeA = [&]() -> bool {
+    const int tid = opaque((int)threadIdx.x), lane = tid & 63, wave = tid >> 6, lr = lane & 15;   // not hoisted (registers)
     const int base0 = a.oXA + ((int)(uA & 1) * Gr + r) * Gf * Br * KC;
     ++uA;
     if (a.spread & 1) {
@@ -351,6 +353,7 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
   };
 
   for (int s = 0; s < a.n_steps; ++s) {
+    const int tid = opaque((int)threadIdx.x), lane = tid & 63, wave = tid >> 6, lr = lane & 15;   // not hoisted (registers)
     const double epsd = a.eps[s];
     const T eps = (T)epsd, ome = (T)(1.0 - epsd), nsc = (T)(2.0 * epsd);
     const int n = a.n_iter[s];
@@ -408,6 +411,7 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
 
     double kin1 = 0.0;
     for (int it = 0; it < n; ++it) {
+      const int tid = opaque((int)threadIdx.x), lane = tid & 63, wave = tid >> 6, lr = lane & 15;   // not hoisted (registers)
       const bool last = it == n - 1;
       if (it == 0) {
         // drift of the whole F_f slice by p0 (every member computes it identically; sghmc.py:32)
@@ -519,17 +523,22 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
         ++uD;
         bool ok;
         if (a.spread & 2) {
-          ok = gather(rs, base0, NXA, Gf, NXA0, [](int i) { return i; }, all_items, ep, a.abort_flag, stg);
-          if (!all_ok(ok, ish)) return;
-          if (tid < HA) {
-            hv = stg[tid];
-            for (int p = 1; p < Gf; ++p) hv += stg[p * NXA0 + tid];
-          }
-          for (int q = tid; q < Gf * NXA0; q += QTH) {
+          // diff rows straight into Ds, headers into stg (no staging copy, no second barrier)
+          ok = gather_st(rs, base0, NXA, Gf, NXA0, [](int i) { return i; }, ep, a.abort_flag, [&](int q, double v) {
             const int p = q / NXA0, t = q - p * NXA0;
-            if (t >= HA) Ds[(p * Ro + (t - HA) / KC) * 16 + (t - HA) % KC] = (T)stg[q];
+            if (t < HA) stg[q] = v;
+            else Ds[(p * Ro + (t - HA) / KC) * 16 + (t - HA) % KC] = (T)v;
+          });
+          if (!all_ok(ok, ish)) return;
+          if (tid < HA) {                           // producer order; the loads issued together
+            double hvs[QNPM];
+#pragma unroll
+            for (int p = 0; p < QNPM; ++p) hvs[p] = stg[min(p, Gf - 1) * NXA0 + tid];
+            hv = hvs[0];
+#pragma unroll
+            for (int p = 1; p < QNPM; ++p)
+              if (p < Gf) hv += hvs[p];
           }
-          __syncthreads();
         } else if (tid < HA) {
           ok = poll<true>(rs, base0, NXA, Gf, -1, tid, true, ep, nullptr, 0, &hv, a.abort_flag);
         } else {

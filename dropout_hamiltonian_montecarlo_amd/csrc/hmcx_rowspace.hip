@@ -194,14 +194,6 @@ __device__ inline double rs_noise(const RSArgs& a, int s, uint32_t slot, uint32_
   return philox_normal_d(a.seed, a.chain0, a.step_base + (uint32_t)s, slot, e);
 }
 
-// The thread index as a value the compiler cannot see through: index arithmetic derived from it is
-// recomputed where it is used instead of being hoisted out of the step loop and kept live (the
-// hoisted offsets of every gather and load batch exceeded the register file and spilled).
-__device__ inline int opaque(int x) {
-  asm volatile("" : "+v"(x));
-  return x;
-}
-
 // All-gather of np producers × nitems granules (producer p's item i at base0 + p·pstride + i), U
 // granules per thread in one batch of loads.  Item i < nsplit lands in dstA[p·nsplit + i] (pairs with
 // p·nsplit + i ≥ limA are not polled), the others in dstB[p·(nitems − nsplit) + i − nsplit].
