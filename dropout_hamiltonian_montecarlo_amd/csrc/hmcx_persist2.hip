@@ -201,19 +201,27 @@ __device__ inline typename mfma16<T>::acc_t mfma_tile(const T* a, int as_i, int 
   return c0 + c1;
 }
 
-template <typename T, int KC>
+template <typename T, int KC, int SPEC = 0>
 __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
   using M = mfma16<T>;
+  // SPEC = 1: the plan of BASELINE config 2 (f64, B=500, D=784, K=10: 8 x 16 teams, 64-row x 49-feature
+  // tiles) with every knob at its default, folded into constants — fewer live scalars (the generic
+  // kernel spills SGPRs into VGPR lanes) and no runtime branches on the knobs
+  constexpr bool SP = SPEC != 0;
+  const int spread = SP ? 2 : a.spread, pad = SP ? 1 : a.pad, xmap = SP ? 0 : a.xmap, fl2 = SP ? 1 : a.fl2,
+            al2 = SP ? 0 : a.al2, prefetch = SP ? 1 : a.prefetch, acc1 = SP ? 1 : a.acc1,
+            zoffa = SP ? 1 : a.zoff, bara = SP ? 1 : a.bar;
   extern __shared__ __align__(16) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15;
-  const int Gr = a.Gr, Gf = a.Gf, G = Gr * Gf;
+  const int Gr = SP ? 8 : a.Gr, Gf = SP ? 16 : a.Gf, G = Gr * Gf;
   // workgroups are dealt to the 8 XCDs round-robin by blockIdx: with the identity map feature team
   // f (blocks f, f+Gf, …) shares an XCD when Gf % 8 == 0; xmap = 1 puts each row team on one XCD
   const int pbid = blockIdx.x;
-  const int bid = a.xmap ? (pbid & 7) * (G >> 3) + (pbid >> 3) : pbid;
+  const int bid = xmap ? (pbid & 7) * (G >> 3) + (pbid >> 3) : pbid;
   const int r = bid / Gf, f = bid - (bid / Gf) * Gf;
-  const int Br = a.Br, Bf = a.Bf, BfP = a.BfP, BFP = a.BFP, Ro = a.Ro, Fo = a.Fo;
-  const int K = a.K, D = a.D, B = a.B;
+  const int Br = SP ? 64 : a.Br, Bf = SP ? 49 : a.Bf, BfP = SP ? 64 : a.BfP, BFP = SP ? 66 : a.BFP, Ro = SP ? 4 : a.Ro,
+            Fo = SP ? 7 : a.Fo;
+  const int K = SP ? 10 : a.K, D = SP ? 784 : a.D, B = SP ? 500 : a.B;
   const int row0 = r * Br, feat0 = f * Bf;
   const int nrow = max(0, min(Br, B - row0));
   const int nfeat = max(0, min(Bf, D - feat0));
@@ -227,11 +235,11 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
   const int MTA = Br / 16, WPA = max(1, QNW / MTA);
   const int MTB = BfP / 16, WPB = max(1, QNW / MTB);
   const int HA = KC + 1;                              // payload header: colsum[KC], ll
-  // payload blocks per producer, rounded to whole 128-byte lines (8 granules) when a.pad is set
+  // payload blocks per producer, rounded to whole 128-byte lines (8 granules) when pad is set
   const int NXA0 = HA + Ro * KC;                      // A-AG payload per producer
-  const int NXA = p2_pad(NXA0, a.pad);                // ... and its block stride
-  const int NXB = p2_pad(HA + Bf * KC, a.pad);        // B-RS payload per producer
-  const int NXS = a.pad ? 8 : 4;                      // accept partials per workgroup
+  const int NXA = p2_pad(NXA0, pad);                // ... and its block stride
+  const int NXB = p2_pad(HA + Bf * KC, pad);        // B-RS payload per producer
+  const int NXS = pad ? 8 : 4;                      // accept partials per workgroup
 
   // ---- LDS carve-up (mirrored by p2_lds)
   T* Xs = reinterpret_cast<T*>(smem);                 // [Br][BFP]
@@ -260,9 +268,9 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
   T* pWs = zbuf + Fo * 16 + 16;                       // [BfP][16] momentum of the whole slice (bar)
   // friction noise by the waves that do not poll A-RS (threads from NZ0 on), when they fit
   const int NZ0 = ((nro * KC + 63) / 64) * 64;
-  const bool zoff = a.zoff && !(a.spread & 1) && NZ0 + Fo * KC + K <= QTH;
-  // B all-reduce (a.bar) needs the owners' noise in LDS (zoff) to fold it into their partials
-  const bool bar = a.bar && zoff;
+  const bool zoff = zoffa && !(spread & 1) && NZ0 + Fo * KC + K <= QTH;
+  // B all-reduce (bara) needs the owners' noise in LDS (zoff) to fold it into their partials
+  const bool bar = bara && zoff;
   const auto all_items = [](int, int) { return true; };
 
   // owned weight of this thread: feature fo0 + od, class ok (thread t = od·KC + ok)
@@ -310,7 +318,7 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int row = mt * 16 + M::row(lane, q);
-          if (row < nrow && lr < KC) put_t(a.al2, rs, reg + row * KC + lr, (double)c[q], ep);
+          if (row < nrow && lr < KC) put_t(al2, rs, reg + row * KC + lr, (double)c[q], ep);
         }
       } else {
 #pragma unroll
@@ -323,7 +331,7 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
         const int i = e / KC, k = e - (e / KC) * KC;
         T v = Zp[i * 16 + k];
         for (int p = 1; p < WPA; ++p) v += Zp[(p * Br + i) * 16 + k];
-        put_t(a.al2, rs, reg + e, (double)v, ep);
+        put_t(al2, rs, reg + e, (double)v, ep);
       }
     }
     return true;
@@ -332,7 +340,7 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
     const int tid = opaque((int)threadIdx.x), lane = tid & 63, wave = tid >> 6, lr = lane & 15;   // not hoisted (registers)
     const int base0 = a.oXA + ((int)(uA & 1) * Gr + r) * Gf * Br * KC;
     ++uA;
-    if (a.spread & 1) {
+    if (spread & 1) {
       const int ni = nro * KC;
       const bool ok = gather(rs, base0, Br * KC, Gf, ni, [&](int i) { return ro0 * KC + i; }, all_items, ep,
                              a.abort_flag, stg);
@@ -367,7 +375,7 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
 
     // ---- step start: tile, labels of my rows (step 0 only: later steps' were loaded while the
     //      previous accept round travelled), momentum (hmc.py:82-87), step-start copies
-    if (s == 0 || !a.prefetch) load_step_rows<T>(Xs, Yo, Xg, Yg, Br, BfP, BFP, nrow, nfeat, row0, feat0, D, K, Ro, nro, ro0);
+    if (s == 0 || !prefetch) load_step_rows<T>(Xs, Yo, Xg, Yg, Br, BfP, BFP, nrow, nfeat, row0, feat0, D, K, Ro, nro, ro0);
     for (int e = tid; e < BfP * 16; e += QTH) Wf0[e] = Wf[e];
     pw = own ? noise1<T>(a, s, 0u, (uint32_t)e_own) : T(0);
     const T pw0 = pw;
@@ -516,13 +524,13 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
             const int m = t - HA;
             v = (double)Dme[(m / KC) * 16 + (m % KC)];
           }
-          put_t(a.al2, rs, reg + t, v, ep);
+          put_t(al2, rs, reg + t, v, ep);
         }
         tstamp(s, it, 2);
         const int base0 = a.oXD + ((int)(uD & 1) * Gr + r) * Gf * NXA;
         ++uD;
         bool ok;
-        if (a.spread & 2) {
+        if (spread & 2) {
           // diff rows straight into Ds, headers into stg (no staging copy, no second barrier)
           ok = gather_st(rs, base0, NXA, Gf, NXA0, [](int i) { return i; }, ep, a.abort_flag, [&](int q, double v) {
             const int p = q / NXA0, t = q - p * NXA0;
@@ -546,7 +554,7 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
           ok = poll<false>(rs, base0, NXA, Gf, -1, tid, tid < NXA0, ep, nullptr, 0, nullptr, a.abort_flag,
                            Ds + (m / KC) * 16 + (m % KC), Ro * 16);
         }
-        if (!(a.spread & 2) && !all_ok(ok, ish)) return;
+        if (!(spread & 2) && !all_ok(ok, ish)) return;
         tstamp(s, it, 3);
       }
 
@@ -555,7 +563,7 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
       {
         ++ep;
         const int reg = a.oXB + (((int)(uB & 1) * Gf + f) * Gr + r) * NXB;
-        if (tid < HA) put_t(a.fl2, rs, reg + tid, hv, ep);
+        if (tid < HA) put_t(fl2, rs, reg + tid, hv, ep);
         // bar: the owner of an element folds its friction noise into its partial — Σ partials − 2z, so
         // ε·(−(Σ − 2z − αw)) = ε·g + 2ε·z (sghmc.py:31,34) arrives with the all-reduce and no other
         // member has to draw that noise
@@ -571,7 +579,7 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
               const int d = mt * 16 + M::row(lane, q);
-              if (d < nfeat && lr < KC) put_t(a.fl2, rs, reg + HA + d * KC + lr, bpart(d, lr, (double)c[q]), ep);
+              if (d < nfeat && lr < KC) put_t(fl2, rs, reg + HA + d * KC + lr, bpart(d, lr, (double)c[q]), ep);
             }
           } else {
 #pragma unroll
@@ -584,7 +592,7 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
             const int i = e / KC, k = e - (e / KC) * KC;
             T v = Zp[i * 16 + k];
             for (int q = 1; q < WPB; ++q) v += Zp[(q * BfP + i) * 16 + k];
-            put_t(a.fl2, rs, reg + HA + e, bpart(i, k, (double)v), ep);
+            put_t(fl2, rs, reg + HA + e, bpart(i, k, (double)v), ep);
           }
         }
         const int base0 = a.oXB + ((int)(uB & 1) * Gf + f) * Gr * NXB;
@@ -641,7 +649,7 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
         double sum = 0.0;
         const bool isg = tid < ng, ish_ = tid >= ng && tid < ng + HA;
         const int offB = isg ? HA + fo0 * KC + tid : tid - ng;
-        if (a.spread & 4) {
+        if (spread & 4) {
           const int ni = ng + HA;
           const bool ok = gather(rs, base0, NXB, Gr, ni, [&](int i) { return i < ng ? HA + fo0 * KC + i : i - ng; },
                                  all_items, ep, a.abort_flag, stg);
@@ -653,7 +661,7 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
           if (ish_) hdr[tid - ng] = sum;
           __syncthreads();
         } else {
-          const bool ok = a.fl2 ? poll<true, double, 16>(rs, base0, NXB, Gr, -1, offB, isg || ish_, ep, nullptr, 0, &sum,
+          const bool ok = fl2 ? poll<true, double, 16>(rs, base0, NXB, Gr, -1, offB, isg || ish_, ep, nullptr, 0, &sum,
                                                         a.abort_flag)
                                 : poll<true>(rs, base0, NXB, Gr, -1, offB, isg || ish_, ep, nullptr, 0, &sum, a.abort_flag);
           if (ish_) hdr[tid - ng] = sum;
@@ -681,14 +689,14 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
       prof.stamp(9);
       {
         ++ep;
-        const int per = p2_pad(Fo * KC, a.pad);
+        const int per = p2_pad(Fo * KC, pad);
         const int reg = a.oXW + (((int)(uW & 1) * Gf + f) * Gr + r) * per;
-        if (tid < nfo * KC) put_t(a.fl2, rs, reg + tid, own ? (double)wv : 0.0, ep);
+        if (tid < nfo * KC) put_t(fl2, rs, reg + tid, own ? (double)wv : 0.0, ep);
         tstamp(s, it, 6);
         if (own) Wf[wl] = wv;
         const int base0 = a.oXW + ((int)(uW & 1) * Gf + f) * Gr * per;
         ++uW;
-        if (a.spread & 8) {
+        if (spread & 8) {
           const int ni = Fo * KC;
           const auto want = [&](int p, int i) { return p != r && p < min(Gr, (nfeat - i / KC + Fo - 1) / Fo); };
           const bool ok = gather(rs, base0, per, Gr, ni, [](int i) { return i; }, want, ep, a.abort_flag, stg);
@@ -703,7 +711,7 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
         }
         const int dloc = tid / KC, kk = tid - (tid / KC) * KC;
         const int npd = tid < Fo * KC ? min(Gr, (nfeat - dloc + Fo - 1) / Fo) : 0;   // producers owning feature dloc
-        const bool ok = a.fl2 ? poll<false, T, 16>(rs, base0, per, npd, r, tid, tid < Fo * KC, ep, nullptr, 0, nullptr,
+        const bool ok = fl2 ? poll<false, T, 16>(rs, base0, per, npd, r, tid, tid < Fo * KC, ep, nullptr, 0, nullptr,
                                                   a.abort_flag, Wf + dloc * 16 + kk, Fo * 16)
                               : poll<false>(rs, base0, per, npd, r, tid, tid < Fo * KC, ep, nullptr, 0, nullptr,
                                             a.abort_flag, Wf + dloc * 16 + kk, Fo * 16);
@@ -727,7 +735,7 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
     }
     // next step's tile and labels while the partials travel: Xs and Yo have no reader left in this
     // step (the last B-gemm and softmax ended before a barrier)
-    if (a.prefetch && s + 1 < a.n_steps) {
+    if (prefetch && s + 1 < a.n_steps) {
       const T* Xn = reinterpret_cast<const T*>(a.X) + (size_t)a.row0[s + 1] * D;
       const T* Yn = reinterpret_cast<const T*>(a.Y) + (size_t)a.row0[s + 1] * K;
       load_step_rows<T>(Xs, Yo, Xn, Yn, Br, BfP, BFP, nrow, nfeat, row0, feat0, D, K, Ro, nro, ro0);
@@ -735,7 +743,7 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
     const int sbase = a.oXS + (int)(uS & 1) * G * NXS;
     ++uS;
     double v3[3] = {0.0, 0.0, 0.0};
-    if (a.acc1) {
+    if (acc1) {
       // the three partials of workgroup tid in one batch of loads (one round trip, not three)
       const bool ok = poll_nb<1, false, double>(rs, sbase + tid * NXS, 1, 3, -1, 0, tid < G, ep, nullptr,
                                                 a.abort_flag, stg + 3 * tid, 1);
@@ -776,7 +784,7 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
       if (bid == 0 && tid < K) mo[D * K + tid] = keep_new ? pbsh[tid] : pb0sh[tid];
     }
     if (a.out_trace) {                                                     // sghmc_multicore.py:49-51 row
-      T* tr = reinterpret_cast<T*>(a.out_trace) + (size_t)s * a.P;
+      T* tr = reinterpret_cast<T*>(a.out_trace) + (size_t)s * (D * K + K);
       if (own) tr[e_own] = wv;
       if (bid == 0 && tid < K) tr[D * K + tid] = bsh[tid];
     }
@@ -963,7 +971,14 @@ int sghmc_p2_t(hmcx_ctx* ctx, const hmcx_sampler_args* s, const PersistPlan2& pl
     HMCX_HIP(ctx, hipMemsetAsync(dtrace, 0, ntr * sizeof(unsigned long long), ctx->stream));
   }
   a.trace = dtrace;
-  const void* kfn = KC == 10 ? (const void*)k_sghmc_p2<T, 10> : (const void*)k_sghmc_p2<T, 16>;
+  // the folded instantiation when the call is exactly BASELINE config 2's plan with default knobs
+  const bool spec = sizeof(T) == 8 && KC == 10 && s->B == 500 && s->D == 784 && K == 10 && pl.Gr == 8 && pl.Gf == 16 &&
+                    pl.Br == 64 && pl.Bf == 49 && pl.BfP == 64 && pl.BFP == 66 && pl.Ro == 4 && pl.Fo == 7 &&
+                    a.spread == 2 && a.pad == 1 && a.xmap == 0 && a.fl2 == 1 && a.al2 == 0 && a.prefetch == 1 &&
+                    a.acc1 == 1 && a.zoff == 1 && a.bar == 1;
+  static const bool no_spec = getenv("HMCX_P2_SPEC") && getenv("HMCX_P2_SPEC")[0] == '0';
+  const void* kfn = (spec && !no_spec) ? (const void*)k_sghmc_p2<T, 10, 1>
+                    : KC == 10 ? (const void*)k_sghmc_p2<T, 10> : (const void*)k_sghmc_p2<T, 16>;
   void* kargs[] = {&a};
   // co-residency of all G workgroups is checked here (occupancy query × CUs, cached per kernel); a
   // plain launch then has the same residency as a cooperative one without its per-launch host cost

@@ -76,15 +76,19 @@ def _gpu(kind, cfg, T, dtype=torch.float64, path=0, batched=False):
         acc = np.array([t.get("accepted", True) for t in s.trace])
         return post, acc
 
-    if batched:
-        post, acc = run(0, C)
-        return _flat(post, (C, T)), np.asarray(acc, dtype=bool).T
-    draws, accs = [], []
-    for c in range(C):
-        post, acc = run(c, 1)
-        draws.append(_flat(post, (T,)))
-        accs.append(acc)
-    return np.stack(draws), np.stack(accs).astype(bool)
+    try:
+        if batched:
+            post, acc = run(0, C)
+            return _flat(post, (C, T)), np.asarray(acc, dtype=bool).T
+        draws, accs = [], []
+        for c in range(C):
+            post, acc = run(c, 1)
+            draws.append(_flat(post, (T,)))
+            accs.append(acc)
+        return np.stack(draws), np.stack(accs).astype(bool)
+    finally:
+        if kind == "sghmc":
+            m.ctx.set_sghmc_path(0)                     # the context is shared by later tests
 
 
 def _check(gpu, ora, acc_g=None, acc_o=None):
