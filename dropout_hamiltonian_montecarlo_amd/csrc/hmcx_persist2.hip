@@ -294,9 +294,9 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
   __syncthreads();
   if (own) wv = Wf[wl];
 
-  P2Prof prof{(bid == 0 && tid == 0) ? a.prof : nullptr, profacc, 0ull, 0};
+  P2Prof prof{(!SP && bid == 0 && tid == 0) ? a.prof : nullptr, profacc, 0ull, 0};   // SPEC: compiled out
   // round trace: slot 2·round = payload published, 2·round + 1 = consumed (rounds A, D, B, W)
-  unsigned long long* trb = a.trace ? a.trace + (size_t)bid * P2TR_IT * 8 : nullptr;
+  unsigned long long* trb = (!SP && a.trace) ? a.trace + (size_t)bid * P2TR_IT * 8 : nullptr;
   auto tstamp = [&](int s_, int it_, int slot) {
     if (trb && tid == 0 && s_ == 0 && it_ >= 0 && it_ < P2TR_IT) trb[it_ * 8 + slot] = __builtin_amdgcn_s_memrealtime();
   };
@@ -975,7 +975,7 @@ int sghmc_p2_t(hmcx_ctx* ctx, const hmcx_sampler_args* s, const PersistPlan2& pl
   const bool spec = sizeof(T) == 8 && KC == 10 && s->B == 500 && s->D == 784 && K == 10 && pl.Gr == 8 && pl.Gf == 16 &&
                     pl.Br == 64 && pl.Bf == 49 && pl.BfP == 64 && pl.BFP == 66 && pl.Ro == 4 && pl.Fo == 7 &&
                     a.spread == 2 && a.pad == 1 && a.xmap == 0 && a.fl2 == 1 && a.al2 == 0 && a.prefetch == 1 &&
-                    a.acc1 == 1 && a.zoff == 1 && a.bar == 1;
+                    a.acc1 == 1 && a.zoff == 1 && a.bar == 1 && !a.prof && !a.trace;
   static const bool no_spec = getenv("HMCX_P2_SPEC") && getenv("HMCX_P2_SPEC")[0] == '0';
   const void* kfn = (spec && !no_spec) ? (const void*)k_sghmc_p2<T, 10, 1>
                     : KC == 10 ? (const void*)k_sghmc_p2<T, 10> : (const void*)k_sghmc_p2<T, 16>;
