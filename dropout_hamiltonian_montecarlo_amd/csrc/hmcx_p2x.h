@@ -22,6 +22,13 @@ __host__ __device__ inline int p2_pad(int n, int pad) { return pad ? (n + 7) & ~
 // The thread index as a value the compiler cannot see through: index arithmetic derived from it is
 // recomputed where it is used instead of being hoisted out of the step loop and kept live (the
 // hoisted offsets of every gather and load batch exceeded the register file and spilled).
+// A uniform 64-bit value the compiler must re-read at this point (kept scalar): derived constants
+// (the Philox key schedule of a seed) are recomputed per use instead of being hoisted and spilled.
+__device__ inline uint64_t opaque_s64(uint64_t x) {
+  uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  asm volatile("" : "+s"(lo), "+s"(hi));
+  return ((uint64_t)hi << 32) | lo;
+}
 __device__ inline int opaque(int x) {
   asm volatile("" : "+v"(x));
   return x;

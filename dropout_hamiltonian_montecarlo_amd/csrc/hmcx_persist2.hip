@@ -107,13 +107,13 @@ __device__ inline T noise_at(const Q2Args& a, int s, uint32_t slot, uint32_t e, 
 }
 template <typename T>
 __device__ inline void philox4_if(const Q2Args& a, int s, uint32_t slot, uint32_t g, T z[4]) {
-  if (a.noise_mode != HMCX_NOISE_BUFFER) philox_normal4(a.seed, a.chain0, a.step_base + (uint32_t)s, slot, g, z);
+  if (a.noise_mode != HMCX_NOISE_BUFFER) philox_normal4(opaque_s64(a.seed), a.chain0, a.step_base + (uint32_t)s, slot, g, z);
 }
 // One element's noise (f32 chains: float Box–Muller; f64 chains: the double one, hmcx_common.h).
 template <typename T>
 __device__ inline T noise1(const Q2Args& a, int s, uint32_t slot, uint32_t e) {
   if (a.noise_mode == HMCX_NOISE_BUFFER) return (T)a.noise[a.noff[s] + (int64_t)slot * a.P + e];
-  return philox_normal_t<T>(a.seed, a.chain0, a.step_base + (uint32_t)s, slot, e);
+  return philox_normal_t<T>(opaque_s64(a.seed), a.chain0, a.step_base + (uint32_t)s, slot, e);
 }
 
 // Minibatch tile X[row0:+nrow, feat0:+nfeat] → LDS [Br][BFP], zero padded to BfP columns;
