@@ -96,7 +96,7 @@ EXPORTS = ("hmcx_version", "hmcx_create", "hmcx_destroy", "hmcx_last_error", "hm
            "hmcx_sgld_run", "hmcx_hmc_mvn_run", "hmcx_mlp_masks", "hmcx_mlp_grad", "hmcx_mlp_loss",
            "hmcx_mlp_sghmc_run", "hmcx_logistic_grad", "hmcx_logistic_loglik", "hmcx_logistic_predict",
            "hmcx_sumsq", "hmcx_sgd_run", "hmcx_hmc_run", "hmcx_axpy", "hmcx_mvn_eval",
-           "hmcx_clear_abort", "hmcx_philox_schedule")
+           "hmcx_clear_abort", "hmcx_philox_schedule", "hmcx_host_wait")
 
 _lib = None
 _lock = threading.Lock()
@@ -143,6 +143,7 @@ def load_library():
                                              c_void_p, c_void_p, c_void_p]
         lib.hmcx_sghmc_run.argtypes = [c_void_p, ctypes.POINTER(SamplerArgs)]
         lib.hmcx_clear_abort.argtypes = [c_void_p]
+        lib.hmcx_host_wait.argtypes = [c_void_p, c_void_p]
         lib.hmcx_philox_schedule.argtypes = [ctypes.c_uint64, ctypes.c_uint32, c_int, ctypes.c_uint32, c_int,
                                              c_double, c_dblp, c_dblp, c_i32p, c_dblp]
         lib.hmcx_sgld_run.argtypes = [c_void_p, ctypes.POINTER(SamplerArgs)]

@@ -423,6 +423,19 @@ int hmc_mvn_run(hmcx_ctx* ctx, const hmcx_hmc_mvn_args* s) {
   return HMCX_OK;
 }
 
+// An event behind the copies into an out_host block (one reusable, non-timing event per block).
+static int host_mark(hmcx_ctx* ctx, const void* out_host) {
+  hipEvent_t ev = nullptr;
+  for (auto& m : ctx->host_marks)
+    if (m.first == out_host) { ev = m.second; break; }
+  if (!ev) {
+    HMCX_HIP(ctx, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    ctx->host_marks.emplace_back(out_host, ev);
+  }
+  HMCX_HIP(ctx, hipEventRecord(ev, ctx->stream));
+  return HMCX_OK;
+}
+
 }  // namespace hmcx
 
 // =================================================================== C ABI
@@ -474,6 +487,7 @@ int hmcx_destroy(hmcx_ctx* ctx) {
   if (ctx->t_open) (void)hipEventDestroy(ctx->t_open);
   for (auto& pr : ctx->abort_pend) (void)hipEventDestroy(pr.first);
   for (auto e : ctx->ev_pool) (void)hipEventDestroy(e);
+  for (auto& m : ctx->host_marks) (void)hipEventDestroy(m.second);
   if (ctx->abort_host) (void)hipHostFree(ctx->abort_host);
   if (ctx->abort_dev) (void)hipFree(ctx->abort_dev);
   if (ctx->gx_arena) (void)hipFree(ctx->gx_arena);
@@ -823,14 +837,26 @@ int hmcx_sghmc_run(hmcx_ctx* ctx, const hmcx_sampler_args* a_in) {
     rc = run_traced(ctx, a, [ctx](const hmcx_sampler_args* s) {
       return s->dtype == HMCX_F64 ? sghmc_run_t<double>(ctx, s) : sghmc_run_t<float>(ctx, s);
     });
-  if (rc || !a->out_host || host_by_kernel) return rc;
-  const size_t nsc = (size_t)a->n_steps * a->C;
-  char* h = reinterpret_cast<char*>(a->out_host);
-  HMCX_HIP(ctx, hipMemcpyAsync(h, a->out_A, 36 * nsc, hipMemcpyDeviceToHost, ctx->stream));
-  if (a->out_abort)
-    HMCX_HIP(ctx, hipMemcpyAsync(h + 36 * nsc, a->out_abort, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
-  else
-    reinterpret_cast<int32_t*>(h + 36 * nsc)[0] = 0;
+  if (rc || !a->out_host) return rc;
+  if (!host_by_kernel) {
+    const size_t nsc = (size_t)a->n_steps * a->C;
+    char* h = reinterpret_cast<char*>(a->out_host);
+    HMCX_HIP(ctx, hipMemcpyAsync(h, a->out_A, 36 * nsc, hipMemcpyDeviceToHost, ctx->stream));
+    if (a->out_abort)
+      HMCX_HIP(ctx, hipMemcpyAsync(h + 36 * nsc, a->out_abort, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+    else
+      reinterpret_cast<int32_t*>(h + 36 * nsc)[0] = 0;
+  }
+  return host_mark(ctx, a->out_host);
+}
+
+int hmcx_host_wait(hmcx_ctx* ctx, const void* out_host) {
+  HMCX_GUARD_CTX(ctx);
+  for (auto& m : ctx->host_marks)
+    if (m.first == out_host) {
+      HMCX_HIP(ctx, hipEventSynchronize(m.second));
+      return HMCX_OK;
+    }
   return HMCX_OK;
 }
 

@@ -55,6 +55,7 @@ struct hmcx_ctx {
   int* abort_dev = nullptr;            // device word: raised by a timed-out persistent launch, sticky
                                        // until hmcx_clear_abort (later launches return at once)
   std::vector<std::pair<hipEvent_t, int>> abort_pend;
+  std::vector<std::pair<const void*, hipEvent_t>> host_marks;   // out_host block -> its latest copy's event
   unsigned abort_next = 0;
 };
 constexpr int ABORT_SLOTS = 64;

@@ -74,6 +74,24 @@ struct Q2Args {
   void* out_mom;                            // [P] momentum returned by the last step, or null
   unsigned long long* prof;                 // HMCX_PERSIST_PROF=1: per-segment s_memtime totals (workgroup 0)
   unsigned long long* trace;                // HMCX_P2_TRACE=1: [G][P2TR_IT][8] s_memrealtime stamps (step 0)
+  int* verdict;                             // this launch's abort verdict (hmcx_sampler_args::out_abort), or
+                                            // null: 0 stored by workgroup 0 on completion, 1 by every
+                                            // workgroup that leaves early (no device-to-device copy)
+  int ninl;                                 // > 0: the schedule of the call's ninl steps rides in inl (no
+                                            // host-to-device upload); 0: eps / u / row0 / n_iter above
+  struct { double eps, u; int64_t row0; int32_t n_iter, pad_; } inl[32];
+};
+constexpr int P2_NINL = 32;                 // calls of up to this many steps pass their schedule inline
+
+// Writes the launch's abort verdict when the workgroup leaves the kernel, whichever return it takes:
+// workgroup 0 reaching the end means every member passed the last accept round (0); any early return
+// is a timed-out hand-off or a sticky abort word (1).
+struct P2Verdict {
+  int* out;
+  bool first, done;
+  __device__ ~P2Verdict() {
+    if (out && (!done || first)) out[0] = done ? 0 : 1;
+  }
 };
 constexpr int P2TR_IT = 16;                 // traced leapfrog iterations
 
@@ -280,6 +298,8 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
   const int wl = (fo0 + od) * 16 + okc;               // index in Wf
   T pw = T(0), wv = T(0), w0 = T(0), zn = T(0);
 
+  P2Verdict verdict{threadIdx.x == 0 ? a.verdict : nullptr, bid == 0, false};
+  const bool inl = a.ninl > 0;
   // a launch behind a timed-out one (sticky abort word) leaves everything untouched
   if (__hip_atomic_load(a.abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
   if (tid == 0) ish[0] = 0;
@@ -362,11 +382,12 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
 
   for (int s = 0; s < a.n_steps; ++s) {
     const int tid = opaque((int)threadIdx.x), lane = tid & 63, wave = tid >> 6, lr = lane & 15;   // not hoisted (registers)
-    const double epsd = a.eps[s];
+    const double epsd = inl ? a.inl[s].eps : a.eps[s];
     const T eps = (T)epsd, ome = (T)(1.0 - epsd), nsc = (T)(2.0 * epsd);
-    const int n = a.n_iter[s];
-    const T* Xg = reinterpret_cast<const T*>(a.X) + (size_t)a.row0[s] * D;
-    const T* Yg = reinterpret_cast<const T*>(a.Y) + (size_t)a.row0[s] * K;
+    const int n = inl ? a.inl[s].n_iter : a.n_iter[s];
+    const int64_t rw = inl ? a.inl[s].row0 : a.row0[s];
+    const T* Xg = reinterpret_cast<const T*>(a.X) + (size_t)rw * D;
+    const T* Yg = reinterpret_cast<const T*>(a.Y) + (size_t)rw * K;
     prof.stamp(0);
     if (s == a.force_abort && bid == G - 1) {                             // test knob: a "timed-out" member
       if (tid == 0) __hip_atomic_store(a.abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -736,8 +757,9 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
     // next step's tile and labels while the partials travel: Xs and Yo have no reader left in this
     // step (the last B-gemm and softmax ended before a barrier)
     if (prefetch && s + 1 < a.n_steps) {
-      const T* Xn = reinterpret_cast<const T*>(a.X) + (size_t)a.row0[s + 1] * D;
-      const T* Yn = reinterpret_cast<const T*>(a.Y) + (size_t)a.row0[s + 1] * K;
+      const int64_t rn = inl ? a.inl[s + 1].row0 : a.row0[s + 1];
+      const T* Xn = reinterpret_cast<const T*>(a.X) + (size_t)rn * D;
+      const T* Yn = reinterpret_cast<const T*>(a.Y) + (size_t)rn * K;
       load_step_rows<T>(Xs, Yo, Xn, Yn, Br, BfP, BFP, nrow, nfeat, row0, feat0, D, K, Ro, nro, ro0);
     }
     const int sbase = a.oXS + (int)(uS & 1) * G * NXS;
@@ -763,13 +785,13 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
     int acc;
     if (n <= 0) {
       A = 1.0; Enew = Ecur; llq = L0;
-      acc = a.u[s] < A;
+      acc = (inl ? a.inl[s].u : a.u[s]) < A;
     } else {
       const double K1 = (0.0 + 0.5 * S1) + 0.5 * kb1;
       Enew = a.neg_inv_n * (ll_last + a.log_prior) + K1;
       const double x = exp(Ecur - Enew);
       A = (x < 1.0) ? x : 1.0;                                             // Python min(1, x)
-      acc = a.u[s] < A;
+      acc = (inl ? a.inl[s].u : a.u[s]) < A;
       llq = acc ? ll_last : L0;
     }
     if (!acc || n <= 0) {                                                  // keep q (sghmc.py:36-38)
@@ -802,6 +824,7 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
   //      out (then no workgroup can have passed the last accept round, which needs every member's
   //      write-through partial: an aborted launch leaves W/b as they were)
   if (__hip_atomic_load(a.abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+  verdict.done = true;
   if (own) reinterpret_cast<T*>(a.W)[e_own] = wv;
   if (bid == 0 && tid < K) reinterpret_cast<T*>(a.b)[tid] = bsh[tid];
 }
@@ -893,23 +916,35 @@ int sghmc_p2_t(hmcx_ctx* ctx, const hmcx_sampler_args* s, const PersistPlan2& pl
   for (size_t i = 0; i < n; ++i) rounds += 5u * (unsigned)(std::max(s->n_iter[i], 0) + 2);
   unsigned ep0 = 1;
   if ((rc = gx_epochs(ctx, rounds, &ep0))) return rc;
-  Workspace ws(ctx);
-  char* sched;
-  do {
-    ws.reset();
-    sched = ws.take<char>(sched_bytes);
-  } while (ws.retry());
-  if (ws.failed) return HMCX_ENOMEM;
-  begin_call(ctx);
-  char* dp[5];
-  if ((rc = upload_packed(ctx, sched, 5, hsrc, hbytes, dp))) return rc;
+  Q2Args a{};
+  // a short call's schedule (the driver's 20-step call) rides in the kernel arguments: no staging
+  // copy, no upload, no staging event ahead of the launch
+  char* dp[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+  if (!buf && n <= (size_t)P2_NINL) {
+    a.ninl = (int)n;
+    for (size_t i = 0; i < n; ++i) {
+      a.inl[i].eps = s->eps[i];
+      a.inl[i].u = s->u_accept[i];
+      a.inl[i].row0 = s->row0[i];
+      a.inl[i].n_iter = s->n_iter[i];
+    }
+  } else {
+    Workspace ws(ctx);
+    char* sched;
+    do {
+      ws.reset();
+      sched = ws.take<char>(sched_bytes);
+    } while (ws.retry());
+    if (ws.failed) return HMCX_ENOMEM;
+    begin_call(ctx);
+    if ((rc = upload_packed(ctx, sched, 5, hsrc, hbytes, dp))) return rc;
+  }
   double* d_eps = reinterpret_cast<double*>(dp[0]);
   double* d_u = reinterpret_cast<double*>(dp[1]);
   int64_t* d_row0 = reinterpret_cast<int64_t*>(dp[2]);
   int32_t* d_n = reinterpret_cast<int32_t*>(dp[3]);
   int64_t* d_noff = reinterpret_cast<int64_t*>(dp[4]);
 
-  Q2Args a{};
   a.B = s->B; a.D = s->D; a.K = K; a.P = s->D * K + K; a.n_steps = s->n_steps;
   a.Gr = pl.Gr; a.Gf = pl.Gf; a.Br = pl.Br; a.Bf = pl.Bf; a.BfP = pl.BfP; a.BFP = pl.BFP; a.Ro = pl.Ro; a.Fo = pl.Fo;
   a.alpha = s->alpha; a.neg_inv_n = -1.0 / (double)s->B; a.log_prior = s->log_prior;
@@ -956,6 +991,7 @@ int sghmc_p2_t(hmcx_ctx* ctx, const hmcx_sampler_args* s, const PersistPlan2& pl
   a.out_A = s->out_A; a.out_acc = s->out_accepted; a.out_ll = s->out_ll; a.out_E = s->out_E;
   a.out_trace = s->out_trace;
   a.out_mom = s->out_mom;
+  a.verdict = s->out_abort;
   static const bool prof_on = getenv("HMCX_PERSIST_PROF") && getenv("HMCX_PERSIST_PROF")[0] == '1';
   unsigned long long* dprof = nullptr;
   if (prof_on) {
@@ -989,14 +1025,17 @@ int sghmc_p2_t(hmcx_ctx* ctx, const hmcx_sampler_args* s, const PersistPlan2& pl
   if ((rc = timing_begin(ctx, ctx->stream))) return rc;
   HMCX_HIP(ctx, hipLaunchKernel(kfn, dim3(G), dim3(QTH), kargs, (unsigned)pl.lds, ctx->stream));
   if ((rc = timing_end(ctx, ctx->stream))) return rc;
-  if (s->out_host) {                             // outputs and this launch's verdict, one copy each
+  if (s->out_host) {                             // outputs and this launch's verdict
     char* h = reinterpret_cast<char*>(s->out_host);
-    HMCX_HIP(ctx, hipMemcpyAsync(h, s->out_A, 36 * n, hipMemcpyDeviceToHost, ctx->stream));
-    HMCX_HIP(ctx, hipMemcpyAsync(h + 36 * n, ctx->abort_dev, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    const bool packed = s->out_abort == reinterpret_cast<int32_t*>(reinterpret_cast<char*>(s->out_A) + 36 * n);
+    HMCX_HIP(ctx, hipMemcpyAsync(h, s->out_A, 36 * n + (packed ? sizeof(int) : 0), hipMemcpyDeviceToHost,
+                                 ctx->stream));
+    if (!packed)
+      HMCX_HIP(ctx, hipMemcpyAsync(h + 36 * n, s->out_abort ? (const void*)s->out_abort : ctx->abort_dev,
+                                   sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
     if (!dprof && !dtrace) return HMCX_OK;
   }
-  if (s->out_abort) {                            // the caller reads this launch's verdict itself
-    HMCX_HIP(ctx, hipMemcpyAsync(s->out_abort, ctx->abort_dev, sizeof(int), hipMemcpyDeviceToDevice, ctx->stream));
+  if (s->out_abort) {                            // the kernel stored this launch's verdict there itself
     if (!dprof && !dtrace) return HMCX_OK;
   } else if (!dprof && !dtrace) {                // no per-call sync: checked once the launch is done
     return abort_defer(ctx, a.abort_flag, ctx->stream);

@@ -102,21 +102,22 @@ class sghmc(sgmcmc):
     def _io_slot(self, nbytes, dev):
         """A device output buffer and its pinned host mirror, reused round-robin across calls (all
         slots are allocated by the first call, so later calls allocate nothing)."""
-        ring = self.__dict__.setdefault('_io_ring', [])
-        if not ring:
-            ring.extend({'dev': None, 'host': None, 'ev': torch.cuda.Event(), 'busy': None}
-                        for _ in range(self._IO_SLOTS))
+        ring = self.__dict__.get('_io_ring')
+        if ring is None:
+            self._io_ring = ring = [{'dev': None, 'host': None, 'busy': None, 'cap': 0}
+                                    for _ in range(self._IO_SLOTS)]
         i = self.__dict__.get('_io_next', 0)
         self._io_next = i + 1
         slot = ring[i % self._IO_SLOTS]
         if slot['busy'] is not None:    # an uncollected call keeps its buffers; the slot gets new ones
-            slot.update(dev=None, host=None, ev=torch.cuda.Event(), busy=None)
-        if slot['dev'] is None or slot['dev'].numel() < nbytes:
+            slot.update(dev=None, host=None, busy=None, cap=0)
+        if slot['cap'] < nbytes:
             cap = max(1 << 16, 1 << (int(nbytes) - 1).bit_length())
             for sl in ring:                          # busy slots grow when their turn comes
-                if sl['busy'] is None and (sl['dev'] is None or sl['dev'].numel() < cap):
+                if sl['busy'] is None and sl['cap'] < cap:
                     sl['dev'] = torch.empty(cap, dtype=torch.uint8, device=dev)
                     sl['host'] = torch.empty(cap, dtype=torch.uint8, pin_memory=True)
+                    sl['base'], sl['hptr'], sl['cap'] = sl['dev'].data_ptr(), sl['host'].data_ptr(), cap
         return slot
 
     def _call_template(self, Xd, Yd, W, b, batch_size, D, K, C):
@@ -141,7 +142,7 @@ class sghmc(sgmcmc):
     def _enqueue(self, state, data, rows, eps, rng, batch_size):
         """Prepare the schedule of len(rows) steps and enqueue them (one hmcx_sghmc_run call) without
         waiting: the call copies its outputs into a pinned host buffer behind its kernels (out_host,
-        stream-ordered) and a HIP event marks their arrival.  _collect waits on that event only, so a caller may
+        stream-ordered) and records an event behind them; _collect waits on that event only (hmcx_host_wait), so a caller may
         enqueue the next call before collecting this one — the state stays on the device, stream
         order keeps the calls in sequence, and the host work of call k+1 overlaps the device work of
         call k."""
@@ -158,8 +159,7 @@ class sghmc(sgmcmc):
         nsc = n_steps * C
         philox = self.noise == 'philox'
         if philox:                      # the C call draws the Philox schedule itself (out_L: the L's)
-            L_out = np.empty(nsc)
-            n_iter = u = noise = noise_off = None
+            L_out = n_iter = u = noise = noise_off = None
         else:
             n_iter, u, noise, noise_off = self._schedule(n_steps, eps, rng, P)
             n_iter, u, noise_off = (np.ascontiguousarray(x.reshape(-1)) for x in (n_iter, u, noise_off))
@@ -169,30 +169,43 @@ class sghmc(sgmcmc):
         noise_d = torch.from_numpy(noise).to(dev) if noise is not None else None
         nbytes = 32 * nsc + 4 * nsc + 4                  # A, ll, E (2) f64 | accepted i32 | abort i32
         slot = self._io_slot(nbytes, dev)
-        base = slot['dev'].data_ptr()
+        base = slot['base']
         if mark is not None:
             mark.append(('io slot', time.perf_counter()))
         fast = philox and not self.record_steps and not self.__dict__.get('_want_mom')
         if fast:
-            # the slot keeps its argument struct and host schedule arrays between calls of the same
-            # shape: a call only refills the step rows / sizes and the step id
-            key = (Xd.data_ptr(), Yd.data_ptr(), W.data_ptr(), b.data_ptr(), batch_size, C, n_steps, base,
-                   slot['host'].data_ptr(), self.path_length, self.seed, self.chain)
+            # every slot keeps an argument struct and host schedule arrays (sized for up to `cap` steps)
+            # between calls: a call only refills the step rows / sizes, the step count and the output
+            # offsets.  A miss rebuilds the caches of ALL slots at once, so the first call on each slot
+            # (and a call with a new step count) costs no more than the others.
+            tkey = (Xd.data_ptr(), Yd.data_ptr(), W.data_ptr(), b.data_ptr(), batch_size, C, self.path_length,
+                    self.seed, self.chain)
             ac = slot.get('acache')
-            if ac is None or ac[0] != key:
-                a = nat.SamplerArgs.from_buffer_copy(self._call_template(Xd, Yd, W, b, batch_size, D, K, C))
-                r0b, epb, Lb = np.empty(n_steps, np.int64), np.empty(n_steps), np.empty(nsc)
-                a.n_steps = n_steps
-                a.row0, a.eps, a.out_L = nat.addr(r0b), nat.addr(epb), nat.addr(Lb)
-                a.out_A, a.out_ll, a.out_E = base, base + 8 * nsc, base + 16 * nsc
-                a.out_accepted = base + 32 * nsc
-                a.out_host = slot['host'].data_ptr()
-                slot['acache'] = ac = (key, a, r0b, epb, Lb)
-            _, a, row0, eps_a, L_out = ac
+            if ac is None or ac[0] != tkey or ac[1] is not slot['dev'] or n_steps > ac[6]:
+                cap = max(128, 1 << (n_steps - 1).bit_length())
+                tpl = self._call_template(Xd, Yd, W, b, batch_size, D, K, C)
+                for sl in self._io_ring:
+                    if sl['dev'] is None or (sl is not slot and sl['busy'] is not None):
+                        continue
+                    a = nat.SamplerArgs.from_buffer_copy(tpl)
+                    r0b, epb, Lb = np.empty(cap, np.int64), np.empty(cap), np.empty(cap * C)
+                    a.row0, a.eps, a.out_L = nat.addr(r0b), nat.addr(epb), nat.addr(Lb)
+                    a.out_host = sl['hptr']
+                    sl['acache'] = (tkey, sl['dev'], a, r0b, epb, Lb, cap, [0])
+                ac = slot['acache']
+            _, _, a, r0b, epb, Lb, _, last_n = ac
+            row0, eps_a, L_out = r0b[:n_steps], epb[:n_steps], Lb[:nsc]
             row0[:] = rows
             eps_a[:] = eps
+            if last_n[0] != n_steps:
+                a.n_steps = n_steps
+                a.out_A, a.out_ll, a.out_E = base, base + 8 * nsc, base + 16 * nsc
+                a.out_accepted = base + 32 * nsc
+                last_n[0] = n_steps
             a.out_abort = base + 36 * nsc
         else:
+            if philox:                  # the C call draws the Philox schedule itself (out_L: the L's)
+                L_out = np.empty(nsc)
             row0 = np.asarray(rows, dtype=np.int64)
             eps_a = np.asarray(eps, dtype=np.float64)
             a = nat.SamplerArgs.from_buffer_copy(self._call_template(Xd, Yd, W, b, batch_size, D, K, C))
@@ -208,7 +221,7 @@ class sghmc(sgmcmc):
                 a.noise_off = nat.addr(noise_off)
             a.out_A, a.out_ll, a.out_E = base, base + 8 * nsc, base + 16 * nsc
             a.out_accepted, a.out_abort = base + 32 * nsc, base + 36 * nsc
-            a.out_host = slot['host'].data_ptr()      # outputs + abort word land here (include/hmcx.h)
+            a.out_host = slot['hptr']                 # outputs + abort word land here (include/hmcx.h)
         if mark is not None:
             mark.append(('template', time.perf_counter()))
         a.step_base = self.global_step & 0xFFFFFFFF
@@ -222,23 +235,24 @@ class sghmc(sgmcmc):
             a.out_mom = ptr(out_mom)
         if mark is not None:
             mark.append(('args', time.perf_counter()))
-        ctx = nat.context(dev)
+        cc = self.__dict__.get('_ctx_of')
+        if cc is None or cc[0] != dev:
+            self._ctx_of = cc = (dev, nat.context(dev))
+        ctx = cc[1]
+        ctx.bind_stream()                              # follow torch's current stream
         if mark is not None:
             mark.append(('context', time.perf_counter()))
-        ctx.check(ctx.lib.hmcx_sghmc_run(ctx.h, a), "hmcx_sghmc_run")
+        ctx.check(ctx.lib.hmcx_sghmc_run(ctx.h, a), "hmcx_sghmc_run")     # records the out_host event
         if mark is not None:
             mark.append(('c call', time.perf_counter()))
-        slot['ev'].record()
-        if mark is not None:
-            mark.append(('event', time.perf_counter()))
         if philox and self.trace is not None:                 # while the launch runs
             if C == 1:
-                self.trace.extend({'L': float(l), 'eps': float(e)} for l, e in zip(L_out, eps))
+                self.trace += [{'L': l, 'eps': float(e)} for l, e in zip(L_out.tolist(), eps)]
             else:
                 Ls = L_out.reshape(n_steps, C)
                 self.trace.extend({'L': Ls[i].copy(), 'eps': float(eps[i])} for i in range(n_steps))
         self.global_step += n_steps
-        h = dict(slot=slot, dev=slot['dev'], host=slot['host'], ev=slot['ev'], nbytes=nbytes, n_steps=n_steps,
+        h = dict(slot=slot, dev=slot['dev'], host=slot['host'], nbytes=nbytes, n_steps=n_steps,
                  C=C, t0=t0, ctx=ctx, out_steps=out_steps, out_mom=out_mom,
                  args=a, keep=(row0, eps_a, n_iter, u, noise_off, noise_d, L_out if philox else None))
         slot['busy'] = h
@@ -250,7 +264,7 @@ class sghmc(sgmcmc):
         whose persistent launch timed out is re-run first (_recover)."""
         n_steps, C = h['n_steps'], h['C']
         slot = h['slot']
-        h['ev'].synchronize()
+        h['ctx'].check(h['ctx'].lib.hmcx_host_wait(h['ctx'].h, h['host'].data_ptr()), "hmcx_host_wait")
         nsc = n_steps * C
         raw = h['host'][:h['nbytes']].numpy()
         if raw[36 * nsc:36 * nsc + 4].view(np.int32)[0] and not h.get('recovered'):

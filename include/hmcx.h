@@ -188,12 +188,18 @@ typedef struct hmcx_sampler_args {
                            /* [.. f64 ll][2*n_steps*C f64 E][n_steps*C i32 accepted][i32   */
                            /* abort].  out_A/out_ll/out_E/out_accepted must then be that    */
                            /* layout in one device block; the call copies it behind its     */
-                           /* kernels (one copy of the block, one of the abort word).       */
+                           /* kernels (one copy when out_abort is the i32 right after that  */
+                           /* block, else two) and records an event: hmcx_host_wait.        */
 } hmcx_sampler_args;
 
 /* Replaces hamiltonian/inference/{cpu,gpu}/sghmc.py:19-39 (step, with the A1 completion:
  * momentum ~ N(0,1), MH accept min(1, exp(E_cur - E_new)) from cpu/hmc.py:67-87). */
 int hmcx_sghmc_run(hmcx_ctx* ctx, const hmcx_sampler_args* a);
+
+/* Blocks until the outputs of the latest hmcx_sghmc_run call that named this out_host block have
+ * landed in it (an event recorded behind that call's copies; no stream-wide synchronisation, so
+ * calls enqueued after it keep running).  A block no call has named returns at once. */
+int hmcx_host_wait(hmcx_ctx* ctx, const void* out_host);
 
 /* Persistent-kernel hand-off timeouts (single-chain SGHMC).  A launch whose workgroups time out
  * waiting for each other (they were not co-resident, or not placed on the XCDs the kernel assumes)
