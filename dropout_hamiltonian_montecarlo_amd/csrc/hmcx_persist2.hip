@@ -314,7 +314,9 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
   __syncthreads();
   if (own) wv = Wf[wl];
 
-  P2Prof prof{(!SP && bid == 0 && tid == 0) ? a.prof : nullptr, profacc, 0ull, 0};   // SPEC: compiled out
+  // segment profiler: compiled out of the config-2 instantiation (SPEC = 1); SPEC = 3 is that
+  // instantiation with it (HMCX_PERSIST_PROF=1 at the config-2 shape)
+  P2Prof prof{((!SP || SPEC == 3) && bid == 0 && tid == 0) ? a.prof : nullptr, profacc, 0ull, 0};
   // round trace: slot 2·round = payload published, 2·round + 1 = consumed (rounds A, D, B, W)
   unsigned long long* trb = (!SP && a.trace) ? a.trace + (size_t)bid * P2TR_IT * 8 : nullptr;
   auto tstamp = [&](int s_, int it_, int slot) {
@@ -398,13 +400,16 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
     //      previous accept round travelled), momentum (hmc.py:82-87), step-start copies
     if (s == 0 || !prefetch) load_step_rows<T>(Xs, Yo, Xg, Yg, Br, BfP, BFP, nrow, nfeat, row0, feat0, D, K, Ro, nro, ro0);
     for (int e = tid; e < BfP * 16; e += QTH) Wf0[e] = Wf[e];
+    // momentum (hmc.py:82-87): the owned elements' by their threads, the bias's by the last 16 threads
+    // (not the owners of elements 0..15: one Box–Muller latency per thread, not two)
     pw = own ? noise1<T>(a, s, 0u, (uint32_t)e_own) : T(0);
     const T pw0 = pw;
     w0 = wv;
-    if (tid < 16) {
-      pbsh[tid] = tid < K ? noise1<T>(a, s, 0u, (uint32_t)(D * K + tid)) : T(0);
-      pb0sh[tid] = pbsh[tid];
-      b0sh[tid] = bsh[tid];
+    if (tid >= QTH - 16) {
+      const int k = tid - (QTH - 16);
+      pbsh[k] = k < K ? noise1<T>(a, s, 0u, (uint32_t)(D * K + k)) : T(0);
+      pb0sh[k] = pbsh[k];
+      b0sh[k] = bsh[k];
     }
     const double kin0 = wsum((double)pw * (double)pw, dsh);
     double kb0 = 0.0;
@@ -414,6 +419,27 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
     double ll0 = 0.0, ll_last = 0.0;
     prof.stamp(11);
     roundA();
+    if (n > 0) {
+      // iteration 0's drift of the whole F_f slice by p0 (every member computes it identically;
+      // sghmc.py:32), by the waves that do not poll this A-RS round, while the partials travel —
+      // after a barrier: every wave's A-gemm has read Wf
+      __syncthreads();
+      const int nzp = (spread & 1) ? 0 : ((nro * KC + 63) / 64) * 64;   // the polling threads
+      const int ge0 = (feat0 * K) >> 2, ge1 = ((feat0 + nfeat) * K + 3) >> 2;
+      for (int g = ge0 + tid - nzp; tid >= nzp && g < ge1; g += QTH - nzp) {
+        T z4[4];
+        philox4_if(a, s, 0u, (uint32_t)g, z4);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int e = 4 * g + q;
+          if (e < feat0 * K || e >= (feat0 + nfeat) * K) continue;
+          const int i = e / K - feat0, k = e - (e / K) * K;
+          const T p0 = noise_at<T>(a, s, 0u, (uint32_t)e, z4);
+          Wf[i * 16 + k] = Wf[i * 16 + k] + eps * p0;
+          if (bar) pWs[i * 16 + k] = p0;
+        }
+      }
+    }
     if (!consumeA()) return;
     {
       const int k = lane & 15, grp = tid >> 4;
@@ -442,25 +468,7 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
     for (int it = 0; it < n; ++it) {
       const int tid = opaque((int)threadIdx.x), lane = tid & 63, wave = tid >> 6, lr = lane & 15;   // not hoisted (registers)
       const bool last = it == n - 1;
-      if (it == 0) {
-        // drift of the whole F_f slice by p0 (every member computes it identically; sghmc.py:32)
-        const int ge0 = (feat0 * K) >> 2, ge1 = ((feat0 + nfeat) * K + 3) >> 2;
-        for (int g = ge0 + tid; g < ge1; g += QTH) {
-          T z4[4];
-          philox4_if(a, s, 0u, (uint32_t)g, z4);
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int e = 4 * g + q;
-            if (e < feat0 * K || e >= (feat0 + nfeat) * K) continue;
-            const int i = e / K - feat0, k = e - (e / K) * K;
-            const T p0 = noise_at<T>(a, s, 0u, (uint32_t)e, z4);
-            Wf[i * 16 + k] = Wf[i * 16 + k] + eps * p0;
-            if (bar) pWs[i * 16 + k] = p0;
-          }
-        }
-        if (own) wv = wv + eps * pw;
-        __syncthreads();
-      }
+      if (it == 0 && own) wv = wv + eps * pw;          // the slice drifted during the it = -1 round
       if (tid < 16) bpsh[tid] = bsh[tid] + eps * pbsh[tid];                // b' (bias sub-step)
 
       // ===== A-RS: partial logits → owners of the row slices
@@ -756,6 +764,8 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
     }
     // next step's tile and labels while the partials travel: Xs and Yo have no reader left in this
     // step (the last B-gemm and softmax ended before a barrier)
+    // (measured: loading it with only the half of the workgroup that does not poll the accept round
+    // is slower — 9.68 vs 9.44 µs per leapfrog: two load batches instead of one)
     if (prefetch && s + 1 < a.n_steps) {
       const int64_t rn = inl ? a.inl[s + 1].row0 : a.row0[s + 1];
       const T* Xn = reinterpret_cast<const T*>(a.X) + (size_t)rn * D;
@@ -1011,9 +1021,9 @@ int sghmc_p2_t(hmcx_ctx* ctx, const hmcx_sampler_args* s, const PersistPlan2& pl
   const bool spec = sizeof(T) == 8 && KC == 10 && s->B == 500 && s->D == 784 && K == 10 && pl.Gr == 8 && pl.Gf == 16 &&
                     pl.Br == 64 && pl.Bf == 49 && pl.BfP == 64 && pl.BFP == 66 && pl.Ro == 4 && pl.Fo == 7 &&
                     a.spread == 2 && a.pad == 1 && a.xmap == 0 && a.fl2 == 1 && a.al2 == 0 && a.prefetch == 1 &&
-                    a.acc1 == 1 && a.zoff == 1 && a.bar == 1 && !a.prof && !a.trace;
+                    a.acc1 == 1 && a.zoff == 1 && a.bar == 1 && !a.trace;
   static const bool no_spec = getenv("HMCX_P2_SPEC") && getenv("HMCX_P2_SPEC")[0] == '0';
-  const void* kfn = (spec && !no_spec) ? (const void*)k_sghmc_p2<T, 10, 1>
+  const void* kfn = (spec && !no_spec) ? (a.prof ? (const void*)k_sghmc_p2<T, 10, 3> : (const void*)k_sghmc_p2<T, 10, 1>)
                     : KC == 10 ? (const void*)k_sghmc_p2<T, 10> : (const void*)k_sghmc_p2<T, 16>;
   void* kargs[] = {&a};
   // co-residency of all G workgroups is checked here (occupancy query × CUs, cached per kernel); a
