@@ -465,16 +465,24 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
     }
 
     double kin1 = 0.0;
+    T zb_prev = T(0);                                   // bias friction noise of the previous iteration
     for (int it = 0; it < n; ++it) {
       const int tid = opaque((int)threadIdx.x), lane = tid & 63, wave = tid >> 6, lr = lane & 15;   // not hoisted (registers)
       const bool last = it == n - 1;
       if (it == 0 && own) wv = wv + eps * pw;          // the slice drifted during the it = -1 round
-      if (tid < 16) bpsh[tid] = bsh[tid] + eps * pbsh[tid];                // b' (bias sub-step)
 
       // ===== A-RS: partial logits → owners of the row slices
       prof.stamp(1);
       roundA();
       tstamp(s, it, 0);
+      // B-AR: the previous iteration's bias sub-step runs here, after this workgroup's A partials went
+      // out (it only has to be done before the softmax), then b' of this iteration
+      if (bar && it > 0 && tid < K) {
+        const T gr = -((T)hdr[tid] - alpha * bpsh[tid]);
+        pbsh[tid] = (ome * pbsh[tid] + eps * gr) + nsc * zb_prev;
+        bsh[tid] = bpsh[tid];
+      }
+      if (tid < 16) bpsh[tid] = bsh[tid] + eps * pbsh[tid];                // b' (bias sub-step)
       prof.stamp(2);
       // friction noise of this iteration (sghmc.py:31), generated while the partials travel
       T zb = T(0);
@@ -661,16 +669,17 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
           if (!all_ok(ok, ish)) return;
           tstamp(s, it, 5);
           prof.stamp(8);
-          if (tid < K) {                                                      // bias sub-step, replicated
-            const T gr = -((T)hdr[tid] - alpha * bpsh[tid]);
-            pbsh[tid] = (ome * pbsh[tid] + eps * gr) + nsc * zb;
-            bsh[tid] = bpsh[tid];
-          }
           if (last) {
+            if (tid < K) {                                                    // bias sub-step, replicated
+              const T gr = -((T)hdr[tid] - alpha * bpsh[tid]);
+              pbsh[tid] = (ome * pbsh[tid] + eps * gr) + nsc * zb;
+              bsh[tid] = bpsh[tid];
+            }
             ll_last = hdr[KC];                                                // ll(q_new) on this batch
             kin1 = kl;
             break;
           }
+          zb_prev = zb;                               // its bias sub-step: after the next A publish
           continue;
         }
         // threads [0, nfo·KC): owned gradient element; threads [nfo·KC, nfo·KC + HA): header
