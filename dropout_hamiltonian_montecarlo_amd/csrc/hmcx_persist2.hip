@@ -215,7 +215,12 @@ __device__ inline typename mfma16<T>::acc_t mfma_tile(const T* a, int as_i, int 
       c1 = M::fma(av[u + 1], bv[u + 1], c1);
     }
   }
-  for (; kk < nk; ++kk) c0 = M::fma(pa[kk * 4 * as_k], pb[kk * 4 * bs_k], c0);
+  // tail: the two accumulators still alternate (two dependent MFMA chains, not one)
+  for (; kk + 2 <= nk; kk += 2) {
+    c0 = M::fma(pa[kk * 4 * as_k], pb[kk * 4 * bs_k], c0);
+    c1 = M::fma(pa[(kk + 1) * 4 * as_k], pb[(kk + 1) * 4 * bs_k], c1);
+  }
+  if (kk < nk) c0 = M::fma(pa[kk * 4 * as_k], pb[kk * 4 * bs_k], c0);
   return c0 + c1;
 }
 
@@ -331,7 +336,9 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
     const int tid = opaque((int)threadIdx.x), lane = tid & 63, wave = tid >> 6, lr = lane & 15;   // not hoisted (registers)
     ++ep;
     const int reg = a.oXA + (((int)(uA & 1) * Gr + r) * Gf + f) * Br * KC;
-    const int nkp = WPA == 1 ? (nfeat + 3) / 4 : (BfP / 4) / WPA;   // zero-padded tail skipped
+    // zero-padded tail skipped; config 2: 49 features in every feature team → 13 k-steps (a constant:
+    // the k loop unrolls completely)
+    const int nkp = SP ? 13 : WPA == 1 ? (nfeat + 3) / 4 : (BfP / 4) / WPA;
     for (int item = wave; item < MTA * WPA; item += QNW) {
       const int mt = item % MTA, part = item / MTA;
       const typename M::acc_t c = mfma_tile<T>(Xs + mt * 16 * BFP + part * nkp * 4, BFP, 1,
