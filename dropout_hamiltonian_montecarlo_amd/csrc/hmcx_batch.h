@@ -50,6 +50,21 @@ __device__ inline bool xcd_tile(int nX, int nCT, int& bx, int& by) {
   return by < nCT;
 }
 inline unsigned xcd_grid(int nX, int nCT) { return 8u * (unsigned)nX * (unsigned)((nCT + 7) / 8); }
+// Same grid and XCD grouping, with every tile of the last x tile (a partial feature tile, cheap once
+// its empty m-tiles skip the MFMA loop) dispatched after all full tiles: the full tiles fill whole
+// rounds of the chip's workgroup slots and the partial ones run as a short final round, instead of
+// being spread through the rounds and leaving the last round a quarter full of full-cost tiles.
+__device__ inline bool xcd_tile_tail_last(int nX, int nCT, int& bx, int& by) {
+  const int L = blockIdx.x, x = L & 7, s = L >> 3, ng = (nCT + 7) / 8, nXm = nX - 1;
+  if (s < nXm * ng) {
+    by = x + 8 * (s / nXm);
+    bx = s - (s / nXm) * nXm;
+  } else {
+    by = x + 8 * (s - nXm * ng);
+    bx = nXm;
+  }
+  return by < nCT;
+}
 
 template <typename T> struct BFwdArgs {
   const T* X; const T* Y;           // minibatch rows (offset to the step's first row)
@@ -73,6 +88,7 @@ template <typename T> struct BGradArgs {
   double* kin_part;                 // [nDB][C]
   int nDB_all;                      // k_bgrad2: kin_part rows past its grid are zero-filled up to here
   int nX, nCT;                      // feature tiles × chain tiles (XCD-grouped 1-D grid, xcd_tile)
+  int tail_last;                    // k_bgradw: partial last feature tile dispatched last (xcd_tile_tail_last)
   double* kinb;                     // [C]
   int noise_mode; const double* noise; const int64_t* noff;
   uint64_t seed; uint32_t chain0, step, slot;
@@ -553,7 +569,7 @@ __global__ __launch_bounds__(64 * NW) void k_bgradw(BGradArgs<T> a) {
   int* chs = reinterpret_cast<int*>(pbs + BNT);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lg = lane >> 4;
   int bx, by;
-  if (!xcd_tile(a.nX, a.nCT, bx, by)) return;
+  if (!(a.tail_last ? xcd_tile_tail_last(a.nX, a.nCT, bx, by) : xcd_tile(a.nX, a.nCT, bx, by))) return;
   const int d0 = bx * G::FT, rank0 = by * BCT;
   const int nfeat = min(G::FT, a.D - d0);
   const int D = a.D, N = a.N, B = a.B;
@@ -601,6 +617,9 @@ __global__ __launch_bounds__(64 * NW) void k_bgradw(BGradArgs<T> a) {
   };
 
   const int mt = wave % G::NMT, nh = wave / G::NMT;     // wave: features mt·32 .. +32, columns nh·80 .. +80
+  // m-tiles of this wave holding features (wave-uniform): a partial last tile (D = 784: 16 of 64
+  // features) skips the MFMAs of its empty m-tiles; their accumulators stay zero and are never stored
+  const int nmw = min(2, max(0, (nfeat - mt * 32 + 15) / 16));
   typename M::acc_t acc[2][5];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -613,17 +632,29 @@ __global__ __launch_bounds__(64 * NW) void k_bgradw(BGradArgs<T> a) {
     __syncthreads();
     if (r0 + BCH < B) fetch(r0 + BCH);
     const int nks = min(BCH, B - r0 + 3) / 4;
+    if (nmw == 2) {
 #pragma unroll 2
-    for (int ks = 0; ks < nks; ++ks) {
-      T av[2], bv[5];
+      for (int ks = 0; ks < nks; ++ks) {
+        T av[2], bv[5];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) av[i] = Xs[(ks * 4 + lg) * G::XP + mt * 32 + i * 16 + lr];
+        for (int i = 0; i < 2; ++i) av[i] = Xs[(ks * 4 + lg) * G::XP + mt * 32 + i * 16 + lr];
 #pragma unroll
-      for (int j = 0; j < 5; ++j) bv[j] = Ds[(ks * 4 + lg) * BWP + (nh * 5 + j) * 16 + lr];
+        for (int j = 0; j < 5; ++j) bv[j] = Ds[(ks * 4 + lg) * BWP + (nh * 5 + j) * 16 + lr];
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 5; ++j) acc[i][j] = M::fma(av[i], bv[j], acc[i][j]);
+          for (int j = 0; j < 5; ++j) acc[i][j] = M::fma(av[i], bv[j], acc[i][j]);
+      }
+    } else if (nmw == 1) {
+#pragma unroll 2
+      for (int ks = 0; ks < nks; ++ks) {
+        T bv[5];
+        const T av = Xs[(ks * 4 + lg) * G::XP + mt * 32 + lr];
+#pragma unroll
+        for (int j = 0; j < 5; ++j) bv[j] = Ds[(ks * 4 + lg) * BWP + (nh * 5 + j) * 16 + lr];
+#pragma unroll
+        for (int j = 0; j < 5; ++j) acc[0][j] = M::fma(av, bv[j], acc[0][j]);
+      }
     }
   }
   __syncthreads();

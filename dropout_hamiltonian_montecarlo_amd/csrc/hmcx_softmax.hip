@@ -1376,6 +1376,8 @@ int sghmc_batch_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
       g.nCT = ctiles;
       if (nDB2 * ctiles >= 2 * ctx->num_cus) {
         g.nX = nDB2;
+        static const bool tail_off = getenv("HMCX_BGW_TAIL") && getenv("HMCX_BGW_TAIL")[0] == '0';
+        g.tail_last = !tail_off && nDB2 > 1 && D % BRW2 != 0 && D % BRW2 <= BRW2 / 2;
         hipLaunchKernelGGL((k_bgradw<T, 4>), dim3(xcd_grid(g.nX, g.nCT)), dim3(256), lds4, st, g);
       } else {
         g.nX = nDB;

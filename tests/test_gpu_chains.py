@@ -44,8 +44,10 @@ def _run_chains(c, chains, dtype=torch.float64, noise="numpy", seed=0, chain=0, 
 
 
 @pytest.mark.parametrize("name,chains", [("sghmc_small", 16), ("sghmc_small", 4), ("sghmc_mnist", 16), ("sghmc_small", 512),
-                                         ("sghmc_hot", 32), ("sgld_small", 16)])
+                                         ("sghmc_mnist", 1024), ("sghmc_hot", 32), ("sgld_small", 16)])
 def test_replica_chains_match_oracle(name, chains):
+    # ("sghmc_mnist", 1024): D = 784 with 64 chain tiles runs the wide gradient kernel k_bgradw, whose
+    # last feature tile is partial (16 of 64 features: empty m-tiles skipped, dispatched last)
     c = gi.TRAJ_CONFIGS[name]
     post_r, logp_r, tr_r, _ = _run_oracle(c)
     post_g, logp_g, tr_g = _run_chains(c, chains)
