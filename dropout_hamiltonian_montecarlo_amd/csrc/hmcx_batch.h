@@ -486,38 +486,58 @@ __global__ __launch_bounds__(256) void k_bgrad(BGradArgs<T> a) {
   double* kp = reinterpret_cast<double*>(Xs);        // [mt·4 + lg][160] Σ p² over the lane's rows
   T* __restrict__ Wg = a.W;                          // all 20 W / pW loads first (no aliasing), then
   T* __restrict__ Pg = a.pW;                         // the updates: one HBM round trip per thread
+  // every load unconditional (clamped address, value selected afterwards) and the noise source chosen
+  // per launch outside the element loops (see k_bgradw)
+  const bool buf = a.noise_mode == HMCX_NOISE_BUFFER;
   T wv[5][4], pv[5][4];
-#pragma unroll
-  for (int j = 0; j < 5; ++j)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int fi = mt * 16 + M::row(lane, q), col = (nh * 5 + j) * 16 + lr;
-      const int cs = col / BKC, k = col - cs * BKC, ch = chs[cs];
-      const bool ok = ch >= 0 && fi < nfeat;
-      const size_t idx = ok ? ((size_t)ch * D + (d0 + fi)) * BKC + k : 0;
-      wv[j][q] = ok ? Wg[idx] : T(0);
-      pv[j][q] = ok ? Pg[idx] : T(0);
-    }
+  int lastm = 0;
 #pragma unroll
   for (int j = 0; j < 5; ++j) {
     const int col = (nh * 5 + j) * 16 + lr;
+    const int cs = col / BKC, k = col - cs * BKC, ch = chs[cs];
+    const int n = a.n_iter[ch >= 0 ? ch : 0];
+    lastm |= (ch >= 0 && a.iter >= n - 1) << j;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int fi = mt * 16 + M::row(lane, q);
+      const bool ok = ch >= 0 && fi < nfeat;
+      const size_t idx = ok ? ((size_t)ch * D + (d0 + fi)) * BKC + k : 0;
+      const T w = Wg[idx], pw = Pg[idx];
+      wv[j][q] = ok ? w : T(0);
+      pv[j][q] = ok ? pw : T(0);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    const int col = (nh * 5 + j) * 16 + lr;
+    const int cs = col / BKC, k = col - cs * BKC, ch = chs[cs];
+    const bool last = (lastm >> j) & 1;
+    T zv[4];
+    if (buf) {
+      const int64_t nb = (ch >= 0 ? a.noff[ch] : 0) + (int64_t)a.slot * a.P;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int fi = mt * 16 + M::row(lane, q);
+        const bool ok = ch >= 0 && fi < nfeat;
+        const double z = a.noise[ok ? nb + (uint32_t)((d0 + fi) * BKC + k) : 0];
+        zv[q] = ok ? (T)z : T(0);
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) zv[q] = Nz[(mt * 16 + M::row(lane, q)) * BNP + col];
+    }
     double p2s = 0.0;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int fi = mt * 16 + M::row(lane, q);
-      const int cs = col / BKC, k = col - cs * BKC, ch = chs[cs];
       if (ch >= 0 && fi < nfeat) {
         const int d = d0 + fi;
         const size_t idx = ((size_t)ch * D + d) * BKC + k;
         const T w = wv[j][q];
         const T gr = -(acc[j][q] - a.alpha * w);
-        const T z = a.noise_mode == HMCX_NOISE_BUFFER
-                        ? (T)a.noise[a.noff[ch] + (int64_t)a.slot * a.P + (uint32_t)(d * BKC + k)]
-                        : Nz[fi * BNP + col];
-        const T p = (a.one_minus_eps * pv[j][q] + a.eps * gr) + a.noise_scale * z;
+        const T p = (a.one_minus_eps * pv[j][q] + a.eps * gr) + a.noise_scale * zv[q];
         Pg[idx] = p;
-        const int n = a.n_iter[ch];
-        if (a.iter < n - 1) Wg[idx] = w + a.eps * p;
+        if (!last) Wg[idx] = w + a.eps * p;
         else p2s += (double)(p * p);
       }
     }
@@ -557,8 +577,9 @@ template <typename T, int NW> struct BGW {
 };
 constexpr int BRW2 = 64;          // k_bgradw<T, 4> feature tile
 
+// amdgpu_waves_per_eu(2): two 4-wave workgroups per CU (the LDS allows two) need <= 256 registers.
 template <typename T, int NW>
-__global__ __launch_bounds__(64 * NW) void k_bgradw(BGradArgs<T> a) {
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) void k_bgradw(BGradArgs<T> a) {
   using M = mfma16<T>;
   using G = BGW<T, NW>;
   typedef typename StageMap<T>::v2 v2;
@@ -617,6 +638,15 @@ __global__ __launch_bounds__(64 * NW) void k_bgradw(BGradArgs<T> a) {
   };
 
   const int mt = wave % G::NMT, nh = wave / G::NMT;     // wave: features mt·32 .. +32, columns nh·80 .. +80
+  // bit j: column j of this lane belongs to a chain whose path ends at this iteration (read once here,
+  // its latency hidden by the main loop, instead of a waited load per column in the epilogue)
+  int lastm = 0;
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    const int ch = chs[((nh * 5 + j) * 16 + lr) / BKC];
+    const int n = a.n_iter[ch >= 0 ? ch : 0];
+    lastm |= (ch >= 0 && a.iter >= n - 1) << j;
+  }
   // m-tiles of this wave holding features (wave-uniform): a partial last tile (D = 784: 16 of 64
   // features) skips the MFMAs of its empty m-tiles; their accumulators stay zero and are never stored
   const int nmw = min(2, max(0, (nfeat - mt * 32 + 15) / 16));
@@ -662,13 +692,19 @@ __global__ __launch_bounds__(64 * NW) void k_bgradw(BGradArgs<T> a) {
   T* Nz = Ds;
   double* kp = reinterpret_cast<double*>(Xs);        // [mt·4 + lg][BNP] Σ p² over the lane's rows
   // The elements of one column (the pass's m-tiles × 4 rows) are loaded together (W and pW never
-  // alias): one HBM round trip per column instead of one per element.
+  // alias); every load is unconditional (clamped address, value selected afterwards) and the noise source is
+  // chosen per launch outside the element loops: a load under a branch — or one through a pointer
+  // that may be LDS or global, i.e. a flat load — made hipcc wait for each element's load (and the
+  // previous element's stores) before the next.
   T* __restrict__ Wg = a.W;
   T* __restrict__ Pg = a.pW;
+  const bool buf = a.noise_mode == HMCX_NOISE_BUFFER;
   double p2s[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+  constexpr int NI = 2 / G::NPASS;                   // m-tiles of one pass
 #pragma unroll
   for (int h = 0; h < G::NPASS; ++h) {
-    if (a.noise_mode != HMCX_NOISE_BUFFER) {
+    const int i0 = G::NPASS == 2 ? h : 0;
+    if (!buf) {
       if (h) __syncthreads();                      // pass 0's noise has been read
       if constexpr (G::NPASS == 2)
         gen_tile_noise(a, chs, d0, nfeat, Nz, G::NZR, [h](int fl) { return (fl >> 4) * 32 + h * 16 + (fl & 15); });
@@ -676,14 +712,12 @@ __global__ __launch_bounds__(64 * NW) void k_bgradw(BGradArgs<T> a) {
         gen_tile_noise(a, chs, d0, nfeat, Nz, G::FT, [](int fl) { return fl; });
       __syncthreads();
     }
-    constexpr int NI = 2 / G::NPASS;                 // m-tiles of this pass
-    const int i0 = G::NPASS == 2 ? h : 0;
 #pragma unroll
     for (int j = 0; j < 5; ++j) {
       const int col = (nh * 5 + j) * 16 + lr;
       const int cs = col / BKC, k = col - cs * BKC, ch = chs[cs];
-      const bool last = ch >= 0 && a.iter >= a.n_iter[ch] - 1;
-      T wv[NI * 4], pv[NI * 4];
+      const bool last = (lastm >> j) & 1;
+      T wv[NI * 4], pv[NI * 4], zv[NI * 4];
 #pragma unroll
       for (int ii = 0; ii < NI; ++ii)
 #pragma unroll
@@ -691,9 +725,31 @@ __global__ __launch_bounds__(64 * NW) void k_bgradw(BGradArgs<T> a) {
           const int fi = mt * 32 + (i0 + ii) * 16 + M::row(lane, q);
           const bool ok = ch >= 0 && fi < nfeat;
           const size_t idx = ok ? ((size_t)ch * D + (d0 + fi)) * BKC + k : 0;
-          wv[ii * 4 + q] = ok ? Wg[idx] : T(0);
-          pv[ii * 4 + q] = ok ? Pg[idx] : T(0);
+          const T w = Wg[idx], pw = Pg[idx];
+          wv[ii * 4 + q] = ok ? w : T(0);
+          pv[ii * 4 + q] = ok ? pw : T(0);
         }
+      if (buf) {
+        const int64_t nb = (ch >= 0 ? a.noff[ch] : 0) + (int64_t)a.slot * a.P;
+#pragma unroll
+        for (int ii = 0; ii < NI; ++ii)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int fi = mt * 32 + (i0 + ii) * 16 + M::row(lane, q);
+            const bool ok = ch >= 0 && fi < nfeat;
+            const double z = a.noise[ok ? nb + (uint32_t)((d0 + fi) * BKC + k) : 0];
+            zv[ii * 4 + q] = ok ? (T)z : T(0);
+          }
+      } else {
+#pragma unroll
+        for (int ii = 0; ii < NI; ++ii)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int fi = mt * 32 + (i0 + ii) * 16 + M::row(lane, q);
+            const int nzr = G::NPASS == 2 ? mt * 16 + M::row(lane, q) : fi;
+            zv[ii * 4 + q] = Nz[nzr * BNP + col];
+          }
+      }
 #pragma unroll
       for (int ii = 0; ii < NI; ++ii)
 #pragma unroll
@@ -705,11 +761,7 @@ __global__ __launch_bounds__(64 * NW) void k_bgradw(BGradArgs<T> a) {
             const size_t idx = ((size_t)ch * D + d) * BKC + k;
             const T w = wv[ii * 4 + q];
             const T gr = -(acc[i][j][q] - a.alpha * w);
-            const int nzr = G::NPASS == 2 ? mt * 16 + M::row(lane, q) : fi;
-            const T z = a.noise_mode == HMCX_NOISE_BUFFER
-                            ? (T)a.noise[a.noff[ch] + (int64_t)a.slot * a.P + (uint32_t)(d * BKC + k)]
-                            : Nz[nzr * BNP + col];
-            const T p = (a.one_minus_eps * pv[ii * 4 + q] + a.eps * gr) + a.noise_scale * z;
+            const T p = (a.one_minus_eps * pv[ii * 4 + q] + a.eps * gr) + a.noise_scale * zv[ii * 4 + q];
             Pg[idx] = p;
             if (!last) Wg[idx] = w + a.eps * p;
             else p2s[j] += (double)(p * p);
