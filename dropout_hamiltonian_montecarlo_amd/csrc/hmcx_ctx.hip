@@ -477,6 +477,11 @@ int hmcx_create(int device, hmcx_ctx** out) {
     delete c;
     return HMCX_EHIP;
   }
+  if (hipMalloc(&c->zeros_dev, 256) != hipSuccess || hipMemset(c->zeros_dev, 0, 256) != hipSuccess) {
+    (void)hipFree(c->abort_dev);
+    delete c;
+    return HMCX_EHIP;
+  }
   int ncu = 0, lds = 0;
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
     c->num_cus = ncu;
@@ -504,6 +509,7 @@ int hmcx_destroy(hmcx_ctx* ctx) {
   for (auto e : ctx->host_mark_pool) (void)hipEventDestroy(e);
   if (ctx->abort_host) (void)hipHostFree(ctx->abort_host);
   if (ctx->abort_dev) (void)hipFree(ctx->abort_dev);
+  if (ctx->zeros_dev) (void)hipFree(ctx->zeros_dev);
   if (ctx->gx_arena) (void)hipFree(ctx->gx_arena);
   for (auto& g : ctx->graveyard) {
     (void)hipGraphExecDestroy(g.first);

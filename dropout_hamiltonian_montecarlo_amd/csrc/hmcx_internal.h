@@ -53,6 +53,7 @@ struct hmcx_ctx {
   // checked once the launch's event has completed (next call, hmcx_synchronize), not by a per-call sync
   int* abort_host = nullptr;           // pinned [ABORT_SLOTS]
   int* abort_dev = nullptr;            // device word: raised by a timed-out persistent launch, sticky
+  void* zeros_dev = nullptr;           // 256 zero bytes: a valid target for loads whose value is discarded
                                        // until hmcx_clear_abort (later launches return at once)
   std::vector<std::pair<hipEvent_t, int>> abort_pend;
   std::vector<std::pair<const void*, hipEvent_t>> host_marks;   // out_host block -> its latest copy's event

@@ -82,6 +82,16 @@ struct Q2Args {
   struct { double eps, u; int64_t row0; int32_t n_iter, pad_; } inl[32];
 };
 constexpr int P2_NINL = 32;                 // calls of up to this many steps pass their schedule inline
+// One schedule value of step s: the kernel-argument copy (inline calls) and the global array are both
+// loaded and the value selected.  A conditional `inl ? a.inl[s].x : a.x[s]` became one load through a
+// pointer that may be the kernarg segment or global memory — a flat load, which every later
+// `s_waitcnt lgkmcnt` (LDS traffic) then also waited for.  Inline calls point the arrays at zeros.
+__device__ inline int sched_k(int s) { return s < P2_NINL ? s : P2_NINL - 1; }
+template <typename V>
+__device__ inline V sched_at(bool inl, int s, V kv, const V* g) {
+  const V gv = g[inl ? 0 : s];
+  return inl ? kv : gv;
+}
 
 // Writes the launch's abort verdict when the workgroup leaves the kernel, whichever return it takes:
 // workgroup 0 reaching the end means every member passed the last accept round (0); any early return
@@ -391,10 +401,10 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
 
   for (int s = 0; s < a.n_steps; ++s) {
     const int tid = opaque((int)threadIdx.x), lane = tid & 63, wave = tid >> 6, lr = lane & 15;   // not hoisted (registers)
-    const double epsd = inl ? a.inl[s].eps : a.eps[s];
+    const double epsd = sched_at(inl, s, a.inl[sched_k(s)].eps, a.eps);
     const T eps = (T)epsd, ome = (T)(1.0 - epsd), nsc = (T)(2.0 * epsd);
-    const int n = inl ? a.inl[s].n_iter : a.n_iter[s];
-    const int64_t rw = inl ? a.inl[s].row0 : a.row0[s];
+    const int n = sched_at(inl, s, a.inl[sched_k(s)].n_iter, a.n_iter);
+    const int64_t rw = sched_at(inl, s, a.inl[sched_k(s)].row0, a.row0);
     const T* Xg = reinterpret_cast<const T*>(a.X) + (size_t)rw * D;
     const T* Yg = reinterpret_cast<const T*>(a.Y) + (size_t)rw * K;
     prof.stamp(0);
@@ -783,7 +793,7 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
     // (measured: loading it with only the half of the workgroup that does not poll the accept round
     // is slower — 9.68 vs 9.44 µs per leapfrog: two load batches instead of one)
     if (prefetch && s + 1 < a.n_steps) {
-      const int64_t rn = inl ? a.inl[s + 1].row0 : a.row0[s + 1];
+      const int64_t rn = sched_at(inl, s + 1, a.inl[sched_k(s + 1)].row0, a.row0);
       const T* Xn = reinterpret_cast<const T*>(a.X) + (size_t)rn * D;
       const T* Yn = reinterpret_cast<const T*>(a.Y) + (size_t)rn * K;
       load_step_rows<T>(Xs, Yo, Xn, Yn, Br, BfP, BFP, nrow, nfeat, row0, feat0, D, K, Ro, nro, ro0);
@@ -811,13 +821,13 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
     int acc;
     if (n <= 0) {
       A = 1.0; Enew = Ecur; llq = L0;
-      acc = (inl ? a.inl[s].u : a.u[s]) < A;
+      acc = sched_at(inl, s, a.inl[sched_k(s)].u, a.u) < A;
     } else {
       const double K1 = (0.0 + 0.5 * S1) + 0.5 * kb1;
       Enew = a.neg_inv_n * (ll_last + a.log_prior) + K1;
       const double x = exp(Ecur - Enew);
       A = (x < 1.0) ? x : 1.0;                                             // Python min(1, x)
-      acc = (inl ? a.inl[s].u : a.u[s]) < A;
+      acc = sched_at(inl, s, a.inl[sched_k(s)].u, a.u) < A;
       llq = acc ? ll_last : L0;
     }
     if (!acc || n <= 0) {                                                  // keep q (sghmc.py:36-38)
@@ -976,6 +986,11 @@ int sghmc_p2_t(hmcx_ctx* ctx, const hmcx_sampler_args* s, const PersistPlan2& pl
   a.alpha = s->alpha; a.neg_inv_n = -1.0 / (double)s->B; a.log_prior = s->log_prior;
   a.X = s->X; a.Y = s->Y;
   a.eps = d_eps; a.u = d_u; a.row0 = d_row0; a.n_iter = d_n;
+  if (a.ninl > 0) {              // the kernel loads both sources and selects the value (sched_at)
+    a.eps = a.u = reinterpret_cast<double*>(ctx->zeros_dev);
+    a.row0 = reinterpret_cast<int64_t*>(ctx->zeros_dev);
+    a.n_iter = reinterpret_cast<int32_t*>(ctx->zeros_dev);
+  }
   a.noise_mode = s->noise_mode; a.noise = s->noise; a.noff = d_noff;
   a.seed = s->seed; a.chain0 = s->chain0; a.step_base = s->step_base;
   a.W = s->W; a.b = s->b;
