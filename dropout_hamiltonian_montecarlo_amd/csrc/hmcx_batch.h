@@ -171,6 +171,11 @@ __global__ __launch_bounds__(256) void k_bfwd(BFwdArgs<T> a) {
   __shared__ T Ws[BCH * BWP];          // also the epilogue tile, 32 rows at a time
   __shared__ double Lt[ROWS][BCT];
   __shared__ int chs[BCT];
+  // epilogue operands loaded with the first chunk (their latency hidden by the main loop, not paid
+  // per row pair in the epilogue): the tile's labels, the chains' b / pb, the path-end flags
+  __shared__ T Ysh[ROWS * BKC];
+  __shared__ T bsh[BNT], pbsh[BNT];
+  __shared__ int lastsh[BCT];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lg = lane >> 4;
   int bx, by;
   if (!xcd_tile(a.nX, a.nCT, bx, by)) return;
@@ -219,6 +224,26 @@ __global__ __launch_bounds__(256) void k_bfwd(BFwdArgs<T> a) {
 #pragma unroll
     for (int j = 0; j < 5; ++j) acc[i][j] = M::zero();
   fetch(0);
+  {
+    const bool sg = a.mode == FWD_SGHMC;
+    constexpr int NYV = (ROWS * BKC + 255) / 256;
+    T yv[NYV];
+#pragma unroll
+    for (int u = 0; u < NYV; ++u) {
+      const int t = min(tid + 256 * u, ROWS * BKC - 1), r = t / BKC;
+      yv[u] = a.Y[(size_t)(m0 + min(r, nrow - 1)) * BKC + (t - r * BKC)];
+    }
+    const int tb = min(tid, BNT - 1), cs = tb / BKC, ch = chs[cs];
+    const size_t bi = (size_t)(ch >= 0 ? ch : 0) * BKC + (tb - cs * BKC);
+    const T bv0 = a.b[bi], pbv0 = sg ? a.pb[bi] : T(0);
+    const int cl = chs[tid & (BCT - 1)];
+    const int nt = a.n_iter[cl >= 0 ? cl : 0];
+#pragma unroll
+    for (int u = 0; u < NYV; ++u)
+      if (tid + 256 * u < ROWS * BKC) Ysh[tid + 256 * u] = yv[u];
+    if (tid < BNT) { bsh[tid] = bv0; pbsh[tid] = pbv0; }
+    if (tid < BCT) lastsh[tid] = sg && cl >= 0 && a.iter == nt - 1;
+  }
   for (int k0 = 0; k0 < D; k0 += BCH) {
     __syncthreads();
     stash();
@@ -262,18 +287,18 @@ __global__ __launch_bounds__(256) void k_bfwd(BFwdArgs<T> a) {
       const int il = pr >> 4, cs = pr & 15, ch = chs[cs];
       const int i = half * 32 + il;
       if (ch < 0 || i >= nrow) { Lt[i][cs] = 0.0; continue; }
-      const bool last = sghmc && a.iter == a.n_iter[ch] - 1;
+      const bool last = lastsh[cs];
       T z[BKC], y[BKC];
 #pragma unroll
       for (int k = 0; k < BKC; ++k) {
         z[k] = Zt[il * BWP + cs * BKC + k];
-        y[k] = a.Y[(size_t)(m0 + i) * BKC + k];
+        y[k] = Ysh[i * BKC + k];
       }
       // variant 1: bias b (weights sub-step diff / LL mode)
       T zc[BKC], m = T(0), s = T(0);
 #pragma unroll
       for (int k = 0; k < BKC; ++k) {
-        zc[k] = clipz(z[k] + a.b[ch * BKC + k], hi, lo);
+        zc[k] = clipz(z[k] + bsh[cs * BKC + k], hi, lo);
         m = k == 0 ? zc[0] : max_nan(m, zc[k]);
       }
       T e[BKC];
@@ -294,7 +319,7 @@ __global__ __launch_bounds__(256) void k_bfwd(BFwdArgs<T> a) {
       T m2 = T(0), s2 = T(0);
 #pragma unroll
       for (int k = 0; k < BKC; ++k) {
-        const T bp = a.b[ch * BKC + k] + a.eps * a.pb[ch * BKC + k];
+        const T bp = bsh[cs * BKC + k] + a.eps * pbsh[cs * BKC + k];
         zc[k] = clipz(z[k] + bp, hi, lo);
         m2 = k == 0 ? zc[0] : max_nan(m2, zc[k]);
       }
