@@ -451,7 +451,7 @@ def main():
                         "source": "%d untimed steps after the timed region, state after every step; Welford "
                                   "mean/M2 per parameter and every %dth draw, one all_gather" % (DIAG_STEPS, DIAG_THIN),
                         "rhat_ll": float(np.ravel(diag["rhat"])[0]), "ess_ll": float(np.ravel(diag["ess"])[0]),
-                        "gather": "torch.distributed all_gather (%s)" % (parallel.backend_name() if world > 1 else "local")},
+                        "gather": "torch.distributed all_gather (%s)" % (parallel.backend_name() if parallel.dist.is_initialized() else "local")},
         "cpu_baseline": None,
         "chain_batched": batched,
         "mlp": mlp_out,
@@ -461,6 +461,8 @@ def main():
         out["cpu_baseline"] = cpu_baseline(X, Y, args.cpu_seconds)
         out["cpu_baseline_1thread"] = cpu_baseline(X, Y, args.cpu_seconds, threads=1)
     print(json.dumps(out))
+    if parallel.dist.is_initialized():
+        parallel.dist.destroy_process_group()
 
 
 if __name__ == "__main__":

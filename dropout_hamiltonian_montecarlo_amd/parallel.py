@@ -26,11 +26,14 @@ from . import diagnostics
 
 def init(backend=None):
     """Initialise the process group from the environment; returns (rank, world, local_rank).
-    Backend: `backend`, else $HMCX_DIST_BACKEND, else "nccl" (RCCL) with a GPU and "gloo" without."""
+    Backend: `backend`, else $HMCX_DIST_BACKEND, else "nccl" (RCCL) with a GPU and "gloo" without.
+    One rank normally runs without a process group; HMCX_DIST_FORCE=1 creates it anyway (a world-1
+    RCCL communicator: the collective path of the multi-GPU run, exercised on one GPU)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
-    if world > 1 and not dist.is_initialized():
+    force = os.environ.get("HMCX_DIST_FORCE") == "1"
+    if (world > 1 or force) and not dist.is_initialized():
         if backend is None:
             backend = os.environ.get("HMCX_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         if backend == "nccl":

@@ -1,0 +1,40 @@
+"""The collective path of the multi-GPU bench on real hardware: bench.py launched by torchrun with
+one rank and HMCX_DIST_FORCE=1, so the process group is an RCCL ("nccl") communicator and the
+timing max/sum reductions and the per-parameter summary all-gather go through RCCL on the GPU
+(parallel.init, gather_summaries).  N > 1 ranks need one GPU each (the driver's 8-GPU run); the
+N = 2 logic itself is covered by the gloo tests in tests/test_parallel_cpu.py."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_bench_world1_through_rccl():
+    port = str(_free_port())
+    env = dict(os.environ, HMCX_DIST_FORCE="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", port, "bench.py", "--gpus", "1",
+           "--steps", "5", "--warmup", "2", "--cpu-seconds", "0", "--batched-chains", "0",
+           "--mlp-steps", "0", "--sgld-steps", "0"]
+    r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 1 and line["value"] > 0
+    diag = line["diagnostics"]
+    assert "nccl" in diag["gather"], diag["gather"]
+    pp = diag["per_parameter"]
+    assert pp["chains"] == 1 and pp["params"] == 7850
+    assert 0.5 < pp["rhat"]["median"] < 2.0
