@@ -77,8 +77,6 @@ template <typename T> struct BFwdArgs {
   int nX, nCT;                      // row tiles × chain tiles (XCD-grouped 1-D grid, xcd_tile)
   T* colsum_part;                   // [nRB][N]
   double* ll_part;                  // [nRB][C]
-  double* ll0_part;                 // FWD_SGHMC at iteration 0 (non-null): also the log-likelihood at the
-                                    // step's start (q0, b0) — the E_current forward — into [nRB][C]
 };
 
 template <typename T> struct BGradArgs {
@@ -269,10 +267,6 @@ __global__ __launch_bounds__(256) void k_bfwd(BFwdArgs<T> a) {
   // ---- epilogue, 32 rows at a time through Zt: softmax.py:32-36 (clip, max, exp, normalise), :52
   const T hi = (T)CLIP_HI, lo = (T)CLIP_LO;
   const bool sghmc = a.mode == FWD_SGHMC;
-  // iteration 0 evaluates the logits at q0 = the step's start, so its variant-1 softmax (bias b0) is
-  // also E_current's log-likelihood (same GEMM, same reduction order as the FWD_LL launch it replaces)
-  const bool with_ll0 = sghmc && a.ll0_part != nullptr;
-  double* Lt0 = reinterpret_cast<double*>(Xs);         // [ROWS][BCT] (the X chunk is dead by now)
   T* Zt = Ws;                                          // [32][BWP] logits, then y − ŷ'
   T cs_acc = T(0);                                     // thread t < 160: Σ_rows (y − ŷ') of column t
   for (int half = 0; half < MT; ++half) {
@@ -292,11 +286,7 @@ __global__ __launch_bounds__(256) void k_bfwd(BFwdArgs<T> a) {
     for (int pr = tid; pr < 32 * BCT; pr += 256) {
       const int il = pr >> 4, cs = pr & 15, ch = chs[cs];
       const int i = half * 32 + il;
-      if (ch < 0 || i >= nrow) {
-        Lt[i][cs] = 0.0;
-        if (with_ll0) Lt0[i * BCT + cs] = 0.0;
-        continue;
-      }
+      if (ch < 0 || i >= nrow) { Lt[i][cs] = 0.0; continue; }
       const bool last = lastsh[cs];
       T z[BKC], y[BKC];
 #pragma unroll
@@ -314,16 +304,13 @@ __global__ __launch_bounds__(256) void k_bfwd(BFwdArgs<T> a) {
       T e[BKC];
 #pragma unroll
       for (int k = 0; k < BKC; ++k) { e[k] = exp(zc[k] - m); s += e[k]; }
-      if (!sghmc || with_ll0) {
+      if (!sghmc) {
         const T lse = log(s) + m;
         double ll = 0.0;
 #pragma unroll
         for (int k = 0; k < BKC; ++k) ll += (double)(y[k] * (zc[k] - lse));
-        if (!sghmc) {
-          Lt[i][cs] = ll;
-          continue;
-        }
-        Lt0[i * BCT + cs] = ll;
+        Lt[i][cs] = ll;
+        continue;
       }
       T* drow = a.diff + ((size_t)ch * a.B + (m0 + i)) * BKC;
 #pragma unroll
@@ -364,11 +351,6 @@ __global__ __launch_bounds__(256) void k_bfwd(BFwdArgs<T> a) {
       double v = 0.0;
       for (int i = 0; i < nrow; ++i) v += Lt[i][tid];
       a.ll_part[(size_t)bx * a.C + ch] = v;
-    }
-    if (with_ll0 && ch >= 0) {
-      double v = 0.0;
-      for (int i = 0; i < nrow; ++i) v += Lt0[i * BCT + tid];
-      a.ll0_part[(size_t)bx * a.C + ch] = v;
     }
   }
 }

@@ -1347,15 +1347,9 @@ int sghmc_batch_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
     f.W = (const T*)s->W; f.b = (const T*)s->b; f.pb = pb;
     f.ll_part = ll0;
     f.nX = nRB; f.nCT = (C + BCT - 1) / BCT;
-    // E_current's forward rides in iteration 0's forward (launched over all C chains; chains with no
-    // iteration only contribute their log-likelihood) unless no chain iterates this step
-    static const bool ll_sep = getenv("HMCX_BATCH_LL0") && getenv("HMCX_BATCH_LL0")[0] == '0';
-    const bool fuse_ll0 = maxit > 0 && !ll_sep;
-    if (!fuse_ll0) {
-      if (big) hipLaunchKernelGGL((k_bfwd<T, 2, 0>), dim3(xcd_grid(f.nX, f.nCT)), dim3(256), 0, st, f);
-      else hipLaunchKernelGGL((k_bfwd<T, 1, 0>), dim3(xcd_grid(f.nX, f.nCT)), dim3(256), 0, st, f);
-      HMCX_HIP(ctx, hipGetLastError());
-    }
+    if (big) hipLaunchKernelGGL((k_bfwd<T, 2, 0>), dim3(xcd_grid(f.nX, f.nCT)), dim3(256), 0, st, f);
+    else hipLaunchKernelGGL((k_bfwd<T, 1, 0>), dim3(xcd_grid(f.nX, f.nCT)), dim3(256), 0, st, f);
+    HMCX_HIP(ctx, hipGetLastError());
 
     f.mode = FWD_SGHMC; f.W = Wwork; f.b = bwork;
     f.diff = diff; f.colsum_part = csp; f.ll_part = ll1;
@@ -1372,9 +1366,7 @@ int sghmc_batch_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
       int c_act = 0;
       while (c_act < C && ni_h[perm[(size_t)st_i * C + c_act]] > it) ++c_act;
       f.iter = it; f.c_act = c_act;
-      f.ll0_part = nullptr;
-      if (it == 0 && fuse_ll0) { f.c_act = C; f.ll0_part = ll0; }
-      f.nX = nRB; f.nCT = (f.c_act + BCT - 1) / BCT;
+      f.nX = nRB; f.nCT = (c_act + BCT - 1) / BCT;
       if (big) hipLaunchKernelGGL((k_bfwd<T, 2, 1>), dim3(xcd_grid(f.nX, f.nCT)), dim3(256), 0, st, f);
       else hipLaunchKernelGGL((k_bfwd<T, 1, 1>), dim3(xcd_grid(f.nX, f.nCT)), dim3(256), 0, st, f);
       HMCX_HIP(ctx, hipGetLastError());
