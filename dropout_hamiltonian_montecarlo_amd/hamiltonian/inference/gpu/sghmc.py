@@ -289,14 +289,16 @@ class sghmc(sgmcmc):
         if self.trace is not None:
             t0 = h['t0']
             if C == 1:                       # Python floats / bools straight from tolist()
-                for t, a_, c_ in zip(self.trace[t0:t0 + n_steps], A.tolist(), acc.tolist()):
+                for t, a_, c_, e_ in zip(self.trace[t0:t0 + n_steps], A.tolist(), acc.tolist(), res.E.tolist()):
                     t['A'] = a_
                     t['accepted'] = c_
+                    t['E'] = e_                      # (E_current, E_new) of the accept test
             else:
                 for s in range(n_steps):
                     t = self.trace[t0 + s]
                     t['A'] = res.A[s].copy()
                     t['accepted'] = res.accepted[s].copy()
+                    t['E'] = res.E[s].copy()
         return res
 
     def _recover(self, h):

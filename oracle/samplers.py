@@ -109,7 +109,7 @@ class sghmc(sgmcmc):
             p = p_new.copy()
         if self.trace is not None:
             self.trace.append({'L': float(path_length), 'A': float(acceptprob),
-                               'accepted': accepted, 'eps': float(epsilon)})
+                               'accepted': accepted, 'eps': float(epsilon), 'E': self._E})
         return q, p, acceptprob
 
     # --- A1 completion: cpu/hmc.py:67-87 -------------------------------------
@@ -117,6 +117,7 @@ class sghmc(sgmcmc):
         E_new = (self.model.negative_log_posterior(proposal_q, **args) + self.potential_energy(proposal_p))
         E_current = (self.model.negative_log_posterior(current_q, **args) + self.potential_energy(current_p))
         A = min(1, np.exp(E_current - E_new))
+        self._E = (float(E_current), float(E_new))        # test-side record for the trace (no effect on A)
         return A
 
     def potential_energy(self, p):                                        # hmc.py:74-79

@@ -57,6 +57,10 @@ def test_replica_chains_match_oracle(name, chains):
         for t_g, t_r in zip(tr_g, tr_r):
             assert np.all(t_g["L"] == t_r["L"])
             assert np.all(t_g["accepted"] == t_r["accepted"])
+            # both energies of the accept test (E_current at the step start, E_new at the proposal):
+            # A and the accept flag alone do not pin them — A is capped at 1, or ~0 on hot chains
+            np.testing.assert_allclose(np.broadcast_to(t_g["A"], (chains,)), t_r["A"], rtol=1e-9, atol=1e-12)
+            np.testing.assert_allclose(t_g["E"], np.broadcast_to(t_r["E"], (chains, 2)), rtol=1e-10, atol=1e-9)
     for ch in range(chains):
         for v in ("weights", "bias"):
             np.testing.assert_allclose(post_g[v][ch], post_r[v], rtol=1e-9, atol=1e-12)

@@ -77,6 +77,7 @@ def test_trajectory_f64_vs_oracle_and_golden(name, path, golden_dir):
         A_r = np.array([t["A"] for t in tr_r])
         A_g = np.array([t["A"] for t in tr_g])
         np.testing.assert_allclose(A_g, A_r, rtol=1e-9, atol=1e-12)
+        np.testing.assert_allclose([t["E"] for t in tr_g], [t["E"] for t in tr_r], rtol=1e-10, atol=1e-9)
     # the printed log lines (4 decimals) are identical to the reference's
     ref_lines = [l for l in log_r.splitlines() if "loss" in l]
     gpu_lines = [l for l in log_g.splitlines() if "loss" in l]
