@@ -163,10 +163,16 @@ struct StageCM {
 // staging per MFMA; used when enough chains are active to fill the chip).
 // CM: W is the chain-major working copy [C][D][10] (else the caller's [D][C·10]); diff is written
 // chain-major [C][B][10].
-template <typename T, int MT, int CM>
-__global__ __launch_bounds__(256) void k_bfwd(BFwdArgs<T> a) {
+// NWV = 8 (MT = 2 only): the same 64-row tile and partial layout with 8 waves, one m-tile each — for
+// launches too small to give every CU two workgroups (the compaction tail), where one 4-wave
+// workgroup per CU leaves the MFMA latency exposed.  Waves 0-3 stage the chunks.
+template <typename T, int MT, int CM, int NWV = 4>
+__global__ __launch_bounds__(64 * NWV) void k_bfwd(BFwdArgs<T> a) {
   using M = mfma16<T>;
   constexpr int ROWS = 32 * MT;
+  constexpr int NTH = 64 * NWV;
+  constexpr int MW = NWV == 8 ? MT / 2 : MT;          // m-tiles per wave
+  static_assert(NWV == 4 || (NWV == 8 && MT == 2), "k_bfwd: 8 waves need 64-row tiles");
   __shared__ T Xs[ROWS * BXP];
   __shared__ T Ws[BCH * BWP];          // also the epilogue tile, 32 rows at a time
   __shared__ double Lt[ROWS][BCT];
@@ -193,7 +199,9 @@ __global__ __launch_bounds__(256) void k_bfwd(BFwdArgs<T> a) {
 #pragma unroll
   for (int u = 0; u < 2 * MT; ++u) xsrc[u] = a.X + (size_t)(m0 + min(sm.xr[u], nrow - 1)) * D + sm.xc[u];
   typename StageMap<T>::v2 xv[2 * MT], wv[10];
+  const bool stager = NWV == 4 || tid < 256;         // wave-uniform
   auto fetch = [&](int k0) {
+    if (!stager) return;
 #pragma unroll
     for (int u = 0; u < 2 * MT; ++u) xv[u] = ld2<T>(xsrc[u] + k0, sm.xr[u] < nrow, D - k0 - sm.xc[u]);
 #pragma unroll
@@ -208,6 +216,7 @@ __global__ __launch_bounds__(256) void k_bfwd(BFwdArgs<T> a) {
     }
   };
   auto stash = [&]() {
+    if (!stager) return;
 #pragma unroll
     for (int u = 0; u < 2 * MT; ++u) st2<T>(Xs + sm.xr[u] * BXP + sm.xc[u], xv[u]);
 #pragma unroll
@@ -217,14 +226,15 @@ __global__ __launch_bounds__(256) void k_bfwd(BFwdArgs<T> a) {
     }
   };
 
-  const int wm = wave & 1, nh = wave >> 1;            // rows [16·(wm·MT + i)], 5 n-tiles per wave
-  typename M::acc_t acc[MT][5];
+  // rows [16·(wm·MW + i)], 5 n-tiles per wave
+  const int wm = NWV == 8 ? (wave & 3) : (wave & 1), nh = NWV == 8 ? (wave >> 2) : (wave >> 1);
+  typename M::acc_t acc[MW][5];
 #pragma unroll
-  for (int i = 0; i < MT; ++i)
+  for (int i = 0; i < MW; ++i)
 #pragma unroll
     for (int j = 0; j < 5; ++j) acc[i][j] = M::zero();
   fetch(0);
-  {
+  if (stager) {
     const bool sg = a.mode == FWD_SGHMC;
     constexpr int NYV = (ROWS * BKC + 255) / 256;
     T yv[NYV];
@@ -252,13 +262,13 @@ __global__ __launch_bounds__(256) void k_bfwd(BFwdArgs<T> a) {
     const int nks = min(BCH, D - k0 + 3) / 4;
 #pragma unroll 2
     for (int ks = 0; ks < nks; ++ks) {
-      T av[MT], bv[5];
+      T av[MW], bv[5];
 #pragma unroll
-      for (int i = 0; i < MT; ++i) av[i] = Xs[((wm * MT + i) * 16 + lr) * BXP + ks * 4 + lg];
+      for (int i = 0; i < MW; ++i) av[i] = Xs[((wm * MW + i) * 16 + lr) * BXP + ks * 4 + lg];
 #pragma unroll
       for (int j = 0; j < 5; ++j) bv[j] = Ws[(ks * 4 + lg) * BWP + (nh * 5 + j) * 16 + lr];
 #pragma unroll
-      for (int i = 0; i < MT; ++i)
+      for (int i = 0; i < MW; ++i)
 #pragma unroll
         for (int j = 0; j < 5; ++j) acc[i][j] = M::fma(av[i], bv[j], acc[i][j]);
     }
@@ -272,9 +282,9 @@ __global__ __launch_bounds__(256) void k_bfwd(BFwdArgs<T> a) {
   for (int half = 0; half < MT; ++half) {
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < MT; ++i) {
-      // wave rows of m-tile (wm·MT + i) fall in half (wm·MT + i) / 2
-      const int mtile = wm * MT + i;
+    for (int i = 0; i < MW; ++i) {
+      // wave rows of m-tile (wm·MW + i) fall in half (wm·MW + i) / 2
+      const int mtile = wm * MW + i;
       if ((mtile >> 1) != half) continue;
 #pragma unroll
       for (int j = 0; j < 5; ++j)
@@ -283,7 +293,7 @@ __global__ __launch_bounds__(256) void k_bfwd(BFwdArgs<T> a) {
           Zt[((mtile & 1) * 16 + M::row(lane, q)) * BWP + (nh * 5 + j) * 16 + lr] = acc[i][j][q];
     }
     __syncthreads();
-    for (int pr = tid; pr < 32 * BCT; pr += 256) {
+    for (int pr = tid; pr < 32 * BCT; pr += NTH) {
       const int il = pr >> 4, cs = pr & 15, ch = chs[cs];
       const int i = half * 32 + il;
       if (ch < 0 || i >= nrow) { Lt[i][cs] = 0.0; continue; }

@@ -1367,7 +1367,11 @@ int sghmc_batch_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
       while (c_act < C && ni_h[perm[(size_t)st_i * C + c_act]] > it) ++c_act;
       f.iter = it; f.c_act = c_act;
       f.nX = nRB; f.nCT = (c_act + BCT - 1) / BCT;
-      if (big) hipLaunchKernelGGL((k_bfwd<T, 2, 1>), dim3(xcd_grid(f.nX, f.nCT)), dim3(256), 0, st, f);
+      // launches that leave CUs without a second workgroup: the 8-wave variant of the 64-row tile
+      static const bool bf8_off = getenv("HMCX_BFWD8") && getenv("HMCX_BFWD8")[0] == '0';
+      if (big && !bf8_off && f.nX * f.nCT <= ctx->num_cus)
+        hipLaunchKernelGGL((k_bfwd<T, 2, 1, 8>), dim3(xcd_grid(f.nX, f.nCT)), dim3(512), 0, st, f);
+      else if (big) hipLaunchKernelGGL((k_bfwd<T, 2, 1>), dim3(xcd_grid(f.nX, f.nCT)), dim3(256), 0, st, f);
       else hipLaunchKernelGGL((k_bfwd<T, 1, 1>), dim3(xcd_grid(f.nX, f.nCT)), dim3(256), 0, st, f);
       HMCX_HIP(ctx, hipGetLastError());
       g.iter = it; g.c_act = c_act; g.slot = (uint32_t)(it + 1);
