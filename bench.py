@@ -52,7 +52,79 @@ def parse():
                     help="SGHMC steps of the secondary config-3 MLP measurement (0 = skip)")
     ap.add_argument("--sgld-steps", type=int, default=400,
                     help="SGLD steps of the secondary config-5 (D=2048, K=38) measurement (0 = skip)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher check without a GPU: ranks rendezvous over gloo, reduce a dummy count "
+                         "and rank 0 prints the JSON line shape (tests/test_bench_launch.py)")
     return ap.parse_args()
+
+
+def launch_ranks(n, argv):
+    """`--gpus N` (N > 1) started without a launcher (no WORLD_SIZE in the environment): start N
+    fresh rank processes of this script, one per GPU, and relay rank 0's JSON line.
+
+    The reference's multi-chain layer starts its own workers (hamiltonian/inference/cpu/
+    sghmc_multicore.py:81-99: a Pool, RandomState(i) per worker); here each rank is a child process
+    with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set, exactly what
+    torch.distributed.run would give it.  Called before anything touches the GPU (this process never
+    imports torch); the children are started with Popen — nothing is exec'd.  Returns the exit
+    code: 0 only when every rank exited 0; a failed rank stops the others (their exact PIDs)."""
+    import signal
+    import socket
+    import subprocess
+    import tempfile
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    me = os.path.abspath(__file__)
+    out0 = tempfile.TemporaryFile(mode="w+")
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HMCX_BENCH_CHILD="1")
+        procs.append(subprocess.Popen([sys.executable, me] + list(argv), env=env, cwd=REPO,
+                                      stdout=out0 if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    live = list(procs)
+    while live:
+        time.sleep(0.2)
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 128 - c
+                print("bench: rank %d exited with %d; stopping the other ranks" % (procs.index(p), c),
+                      file=sys.stderr)
+                for q in live:
+                    q.send_signal(signal.SIGTERM)
+    out0.seek(0)
+    text = out0.read()
+    lines = [ln for ln in text.splitlines() if ln.strip().startswith("{")]
+    if rc == 0 and not lines:
+        print("bench: rank 0 printed no JSON line", file=sys.stderr)
+        rc = 1
+    if lines:
+        print(lines[-1])
+    sys.stdout.flush()
+    return rc
+
+
+def dry_run(args):
+    """--dry-run: the launch and reduction logic of a multi-rank run with no GPU work (gloo)."""
+    from dropout_hamiltonian_montecarlo_amd import parallel
+    rank, world, local = parallel.init("gloo")
+    try:
+        t = parallel.allreduce_max(0.001 * (rank + 1))
+        lf = parallel.allreduce_sum(10.0 * (rank + 1))
+        env = {k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+        envs = parallel.gather_objects(env)
+        if rank == 0:
+            print(json.dumps({"metric": "dry-run", "value": lf / t, "n_gpus": world, "steps": args.steps,
+                              "warmup": args.warmup, "leapfrogs": lf, "t_max": t, "rank_env": envs,
+                              "config": {"chains": world, "local_rank_devices": [e["LOCAL_RANK"] for e in envs]}}))
+    finally:
+        parallel.finalize()
 
 
 def synthetic_data(seed=0):
@@ -74,6 +146,12 @@ def cpu_model():
     return "unknown"
 
 
+def blas_threads():
+    import threadpoolctl
+    blas = [i for i in threadpoolctl.threadpool_info() if i.get("user_api") == "blas"]
+    return int(max((i.get("num_threads", 1) for i in blas), default=1))
+
+
 def cpu_baseline(X, Y, budget_s, threads=None):
     """The oracle (NumPy float64 restatement of the reference SGHMC, bit-exact to it) on host
     cores: bounded sample of the same workload, leapfrogs counted the same way.  threads=None:
@@ -88,9 +166,7 @@ def cpu_baseline(X, Y, budget_s, threads=None):
 
 def _cpu_baseline(X, Y, budget_s):
     from oracle import models as om, samplers as osm
-    import threadpoolctl
-    blas = [i for i in threadpoolctl.threadpool_info() if i.get("user_api") == "blas"]
-    threads = max((i.get("num_threads", 1) for i in blas), default=1)
+    threads = blas_threads()
     nb = 10
     Xs, Ys = X[:nb * B], Y[:nb * B]
     lf, t_total, steps = 0.0, 0.0, 0
@@ -168,11 +244,10 @@ MLP_P = 256 * 784 + 256 + 256 * 256 + 256 + 10 * 256 + 10          # 269,322
 MLP_FLOP_PER_LEAPFROG = 1.0193e9             # SURVEY §8d "M": minimal-recompute schedule, B = 500
 
 
-def mlp_measure(X, lab, n_steps, rank, cpu_seconds):
+def mlp_measure(X, lab, n_steps, rank):
     """Secondary measurement, BASELINE config 3: MNIST MLP 784-256-256-10 SGHMC, batch 500, one
     chain, float32 (Chainer's default dtype), device Philox noise and dropout masks, through the
-    fused hmcx_mlp_sghmc_run.  CPU baseline: the oracle's mlp.grad (NumPy float32) six times
-    per leapfrog — the reference's per-sub-step full gradient (sghmc.py:29-34)."""
+    fused hmcx_mlp_sghmc_run."""
     import torch
     from dropout_hamiltonian_montecarlo_amd.hamiltonian.models.gpu.mlp import mlp
     from dropout_hamiltonian_montecarlo_amd.hamiltonian.inference.gpu.sghmc import sghmc
@@ -205,26 +280,27 @@ def mlp_measure(X, lab, n_steps, rank, cpu_seconds):
                         "frac": achieved / MFMA_PEAK_TFLOPS["f32"], "device_ms": kms,
                         "kernel": "all kernels of one hmcx_mlp_sghmc_run call (k_mm GEMMs + step kernels)",
                         "flop_per_leapfrog": MLP_FLOP_PER_LEAPFROG}}
-    if cpu_seconds > 0:
-        from oracle import models as om
-        rs = np.random.RandomState(0)
-        ref = om.mlp({"alpha": ALPHA}, *MLP_SHAPE)
-        par = {k: v.astype(np.float32) for k, v in m.init_params(1).items()}
-        Xb, yb = X[:B].astype(np.float32), lab[:B]
-        calls, t0 = 0, time.perf_counter()
-        while time.perf_counter() - t0 < cpu_seconds:
-            ref.grad(par, masks=om.dropout_masks(rs, B, MLP_SHAPE[1]), X_train=Xb, y_train=yb)
-            calls += 1
-        dtc = time.perf_counter() - t0
-        lfc = calls / 6.0 / dtc
-        import threadpoolctl
-        blas = [i for i in threadpoolctl.threadpool_info() if i.get("user_api") == "blas"]
-        out["cpu_baseline"] = {"value": lfc * MLP_P, "unit": "leapfrog-steps/s x param-dim",
-                               "cores": int(max((i.get("num_threads", 1) for i in blas), default=1)), "kind": "port",
-                               "sample": "%d oracle mlp.grad calls (NumPy f32, B=500, fresh dropout masks), "
-                                         "6 per leapfrog, %.1f s" % (calls, dtc),
-                               "leapfrogs_per_s": lfc}
     return out
+
+
+def mlp_cpu_baseline(X, lab, cpu_seconds):
+    """CPU baseline of config 3: the oracle's mlp.grad (NumPy float32) six times per leapfrog — the
+    reference's per-sub-step full gradient (sghmc.py:29-34), fresh dropout masks per call."""
+    from oracle import models as om
+    from dropout_hamiltonian_montecarlo_amd.hamiltonian.models.gpu.mlp import init_params
+    rs = np.random.RandomState(0)
+    ref = om.mlp({"alpha": ALPHA}, *MLP_SHAPE)
+    par = {k: v.astype(np.float32) for k, v in init_params(MLP_SHAPE, 1).items()}
+    Xb, yb = X[:B].astype(np.float32), lab[:B]
+    calls, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < cpu_seconds:
+        ref.grad(par, masks=om.dropout_masks(rs, B, MLP_SHAPE[1]), X_train=Xb, y_train=yb)
+        calls += 1
+    dtc = time.perf_counter() - t0
+    lfc = calls / 6.0 / dtc
+    return {"value": lfc * MLP_P, "unit": "leapfrog-steps/s x param-dim", "cores": blas_threads(), "kind": "port",
+            "sample": "%d oracle mlp.grad calls (NumPy f32, B=500, fresh dropout masks), 6 per leapfrog, %.1f s"
+                      % (calls, dtc), "leapfrogs_per_s": lfc}
 
 
 V_D, V_K, V_N = 2048, 38, 20000               # BASELINE config 5 (PlantVillage-like features; SURVEY §8 "V")
@@ -232,16 +308,20 @@ V_P = V_D * V_K + V_K
 V_FLOP_PER_STEP = 4.0 * B * V_D * V_K         # 155.6 MFLOP per SGLD step
 
 
-def plantvillage_measure(n_steps, rank, cpu_seconds):
+def plantvillage_data():
+    return (np.random.RandomState(5).rand(V_N, V_D),
+            np.eye(V_K)[np.random.RandomState(6).randint(0, V_K, V_N)])
+
+
+def plantvillage_measure(n_steps, rank):
     """Secondary measurement, BASELINE config 5: softmax SGLD on conv-feature-like inputs (D=2048,
     K=38, batch 500), one chain per GPU, float64, device Philox noise, through hmcx_sgld_run (the
     wide path, hmcx_wide.hip).  Logging cadence of the reference (log-likelihood every 10
-    minibatches) included.  CPU baseline: the oracle's SGLD on the same shape."""
+    minibatches) included."""
     import torch
     from dropout_hamiltonian_montecarlo_amd.hamiltonian.models.gpu.softmax import softmax
     from dropout_hamiltonian_montecarlo_amd.hamiltonian.inference.gpu.sgld import sgld
-    Xv = np.random.RandomState(5).rand(V_N, V_D)
-    Yv = np.eye(V_K)[np.random.RandomState(6).randint(0, V_K, V_N)]
+    Xv, Yv = plantvillage_data()
     m = softmax({"alpha": ALPHA}, dtype=torch.float64)
     s = sgld(m, {"weights": np.zeros((V_D, V_K)), "bias": np.zeros(V_K)}, step_size=1e-4, noise="philox",
              seed=17, chain=rank)
@@ -268,32 +348,45 @@ def plantvillage_measure(n_steps, rank, cpu_seconds):
                         "frac": tf / MFMA_PEAK_TFLOPS["f64"], "device_ms": kms,
                         "hbm_GBps_X": xbytes * n_steps / (kms * 1e-3) / 1e9,
                         "kernel": "k_wfwd + k_wsoft + k_wgrad per step (+ logging forward every 10th)"}}
-    if cpu_seconds > 0:
-        from oracle import models as om, samplers as osm
-        import threadpoolctl
-        n_cpu = 0
-        t0 = time.perf_counter()
-        while time.perf_counter() - t0 < cpu_seconds:
-            o = osm.sgld(om.softmax({"alpha": ALPHA}), {"weights": np.zeros((V_D, V_K)), "bias": np.zeros(V_K)},
-                         step_size=1e-4, verbose=False)
-            o.out = io.StringIO()
-            np.random.seed(n_cpu)
-            o.sample(epochs=1, burnin=0, batch_size=B, rng=np.random.RandomState(n_cpu),
-                     X_train=Xv[:10 * B], y_train=Yv[:10 * B])
-            n_cpu += 10
-        dtc = time.perf_counter() - t0
-        blas = [i for i in threadpoolctl.threadpool_info() if i.get("user_api") == "blas"]
-        out["cpu_baseline"] = {"value": n_cpu / dtc * V_P, "unit": "leapfrog-steps/s x param-dim",
-                               "cores": int(max((i.get("num_threads", 1) for i in blas), default=1)), "kind": "port",
-                               "sample": "%d oracle SGLD steps (NumPy f64, B=500, D=2048, K=38, logging every 10), %.1f s"
-                                         % (n_cpu, dtc), "leapfrogs_per_s": n_cpu / dtc}
     return out
+
+
+def plantvillage_cpu_baseline(cpu_seconds):
+    """CPU baseline of config 5: the oracle's SGLD on the same shape (logging every 10 minibatches)."""
+    from oracle import models as om, samplers as osm
+    Xv, Yv = plantvillage_data()
+    n_cpu = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < cpu_seconds:
+        o = osm.sgld(om.softmax({"alpha": ALPHA}), {"weights": np.zeros((V_D, V_K)), "bias": np.zeros(V_K)},
+                     step_size=1e-4, verbose=False)
+        o.out = io.StringIO()
+        np.random.seed(n_cpu)
+        o.sample(epochs=1, burnin=0, batch_size=B, rng=np.random.RandomState(n_cpu),
+                 X_train=Xv[:10 * B], y_train=Yv[:10 * B])
+        n_cpu += 10
+    dtc = time.perf_counter() - t0
+    return {"value": n_cpu / dtc * V_P, "unit": "leapfrog-steps/s x param-dim", "cores": blas_threads(), "kind": "port",
+            "sample": "%d oracle SGLD steps (NumPy f64, B=500, D=2048, K=38, logging every 10), %.1f s"
+                      % (n_cpu, dtc), "leapfrogs_per_s": n_cpu / dtc}
 
 
 def main():
     args = parse()
-    import torch
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no launcher: this process starts the N ranks itself and touches no GPU
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if args.dry_run:
+        return dry_run(args)
     from dropout_hamiltonian_montecarlo_amd import parallel
+    try:
+        bench(args, parallel)
+    finally:
+        parallel.finalize()
+
+
+def bench(args, parallel):
+    import torch
     rank, world, local = parallel.init()
     if world != args.gpus and rank == 0:
         print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, world), file=sys.stderr)
@@ -405,14 +498,15 @@ def main():
     mlp_out = None
     if args.mlp_steps > 0:
         lab = np.argmax(Y, axis=1)
-        mlp_out = mlp_measure(X, lab, args.mlp_steps, rank, args.cpu_seconds if world == 1 and rank == 0 else 0)
+        mlp_out = mlp_measure(X, lab, args.mlp_steps, rank)
         parallel.barrier()
     v_out = None
     if args.sgld_steps > 0:
-        v_out = plantvillage_measure(args.sgld_steps, rank, args.cpu_seconds if world == 1 and rank == 0 else 0)
+        v_out = plantvillage_measure(args.sgld_steps, rank)
         parallel.barrier()
+    parallel.barrier()
     if rank != 0:
-        return
+        return                        # main() tears the process group down on every rank
     path = "persistent" if (args.path != "kernels") else "kernels"
     assert kern_n == n_calls, (kern_n, n_calls)
     launch_ms = kern_ms / kern_n
@@ -457,12 +551,16 @@ def main():
         "mlp": mlp_out,
         "plantvillage_sgld": v_out,
     }
-    if world == 1 and args.cpu_seconds > 0:
+    if args.cpu_seconds > 0:
+        # rank 0, after every rank's GPU work (the barrier above): the oracle on host cores
         out["cpu_baseline"] = cpu_baseline(X, Y, args.cpu_seconds)
         out["cpu_baseline_1thread"] = cpu_baseline(X, Y, args.cpu_seconds, threads=1)
+        if mlp_out is not None:
+            mlp_out["cpu_baseline"] = mlp_cpu_baseline(X, np.argmax(Y, axis=1), args.cpu_seconds)
+        if v_out is not None:
+            v_out["cpu_baseline"] = plantvillage_cpu_baseline(args.cpu_seconds)
     print(json.dumps(out))
-    if parallel.dist.is_initialized():
-        parallel.dist.destroy_process_group()
+    sys.stdout.flush()
 
 
 if __name__ == "__main__":

@@ -31,6 +31,18 @@ def mlp_param_shapes(n_in, n_mid, n_out):
             '/l3/W': (n_out, n_mid), '/l3/b': (n_out,)}
 
 
+def init_params(shape, seed=0):
+    """Chainer L.Linear defaults for MyNetwork(n_in, n_mid, n_out): W ~ LeCunNormal (N(0, 1/fan_in)),
+    b = 0 (host numpy, float64).  Needs no device."""
+    shapes = mlp_param_shapes(*shape)
+    rs = np.random.RandomState(seed)
+    out = {}
+    for k in MLP_PARAM_NAMES:
+        shp = shapes[k]
+        out[k] = rs.normal(0, 1.0 / np.sqrt(shp[1]), shp) if len(shp) == 2 else np.zeros(shp)
+    return out
+
+
 class mlp:
     _hmcx_model = 'mlp'
 
@@ -49,12 +61,7 @@ class mlp:
     # -------------------------------------------------------------- helpers
     def init_params(self, seed=0):
         """Chainer L.Linear defaults: W ~ LeCunNormal (N(0, 1/fan_in)), b = 0 (host numpy, float64)."""
-        rs = np.random.RandomState(seed)
-        out = {}
-        for k in MLP_PARAM_NAMES:
-            shp = self.shapes[k]
-            out[k] = rs.normal(0, 1.0 / np.sqrt(shp[1]), shp) if len(shp) == 2 else np.zeros(shp)
-        return out
+        return init_params((self.n_in, self.n_mid, self.n_out), seed)
 
     def _dev(self, a):
         return as_device(a, self.dtype, self.device)

@@ -44,6 +44,13 @@ def init(backend=None):
     return rank, world, local
 
 
+def finalize():
+    """Tear down the process group on every rank (each rank calls this, also when it has nothing
+    to report)."""
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
 def backend_name():
     if not dist.is_initialized():
         return "none"
@@ -95,17 +102,36 @@ def allreduce_sum(x, device=None):
     return float(t.item())
 
 
+def gather_objects(obj):
+    """All-gather one small picklable object per rank (list ordered by rank)."""
+    if not dist.is_initialized():
+        return [obj]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, obj)
+    return out
+
+
 def gather_traces(local_traces, device=None):
-    """All-gather per-chain traces.  local_traces: array [c_local, T, P] (same c_local, T, P on
-    every rank) → array [world·c_local, T, P] ordered by (rank, local chain)."""
+    """All-gather per-chain traces.  local_traces: array [c_local, T, P] (same T, P on every rank;
+    c_local may differ, as chain_block gives the first n % world ranks one chain more) → array
+    [Σ c_local, T, P] ordered by (rank, local chain).  Uneven blocks are padded to the largest
+    c_local for the one all_gather (equal shapes on every rank) and the padding is dropped."""
     x = torch.as_tensor(np.ascontiguousarray(local_traces), dtype=torch.float64)
     if not dist.is_initialized():
         return x.numpy()
     device = _dev(device)
+    world = dist.get_world_size()
+    counts = torch.tensor([x.shape[0]], dtype=torch.int64, device=device)
+    allc = [torch.empty_like(counts) for _ in range(world)]
+    dist.all_gather(allc, counts)
+    allc = [int(c.item()) for c in allc]
+    cmax = max(allc)
+    if x.shape[0] < cmax:
+        x = torch.cat([x, x.new_zeros((cmax - x.shape[0],) + tuple(x.shape[1:]))], dim=0)
     x = x.to(device) if device is not None else x
-    out = [torch.empty_like(x) for _ in range(dist.get_world_size())]
+    out = [torch.empty_like(x) for _ in range(world)]
     dist.all_gather(out, x)
-    return torch.cat(out, dim=0).cpu().numpy()
+    return torch.cat([o[:c] for o, c in zip(out, allc)], dim=0).cpu().numpy()
 
 
 class Welford:
@@ -137,7 +163,7 @@ class Welford:
 
 def gather_summaries(welford, trace, device=None):
     """All-gather the per-chain summaries of this rank (Welford over [c_local, P], thinned trace
-    [c_local, T, P]; the same c_local, T, P on every rank) in ONE collective: returns
+    [c_local, T, P]; the same T, P on every rank, c_local may differ) in one data collective: returns
     (n, mean [C, P], M2 [C, P], trace [C, T, P]) over all C chains, ordered by rank."""
     c, P = welford.mean.shape
     trace = np.asarray(trace, dtype=np.float64).reshape(c, -1, P)

@@ -38,3 +38,19 @@ def test_bench_world1_through_rccl():
     pp = diag["per_parameter"]
     assert pp["chains"] == 1 and pp["params"] == 7850
     assert 0.5 < pp["rhat"]["median"] < 2.0
+
+
+def test_bench_self_launch_two_ranks_shared_gpu():
+    """bench.py --gpus 2 without a launcher starts its own two ranks; on the
+    one-GPU box both share cuda:0 (HMCX_BENCH_SHARED_GPU) and reduce over gloo."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(HMCX_BENCH_SHARED_GPU="1", HMCX_DIST_BACKEND="gloo")
+    cmd = [sys.executable, "bench.py", "--gpus", "2", "--steps", "5", "--warmup", "2", "--cpu-seconds", "0",
+           "--batched-chains", "0", "--mlp-steps", "0", "--sgld-steps", "0"]
+    r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["config"]["chains"] == 2 and line["value"] > 0
+    assert line["diagnostics"]["per_parameter"]["chains"] == 2

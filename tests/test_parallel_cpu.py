@@ -94,7 +94,19 @@ np.testing.assert_allclose(parallel.rhat_from_moments(n, means, M2),
 np.testing.assert_allclose(parallel.diagnostics.split_rhat(tr), parallel.diagnostics.split_rhat(allt[:, ::4]))
 s = parallel.summary_diagnostics(n, means, M2, tr)
 assert s["chains"] == 2 * world and s["params"] == 3 and s["rhat"]["min"] > 1.0
+# uneven blocks (chain_block(5, r, 2) = 3 + 2 chains): padded for the gather, padding dropped
+c0, c = parallel.chain_block(5, rank, world)
+mine = np.stack([np.full((4, 3), float(i)) for i in range(c0, c0 + c)])
+allu = parallel.gather_traces(mine)
+assert allu.shape == (5, 4, 3), allu.shape
+np.testing.assert_array_equal(allu[:, 0, 0], np.arange(5.0))
+wu = parallel.Welford((c, 3)).update(mine)
+n, means, M2, tr = parallel.gather_summaries(wu, mine[:, ::2])
+assert means.shape == (5, 3) and tr.shape == (5, 2, 3)
+np.testing.assert_array_equal(means[:, 0], np.arange(5.0))
+assert parallel.gather_objects(rank) == list(range(world))
 parallel.barrier()
+parallel.finalize()
 print("ok", rank)
 '''
 
