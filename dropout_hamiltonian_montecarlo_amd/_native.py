@@ -62,7 +62,7 @@ class MlpSghmcArgs(ctypes.Structure):
                 ("mask_mode", c_int), ("masks", c_void_p), ("mask_off", c_i64p),
                 ("seed", ctypes.c_uint64), ("chain", ctypes.c_uint32), ("step_base", ctypes.c_uint32),
                 ("par", MlpParams), ("out_A", c_void_p), ("out_accepted", c_void_p),
-                ("out_loss", c_void_p), ("out_nlp", c_void_p), ("out_E", c_void_p)]
+                ("out_loss", c_void_p), ("out_nlp", c_void_p), ("out_E", c_void_p), ("out_abort", c_void_p)]
 
 
 class SgdArgs(ctypes.Structure):
@@ -96,7 +96,7 @@ EXPORTS = ("hmcx_version", "hmcx_create", "hmcx_destroy", "hmcx_last_error", "hm
            "hmcx_sgld_run", "hmcx_hmc_mvn_run", "hmcx_mlp_masks", "hmcx_mlp_grad", "hmcx_mlp_loss",
            "hmcx_mlp_sghmc_run", "hmcx_logistic_grad", "hmcx_logistic_loglik", "hmcx_logistic_predict",
            "hmcx_sumsq", "hmcx_sgd_run", "hmcx_hmc_run", "hmcx_axpy", "hmcx_mvn_eval",
-           "hmcx_clear_abort", "hmcx_philox_schedule", "hmcx_host_wait")
+           "hmcx_clear_abort", "hmcx_philox_schedule", "hmcx_host_wait", "hmcx_set_mlp_fuse")
 
 _lib = None
 _lock = threading.Lock()
@@ -156,6 +156,7 @@ def load_library():
         lib.hmcx_mlp_loss.argtypes = [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                                       ctypes.POINTER(MlpParams), c_void_p, c_void_p, c_void_p]
         lib.hmcx_mlp_sghmc_run.argtypes = [c_void_p, ctypes.POINTER(MlpSghmcArgs)]
+        lib.hmcx_set_mlp_fuse.argtypes = [c_void_p, c_int]
         lib.hmcx_logistic_grad.argtypes = [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
                                            c_void_p, c_void_p, c_double, c_void_p, c_void_p]
         lib.hmcx_logistic_loglik.argtypes = [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
@@ -215,6 +216,13 @@ class Context:
     def clear_abort(self):
         """Lower the context's persistent-launch abort word (include/hmcx.h hmcx_clear_abort)."""
         self.check(self.lib.hmcx_clear_abort(self.h), "hmcx_clear_abort")
+
+    mlp_fuse = True
+
+    def set_mlp_fuse(self, on):
+        """Fused layer-2/3 MLP launches in the sampler (include/hmcx.h hmcx_set_mlp_fuse)."""
+        self.check(self.lib.hmcx_set_mlp_fuse(self.h, 1 if on else 0), "hmcx_set_mlp_fuse")
+        self.mlp_fuse = bool(on)
 
     def set_timing(self, on):
         """Bracket every sampler run's kernels with HIP events on the launch stream (resets totals)."""

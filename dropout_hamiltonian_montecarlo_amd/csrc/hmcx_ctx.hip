@@ -509,6 +509,7 @@ int hmcx_destroy(hmcx_ctx* ctx) {
   for (auto e : ctx->host_mark_pool) (void)hipEventDestroy(e);
   if (ctx->abort_host) (void)hipHostFree(ctx->abort_host);
   if (ctx->abort_dev) (void)hipFree(ctx->abort_dev);
+  if (ctx->mlp_abort_dev) (void)hipFree(ctx->mlp_abort_dev);
   if (ctx->zeros_dev) (void)hipFree(ctx->zeros_dev);
   if (ctx->gx_arena) (void)hipFree(ctx->gx_arena);
   for (auto& g : ctx->graveyard) {
@@ -547,6 +548,12 @@ int hmcx_set_sghmc_path(hmcx_ctx* ctx, int path) {
   if (path < 0 || path > 3)
     return set_error(ctx, HMCX_EINVAL, "path must be 0 (auto), 1 (kernels), 2 (persistent 2-D), 3 (row space)");
   ctx->sghmc_path = path;
+  return HMCX_OK;
+}
+
+int hmcx_set_mlp_fuse(hmcx_ctx* ctx, int on) {
+  HMCX_GUARD_CTX(ctx);
+  ctx->mlp_nofuse = on ? 0 : 1;
   return HMCX_OK;
 }
 

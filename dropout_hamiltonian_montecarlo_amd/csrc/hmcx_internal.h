@@ -59,6 +59,9 @@ struct hmcx_ctx {
   std::vector<std::pair<const void*, hipEvent_t>> host_marks;   // out_host block -> its latest copy's event
   std::vector<hipEvent_t> host_mark_pool;                        // spare events for new out_host blocks
   unsigned abort_next = 0;
+  // fused MLP launches (hmcx_mlp.hip MM_L23): their own abort word, reported per call (out_abort)
+  int* mlp_abort_dev = nullptr;
+  int mlp_nofuse = 0;                  // hmcx_set_mlp_fuse(ctx, 0): the sampler runs unfused
 };
 constexpr int ABORT_SLOTS = 64;
 

@@ -172,7 +172,10 @@ template <typename T> struct MMArgs {
   // workgroups of one row block meet in a tagged-granule arena (see k_mm)
   char* gx; int gx_bytes; unsigned ep; int* abort_flag;
   int N3; const T* bias3; T* gz;     // n_out, b3 and the gz output of the fused layer 3
+  int force_abort;                   // test knob (HMCX_MLP_FORCE_ABORT): raise the abort word, skip the publish
+  unsigned long long* prof;          // HMCX_MLP_PROF: per-workgroup s_memrealtime stamps of the MM_L23 phases
 };
+constexpr int L23_NPH = 8;           // stamps per workgroup and launch (prof)
 
 template <typename T, int OP>
 __device__ inline T op_apply(T x, T mask, T bias) {
@@ -436,10 +439,38 @@ __global__ __launch_bounds__(MM_NT) void k_mm(MMArgs<T> a) {
   using M = mfma16<T>;
   __shared__ T red[MM_NW][32][33];
   __shared__ double rowl[32];
-  run_pending(a.pend);
+  // MM_L23 runs the pending update while its logit partials travel (below); nothing in this launch
+  // reads what it writes (the momentum and the NEXT iteration's position buffer of another variable)
+  if constexpr (EPI != MM_L23) run_pending(a.pend);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lg = lane >> 4;
   // MM_L3CE: blockIdx.y is the n_mid column slice of the layer-3 backward (N = n_out ≤ 32: one tile)
   const int m0 = blockIdx.x * 32, n0 = EPI == MM_L3CE ? 0 : blockIdx.y * 32;
+  const int pbid = blockIdx.y * gridDim.x + blockIdx.x;
+  auto stamp = [&](int ph) {
+    if constexpr (EPI == MM_L23)
+      if (a.prof && tid == 0) a.prof[(size_t)pbid * L23_NPH + ph] = __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
+  // MM_L23: every operand of the epilogue and of layer 3 that does not depend on the GEMM (dropout
+  // masks m1 / m2 and b2 of the two tile elements a thread finishes, the slice's W3 columns, b3) is
+  // loaded before the GEMM's own operands, so the epilogue never waits on memory
+  MRaw<T> pm1[2], pm2[2];
+  T pb2v[2], pw3v[2], pb3v = T(0);
+  if constexpr (EPI == MM_L23) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = tid + MM_NT * u, mm = e >> 5, nn = e & 31, m = m0 + mm, n = n0 + nn;
+      const bool ok = m < a.M && n < a.N;
+      const size_t i = ok ? (size_t)m * a.ldc + n : 0;
+      pm1[u] = mraw(a.ms, 1, i);
+      pm2[u] = mraw(a.ms, 2, i);
+      pb2v[u] = a.bias[ok ? n : 0];
+      const int o = e >> 5, c = e & 31;
+      const bool okw = o < a.N3 && n0 + c < a.N;
+      pw3v[u] = a.W3[okw ? (size_t)o * a.n_mid + n0 + c : 0];
+    }
+    pb3v = a.bias3[tid < a.N3 ? tid : 0];
+  }
   const int Kq = ((a.K + 16 * MM_NW - 1) / (16 * MM_NW)) * 16;   // k range per wave (multiple of 16)
   const int kb = wave * Kq, ke = min(a.K, kb + Kq);
   typename M::acc_t acc[2][2];
@@ -503,15 +534,19 @@ __global__ __launch_bounds__(MM_NT) void k_mm(MMArgs<T> a) {
       red[0][mm][nn] = g;
     } else if constexpr (EPI == MM_L23) {                      // mlp.py:30-31; the tile stays in LDS
       T d = T(0), h = T(0), m1 = T(0), m2 = T(0);
+      mpin(pm1[u]);
+      mpin(pm2[u]);
       if (m < a.M && n < a.N) {
-        const size_t i = (size_t)m * a.ldc + n;
-        m1 = mval(a.ms, 1, i);
-        m2 = mval(a.ms, 2, i);
-        const T t = (v + a.bias[n]) * m1;
+        m1 = mfin(a.ms, pm1[u]);
+        m2 = mfin(a.ms, pm2[u]);
+        const T t = (v + pb2v[u]) * m1;
         h = t > T(0) ? t : T(0);
-        a.C[i] = h;
         d = h * m2;
-        a.C2[i] = d;
+        if (a.C) {                                              // h2 / d3 are dead in the fused sampler
+          const size_t i = (size_t)m * a.ldc + n;
+          a.C[i] = h;
+          a.C2[i] = d;
+        }
       }
       // planes of this element only (each (mm, nn) has one thread): d3, h2, m1, m2 of the tile
       red[0][mm][nn] = d;
@@ -540,37 +575,47 @@ __global__ __launch_bounds__(MM_NT) void k_mm(MMArgs<T> a) {
     // hmcx_persist2.hip — then runs the cross-entropy of the block (slice 0 writes loss and gz) and
     // the layer-3 backward of its own columns.  The epoch is new per launch and the arena only ever
     // holds granules of earlier launches, so no stale value can match.
-    __syncthreads();                                             // the reduction has read every red[w]
     const int No = a.N3, S = gridDim.y, s = blockIdx.y, rb = blockIdx.x;
     T* d3t = &red[0][0][0];                                      // [32][33] d3 of the tile
     T* w3s = &red[1][0][0];                                      // [n_out][32] W3 columns of the slice
     T* zt = &red[2][0][0];                                       // [32][33] logits, then gz
-    for (int e = tid; e < No * 32; e += MM_NT) {
-      const int o = e >> 5, c = e & 31;
-      w3s[e] = n0 + c < a.N ? a.W3[(size_t)o * a.n_mid + n0 + c] : T(0);
+    T* b3s = &red[7][0][0];                                      // [n_out] b3
+    __syncthreads();                                             // the reduction has read every red[w]
+    stamp(1);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = tid + MM_NT * u;
+      if (e < No * 32) w3s[e] = n0 + (e & 31) < a.N ? pw3v[u] : T(0);  // prefetched; zero past n_mid
     }
+    if (tid < No) b3s[tid] = pb3v;
     __syncthreads();
     const __amdgpu_buffer_rsrc_t rs = gx_rsrc(a.gx, a.gx_bytes);
     const int items = 32 * No;
     const int base_rb = rb * S * items;
-    if (tid < items) {
+    if (a.force_abort && pbid == 0 && tid == 0)                  // test knob: this launch never completes
+      __hip_atomic_store(a.abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid < items && !(a.force_abort && pbid == 0)) {
       const int r = tid / No, o = tid - r * No;
       T zp = T(0);
 #pragma unroll 8
       for (int c = 0; c < 32; ++c) zp += d3t[r * 33 + c] * w3s[o * 32 + c];
       gx_put(rs, base_rb + s * items + tid, (double)zp, a.ep);
     }
-    bool ok = true;
+    stamp(2);
+    run_pending(a.pend);                                         // while the partials travel
+    stamp(3);
     if (tid < items) {
       const int r = tid / No, o = tid - r * No;
       double sum = 0.0;
-      ok = gx_poll_sum(rs, base_rb + tid, items, S, a.ep, a.abort_flag, &sum);
-      zt[r * 33 + o] = (m0 + r < a.M) ? (T)sum + a.bias3[o] : T(0);
+      (void)gx_poll_sum(rs, base_rb + tid, items, S, a.ep, a.abort_flag, &sum);   // a timeout raises the
+      zt[r * 33 + o] = (m0 + r < a.M) ? (T)sum + b3s[o] : T(0);                   // MLP abort word
     }
     __syncthreads();
+    stamp(4);
     const bool first = s == 0;
     ce_rows<T>(zt, 33, rowl, m0, a.M, No, a.y, a.gz, No, a.lpart, rb, first);
     __syncthreads();
+    stamp(5);
     // layer-3 backward of the slice's columns, all operands in LDS (gz in zt, W3 slice in w3s, the
     // tile's h2 / d3 / masks): ga2 = ((gz·W3)·m2)·[h2 > 0]·m1 and its column sums (b2 partial),
     // gzᵀ·d3 (W3 partial), column sums of gz (b3 partial, slice 0)
@@ -606,7 +651,7 @@ __global__ __launch_bounds__(MM_NT) void k_mm(MMArgs<T> a) {
       for (int r = 0; r < rows; ++r) cs += zt[r * 33 + tid];
       a.pb3[(size_t)rb * No + tid] = cs;
     }
-    (void)ok;
+    stamp(6);
   }
   if constexpr (EPI == MM_GA1) {
     if (a.colpart) {
@@ -811,6 +856,9 @@ struct MlpNet {
   Pending<T> pend{};                     // consumed by the next launch
   // fused layer 2 + layer 3 (MM_L23): granule arena and epoch counter of the context
   char* gx = nullptr; int gx_bytes = 0; hmcx_ctx* ctx = nullptr; int* abort_flag = nullptr; bool fuse = false;
+  int force_abort = -1, l23_count = 0;   // HMCX_MLP_FORCE_ABORT: the fused launch (0-based, per call) that aborts
+  unsigned long long* prof = nullptr;    // HMCX_MLP_PROF: stamps of every fused launch of the call
+  int prof_cap = 0;
   int nvar(int v) const {
     switch (v) {
       case 0: return n_mid * n_in;  case 1: return n_mid;
@@ -879,7 +927,12 @@ hipError_t mlp_forward(MlpNet<T>& net, T* const* q, const MaskSrc<T>& ms, double
     a.pb2 = w.pb2 ? net.pb2 : nullptr;
     a.pb3 = w.pb3 ? net.pb3 : nullptr;
     a.pw3 = w.pw3 ? net.pw3 : nullptr;
+    a.C = nullptr; a.C2 = nullptr;                             // h2 / d3 stay in LDS
     a.gx = net.gx; a.gx_bytes = net.gx_bytes; a.ep = gx_next_epoch(net.ctx); a.abort_flag = net.abort_flag;
+    a.force_abort = net.l23_count == net.force_abort;
+    if (net.prof && net.l23_count < net.prof_cap)
+      a.prof = net.prof + (size_t)net.l23_count * net.nlb * ((nm + 31) / 32) * L23_NPH;
+    ++net.l23_count;
     return mm<T, MM_L23, 0, 1, OP_H1>(net, a);
   }
   {                                                           // h2, d3 from h1 = max((xw + b1)·m0, 0)
@@ -963,13 +1016,15 @@ hipError_t flush_pending(MlpNet<T>& net) {
   return hipGetLastError();
 }
 
-// Fused layer 2 + layer 3 (MM_L23) when n_out ≤ 32, at most 16 column slices, and the whole grid
-// fits on the chip at once (its slice workgroups wait for each other); HMCX_MLP_FUSE=0 turns it off.
+// Fused layer 2 + layer 3 (MM_L23) in the sampler when n_out ≤ 32, at most 16 column slices, and the
+// whole grid fits on the chip at once (its slice workgroups wait for each other); HMCX_MLP_FUSE=0 or
+// hmcx_set_mlp_fuse(ctx, 0) turns it off.  A timed-out exchange raises the MLP's own abort word
+// (ctx->mlp_abort_dev, never the persistent SGHMC kernels' word) and the call reports it (out_abort).
 template <typename T>
 int net_fuse(hmcx_ctx* ctx, MlpNet<T>& net) {
   static const bool off = getenv("HMCX_MLP_FUSE") && getenv("HMCX_MLP_FUSE")[0] == '0';
   const int S = (net.n_mid + 31) / 32;
-  if (off || net.n_out > 32 || S > 16) return HMCX_OK;
+  if (off || ctx->mlp_nofuse || net.n_out > 32 || S > 16) return HMCX_OK;
   int per_cu = 0;
   const void* kfn = (const void*)k_mm<T, MM_L23, OP_H1, OP_PLAIN, 0, 1, 1, 1>;
   HMCX_HIP(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, MM_NT, 0));
@@ -977,11 +1032,17 @@ int net_fuse(hmcx_ctx* ctx, MlpNet<T>& net) {
   const size_t need = (size_t)net.nlb * S * 32 * net.n_out * 16;
   if (need > 0x7fffffff) return HMCX_OK;
   if (int rc = gx_reserve(ctx, need)) return rc;
+  if (!ctx->mlp_abort_dev) {
+    HMCX_HIP(ctx, hipMalloc((void**)&ctx->mlp_abort_dev, sizeof(int)));
+    HMCX_HIP(ctx, hipMemsetAsync(ctx->mlp_abort_dev, 0, sizeof(int), ctx->stream));
+  }
   net.gx = ctx->gx_arena;
   net.gx_bytes = (int)ctx->gx_bytes;
   net.ctx = ctx;
-  net.abort_flag = ctx->abort_dev;
+  net.abort_flag = ctx->mlp_abort_dev;
   net.fuse = true;
+  const char* fa = getenv("HMCX_MLP_FORCE_ABORT");
+  net.force_abort = fa ? atoi(fa) : -1;
   return HMCX_OK;
 }
 
@@ -1014,8 +1075,7 @@ int mlp_grad_t(hmcx_ctx* ctx, const void* X, const int32_t* y, int B, int n_in, 
                const hmcx_mlp_params* par, const void* masks, double alpha, hmcx_mlp_params* grads, double* loss) {
   MlpNet<T> net{};
   net_init(net, B, n_in, n_mid, n_out, ctx->stream);
-  net.X = (const T*)X; net.y = y;
-  if (int rc = net_fuse<T>(ctx, net)) return rc;
+  net.X = (const T*)X; net.y = y;          // one-off calls run unfused: no exchange that could time out
   Workspace ws(ctx);
   double* lpart;
   do { ws.reset(); mlp_workspace<T>(ws, net); lpart = ws.take<double>(net.nlb); } while (ws.retry());
@@ -1049,8 +1109,7 @@ int mlp_loss_t(hmcx_ctx* ctx, const void* X, const int32_t* y, int B, int n_in, 
                const hmcx_mlp_params* par, const void* masks, double* loss, void* logits) {
   MlpNet<T> net{};
   net_init(net, B, n_in, n_mid, n_out, ctx->stream);
-  net.X = (const T*)X; net.y = y;
-  if (int rc = net_fuse<T>(ctx, net)) return rc;
+  net.X = (const T*)X; net.y = y;          // unfused (see mlp_grad_t)
   Workspace ws(ctx);
   double* lpart;
   do { ws.reset(); mlp_workspace<T>(ws, net); lpart = ws.take<double>(net.nlb); } while (ws.retry());
@@ -1109,9 +1168,14 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
   double *part_cur, *part_new, *lp_cur, *lp_new, *lp_scr;
   uint8_t* keep = nullptr;
   int32_t* accf;
+  static const char* prof_path = getenv("HMCX_MLP_PROF");
+  const int prof_cap = prof_path && net.fuse ? 8192 : 0;
   do {
     ws.reset();
     mlp_workspace<T>(ws, net);
+    net.prof = prof_cap ? ws.take<unsigned long long>((size_t)prof_cap * net.nlb * ((net.n_mid + 31) / 32) * L23_NPH)
+                        : nullptr;
+    net.prof_cap = prof_cap;
     for (int v = 0; v < 6; ++v) { pv[v] = ws.take<T>(dim[v]); qa[v] = ws.take<T>(dim[v]); qb[v] = ws.take<T>(dim[v]); }
     part_cur = ws.take<double>(12 * NPART);
     part_new = ws.take<double>(12 * NPART);
@@ -1208,7 +1272,37 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
   }
   if ((rc = gs.finish())) return rc;
   if ((rc = timing_end(ctx, ctx->stream))) return rc;
-  return net.fuse ? abort_defer(ctx, ctx->abort_dev, ctx->stream) : HMCX_OK;   // a timed-out exchange
+  if (net.prof) {                                            // HMCX_MLP_PROF=<file>: append the stamps
+    HMCX_HIP(ctx, hipStreamSynchronize(st));
+    const size_t n = (size_t)std::min(net.l23_count, net.prof_cap) * net.nlb * ((net.n_mid + 31) / 32) * L23_NPH;
+    std::vector<unsigned long long> h(n);
+    HMCX_HIP(ctx, hipMemcpy(h.data(), net.prof, n * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    if (FILE* f = fopen(getenv("HMCX_MLP_PROF"), "ab")) {
+      const int hdr[4] = {std::min(net.l23_count, net.prof_cap), net.nlb, (net.n_mid + 31) / 32, L23_NPH};
+      fwrite(hdr, sizeof(int), 4, f);
+      fwrite(h.data(), sizeof(unsigned long long), n, f);
+      fclose(f);
+    }
+  }
+  if (!net.fuse) {
+    if (s->out_abort) HMCX_HIP(ctx, hipMemsetAsync(s->out_abort, 0, sizeof(int32_t), st));
+    return HMCX_OK;
+  }
+  // the call's verdict: the MLP abort word (raised by a timed-out exchange of any fused launch of this
+  // call) goes to out_abort and is lowered for the next call — the call's outputs and state are then
+  // invalid and the caller re-runs it unfused (sghmc._run_mlp); without out_abort, wait and report
+  if (s->out_abort) {
+    HMCX_HIP(ctx, hipMemcpyAsync(s->out_abort, ctx->mlp_abort_dev, sizeof(int32_t), hipMemcpyDeviceToDevice, st));
+    HMCX_HIP(ctx, hipMemsetAsync(ctx->mlp_abort_dev, 0, sizeof(int), st));
+    return HMCX_OK;
+  }
+  int flag = 0;
+  HMCX_HIP(ctx, hipMemcpyAsync(&flag, ctx->mlp_abort_dev, sizeof(int), hipMemcpyDeviceToHost, st));
+  HMCX_HIP(ctx, hipMemsetAsync(ctx->mlp_abort_dev, 0, sizeof(int), st));
+  HMCX_HIP(ctx, hipStreamSynchronize(st));
+  if (flag) return set_error(ctx, HMCX_EHIP, "mlp sghmc: fused layer-2/3 exchange timed out; state is invalid "
+                                             "(re-run with hmcx_set_mlp_fuse(ctx, 0))");
+  return HMCX_OK;
 }
 
 template int mlp_masks_t<float>(hmcx_ctx*, int, int, uint64_t, uint32_t, uint32_t, uint32_t, void*);

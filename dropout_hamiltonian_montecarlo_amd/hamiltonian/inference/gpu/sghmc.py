@@ -347,6 +347,7 @@ class sghmc(sgmcmc):
         outs = {k: torch.empty(n_steps * w, dtype=torch.float64, device=dev)
                 for k, w in (('A', 1), ('loss', 1), ('nlp', 1), ('E', 2))}
         out_acc = torch.empty(n_steps, dtype=torch.int32, device=dev)
+        out_abort = torch.zeros(1, dtype=torch.int32, device=dev)
         row0 = np.asarray(rows, dtype=np.int64)
         eps_a = np.asarray(eps, dtype=np.float64)
         a = nat.MlpSghmcArgs()
@@ -371,8 +372,21 @@ class sghmc(sgmcmc):
             a.par.p[i] = state[k].data_ptr()
         a.out_A, a.out_accepted = ptr(outs['A']), ptr(out_acc)
         a.out_loss, a.out_nlp, a.out_E = ptr(outs['loss']), ptr(outs['nlp']), ptr(outs['E'])
+        a.out_abort = ptr(out_abort)
         ctx = nat.context(dev)
+        # the state before the call: a call whose fused exchange timed out leaves it invalid (below)
+        saved = [state[k].clone() for k in MLP_PARAM_NAMES] if ctx.mlp_fuse else None
         ctx.check(ctx.lib.hmcx_mlp_sghmc_run(ctx.h, a), "hmcx_mlp_sghmc_run")
+        if saved is not None and int(out_abort.item()):
+            # a fused layer-2/3 launch timed out in its exchange (include/hmcx.h out_abort): restore the
+            # state and re-run the call unfused — same schedule, noise and masks, so the results are
+            # those the fused launches would have given; the context stays unfused afterwards
+            import sys
+            print("hmcx: fused MLP layer-2/3 exchange timed out; re-running the call unfused", file=sys.stderr)
+            for k, t in zip(MLP_PARAM_NAMES, saved):
+                state[k].copy_(t)
+            ctx.set_mlp_fuse(False)
+            ctx.check(ctx.lib.hmcx_mlp_sghmc_run(ctx.h, a), "hmcx_mlp_sghmc_run (unfused re-run)")
         self.global_step += n_steps
         h = {k: v.cpu().numpy() for k, v in outs.items()}
         res = RunResult(h['A'], out_acc.cpu().numpy().astype(bool), h['loss'], h['E'].reshape(n_steps, 2),

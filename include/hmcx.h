@@ -364,8 +364,16 @@ typedef struct hmcx_mlp_sghmc_args {
   double* out_loss;        /* device [n_steps] */
   double* out_nlp;         /* device [n_steps] or NULL */
   double* out_E;           /* device [n_steps*2] (E_current, E_new) or NULL */
+  int32_t* out_abort;      /* device [1] or NULL: the call's verdict — 1 when an exchange of the fused
+                              layer-2/3 launches timed out; the state and every output of the call are
+                              then invalid: restore the state and re-run with hmcx_set_mlp_fuse(ctx, 0).
+                              NULL: the call waits for its stream and returns an error instead. */
 } hmcx_mlp_sghmc_args;
 int hmcx_mlp_sghmc_run(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* a);
+
+/* on = 0: hmcx_mlp_sghmc_run stops fusing layer 2 and layer 3 into one launch (no cross-workgroup
+ * exchange; one more launch per forward) — the recovery path after out_abort; on = 1 restores it. */
+int hmcx_set_mlp_fuse(hmcx_ctx* ctx, int on);
 
 #ifdef __cplusplus
 }
