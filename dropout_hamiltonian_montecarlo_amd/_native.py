@@ -156,7 +156,8 @@ def load_library():
         lib.hmcx_mlp_loss.argtypes = [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                                       ctypes.POINTER(MlpParams), c_void_p, c_void_p, c_void_p]
         lib.hmcx_mlp_sghmc_run.argtypes = [c_void_p, ctypes.POINTER(MlpSghmcArgs)]
-        lib.hmcx_set_mlp_fuse.argtypes = [c_void_p, c_int]
+        if hasattr(lib, "hmcx_set_mlp_fuse"):          # absent in older builds loaded for A/B runs
+            lib.hmcx_set_mlp_fuse.argtypes = [c_void_p, c_int]
         lib.hmcx_logistic_grad.argtypes = [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
                                            c_void_p, c_void_p, c_double, c_void_p, c_void_p]
         lib.hmcx_logistic_loglik.argtypes = [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int,

@@ -34,6 +34,7 @@
 #include <type_traits>
 #include <algorithm>
 #include <vector>
+#include <cstring>
 
 namespace hmcx {
 
@@ -46,54 +47,76 @@ constexpr int MM_NT = MM_NW * 64;
 // Dropout masks of one forward: m0, m1, m2 at offsets 0, mn, 2·mn.
 template <typename T> struct MaskSrc {
   const T* vals;          // explicit mask values (API / BUFFER mode), or
-  const uint8_t* keep;    // keep flags (PHILOX mode): value = keep ? scale : 0;  both null: no dropout
+  const uint8_t* keep;    // keep flags (k_mlp_keep): value = keep ? scale : 0;  neither: no dropout or MK_PHILOX
   T scale;
   int mn;
+  // MK_PHILOX: the keep flags are drawn where they are used — element e = which·mn + i is word e % 4
+  // of Philox4x32-10({e / 4, slot, step, chain}, seed), the values k_mlp_keep and hmcx_mlp_masks give
+  uint64_t seed; uint32_t chain, step, slot;
 };
-// Mask reads: both candidate sources are loaded unconditionally (an absent source reads a zero
-// dummy) and pinned by an empty asm, so hipcc cannot sink the loads into the (wave-uniform) source
-// branches — a load inside a branch is waited for on the spot (s_waitcnt vmcnt(0) per mask value),
-// which serialised the 48 mask/activation loads of the layer-3 backward.
-__device__ __align__(16) unsigned char g_mask_dummy[32];
-template <typename T> struct MRaw { T v; uint32_t k; };
-// unconditional raw loads of element i of mask `which` from both sources (see above)
-template <typename T> __device__ inline MRaw<T> mraw(const MaskSrc<T>& s, int which, size_t i) {
-  const size_t e = (size_t)which * s.mn + i;
-  const T* vp = s.vals ? s.vals + e : reinterpret_cast<const T*>(g_mask_dummy);
-  const uint8_t* kp = s.keep ? s.keep + e : g_mask_dummy;
-  return MRaw<T>{*vp, (uint32_t)*kp};
-}
-// pin after a whole batch of mraw loads has been issued (the pin waits for its own load only)
-template <typename T> __device__ inline void mpin(MRaw<T>& r) { asm volatile("" : "+v"(r.v), "+v"(r.k)); }
-template <typename T> __device__ inline T mfin(const MaskSrc<T>& s, const MRaw<T>& r) {
-  return s.vals ? r.v : (s.keep ? (r.k ? s.scale : T(0)) : T(1));
-}
-template <typename T> __device__ inline T mval(const MaskSrc<T>& s, int which, size_t i) {
-  MRaw<T> r = mraw(s, which, i);
-  mpin(r);
-  return mfin(s, r);
-}
-// V consecutive mask values from an element index that is a multiple of V (V = 16 / sizeof T)
-template <typename T, int V> __device__ inline void mvals(const MaskSrc<T>& s, int which, size_t i, T (&m)[V]) {
-  const size_t e = (size_t)which * s.mn + i;
-  const T* vp = s.vals ? s.vals + e : reinterpret_cast<const T*>(g_mask_dummy);
-  const uint8_t* kp = s.keep ? s.keep + e : g_mask_dummy;
-  T v[V];
-#pragma unroll
-  for (int q = 0; q < V; ++q) v[q] = vp[q];
-  uint32_t k;
-  if constexpr (V == 4) k = *reinterpret_cast<const uint32_t*>(kp);
-  else k = *reinterpret_cast<const uint16_t*>(kp);
-#pragma unroll
-  for (int q = 0; q < V; ++q) asm volatile("" : "+v"(v[q]));
-  asm volatile("" : "+v"(k));
-#pragma unroll
-  for (int q = 0; q < V; ++q)
-    m[q] = s.vals ? v[q] : (s.keep ? (((k >> (8 * q)) & 0xFF) ? s.scale : T(0)) : T(1));
-}
 
 __device__ inline bool keep_flag(uint32_t w) {                // Chainer dropout: keep iff u >= ratio
   return (float)(w >> 8) * 5.9604644775390625e-08f >= 0.1f;
+}
+template <typename T> __device__ inline u32x4 mask_words(const MaskSrc<T>& s, size_t e) {
+  u32x4 c = {{(uint32_t)(e >> 2), s.slot, s.step, s.chain}};
+  return philox4x32_10(c, (uint32_t)s.seed, (uint32_t)(s.seed >> 32));
+}
+
+// Where the masks come from is a compile-time parameter (MK) of every kernel that reads them, so a
+// mask read is one load of the one source (MK_KEEP / MK_VALS), a Philox draw (MK_PHILOX) or nothing.
+// Loaded values are pinned by an empty asm after the batch they belong to, so hipcc cannot sink
+// a load into a branch (which it then waits for on the spot).
+enum MaskKind { MK_NONE = 0, MK_KEEP = 1, MK_VALS = 2, MK_PHILOX = 3 };
+template <typename T> struct MRaw { T v; uint32_t k; };
+template <typename T, int MK> __device__ inline MRaw<T> mraw(const MaskSrc<T>& s, int which, size_t i) {
+  MRaw<T> r{T(1), 1u};
+  const size_t e = (size_t)which * s.mn + i;
+  if constexpr (MK == MK_KEEP) r.k = s.keep[e];
+  if constexpr (MK == MK_VALS) r.v = s.vals[e];
+  if constexpr (MK == MK_PHILOX) r.k = keep_flag(mask_words(s, e).v[e & 3]) ? 1u : 0u;
+  return r;
+}
+template <typename T, int MK> __device__ inline void mpin(MRaw<T>& r) {
+  if constexpr (MK == MK_KEEP) asm volatile("" : "+v"(r.k));
+  if constexpr (MK == MK_VALS) asm volatile("" : "+v"(r.v));
+}
+template <typename T, int MK> __device__ inline T mfin(const MaskSrc<T>& s, const MRaw<T>& r) {
+  if constexpr (MK == MK_KEEP || MK == MK_PHILOX) return r.k ? s.scale : T(0);
+  else if constexpr (MK == MK_VALS) return r.v;
+  else return T(1);
+}
+template <typename T, int MK> __device__ inline T mval(const MaskSrc<T>& s, int which, size_t i) {
+  MRaw<T> r = mraw<T, MK>(s, which, i);
+  mpin<T, MK>(r);
+  return mfin<T, MK>(s, r);
+}
+// V consecutive mask values from an element index that is a multiple of V (V = 16 / sizeof T)
+template <typename T, int V, int MK> __device__ inline void mvals(const MaskSrc<T>& s, int which, size_t i, T (&m)[V]) {
+  const size_t e = (size_t)which * s.mn + i;
+  if constexpr (MK == MK_VALS) {
+    T v[V];
+#pragma unroll
+    for (int q = 0; q < V; ++q) v[q] = s.vals[e + q];
+#pragma unroll
+    for (int q = 0; q < V; ++q) asm volatile("" : "+v"(v[q]));
+#pragma unroll
+    for (int q = 0; q < V; ++q) m[q] = v[q];
+  } else if constexpr (MK == MK_KEEP) {
+    uint32_t k;
+    if constexpr (V == 4) k = *reinterpret_cast<const uint32_t*>(s.keep + e);
+    else k = *reinterpret_cast<const uint16_t*>(s.keep + e);
+    asm volatile("" : "+v"(k));
+#pragma unroll
+    for (int q = 0; q < V; ++q) m[q] = ((k >> (8 * q)) & 0xFF) ? s.scale : T(0);
+  } else if constexpr (MK == MK_PHILOX) {                        // e % V == 0: one Philox block
+    const u32x4 w = mask_words(s, e);
+#pragma unroll
+    for (int q = 0; q < V; ++q) m[q] = keep_flag(w.v[(e & 3) + q]) ? s.scale : T(0);
+  } else {
+#pragma unroll
+    for (int q = 0; q < V; ++q) m[q] = T(1);
+  }
 }
 
 // Gradient + prior (mlp.py:63) or the SGHMC momentum update (sghmc.py:31,34) of one variable.
@@ -172,10 +195,12 @@ template <typename T> struct MMArgs {
   // workgroups of one row block meet in a tagged-granule arena (see k_mm)
   char* gx; int gx_bytes; unsigned ep; int* abort_flag;
   int N3; const T* bias3; T* gz;     // n_out, b3 and the gz output of the fused layer 3
+  T* h1out;                          // MM_L23: store the slice's columns of h1 = max((xw + b1)·m0, 0)
+  const T* H1;                       // MM_GA1: the gate from a stored h1 (no mask reads)
   int force_abort;                   // test knob (HMCX_MLP_FORCE_ABORT): raise the abort word, skip the publish
   unsigned long long* prof;          // HMCX_MLP_PROF: per-workgroup s_memrealtime stamps of the MM_L23 phases
 };
-constexpr int L23_NPH = 8;           // stamps per workgroup and launch (prof)
+constexpr int L23_NPH = 12;          // stamps per workgroup and launch (prof)
 
 template <typename T, int OP>
 __device__ inline T op_apply(T x, T mask, T bias) {
@@ -196,7 +221,7 @@ template <> __device__ inline int kmap<double>(int u, int lg) { return ((u >> 1)
 // x[u][i] = Op(r, k0 + kmap(u, lg)).  TR: element (r, k) at P[k·ld + r], else P[r·ld + k].
 // VEC (requires !TR, ld % (16/sizeof T) == 0 and a 16-byte aligned P): 16-byte vector loads along k.
 // OP_H1 masks index the stored matrix (element idx); its bias column is TR ? r : k.
-template <typename T, int OP, int TR, int VEC>
+template <typename T, int OP, int TR, int VEC, int MK>
 __device__ inline void load_chunk(T (&x)[4][2], const T* P, int ld, int r0, int R, int k0, int ke, int lr, int lg,
                                   const MaskSrc<T>& ms, const T* b1) {
   if constexpr (!VEC) {
@@ -215,7 +240,7 @@ __device__ inline void load_chunk(T (&x)[4][2], const T* P, int ld, int r0, int 
         okv[i][u] = ok;
         pv[i][u] = P[idx];
         if constexpr (OP == OP_H1) {
-          mr[i][u] = mraw(ms, 0, idx);
+          mr[i][u] = mraw<T, MK>(ms, 0, idx);
           bv[i][u] = b1[ok ? (TR ? r : k) : 0];
         }
       }
@@ -224,8 +249,8 @@ __device__ inline void load_chunk(T (&x)[4][2], const T* P, int ld, int r0, int 
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        if constexpr (OP == OP_H1) mpin(mr[i][u]);
-        const T mv = OP == OP_H1 ? mfin(ms, mr[i][u]) : T(1);
+        if constexpr (OP == OP_H1) mpin<T, MK>(mr[i][u]);
+        const T mv = OP == OP_H1 ? mfin<T, MK>(ms, mr[i][u]) : T(1);
         const T bb = OP == OP_H1 ? bv[i][u] : T(0);
         x[u][i] = okv[i][u] ? op_apply<T, OP>(pv[i][u], mv, bb) : T(0);
       }
@@ -254,7 +279,7 @@ __device__ inline void load_chunk(T (&x)[4][2], const T* P, int ld, int r0, int 
           v[0] = w.x; v[1] = w.y;
         }
         if constexpr (OP == OP_H1) {
-          mvals<T, V>(ms, 0, base, m);
+          mvals<T, V, MK>(ms, 0, base, m);
 #pragma unroll
           for (int q = 0; q < V; ++q) bb[q] = b1[ok ? kv + q : q];
         }
@@ -303,13 +328,61 @@ __device__ inline void ce_rows(T* zt, int zs, double* rowl, int m0, int M, int N
   }
 }
 
+// ce_rows with the classes of a row spread over LPR lanes (LPR ≥ N; 16 or 32): max, Σexp and the
+// label's log-probability by lane butterflies instead of serial loops over LDS, the row's label
+// already in a register (yv[pass], loaded at kernel start).  Same formula as ce_rows (F.softmax_
+// cross_entropy, mean): gz = (exp((z − max) − log Σ) − onehot)/M; lpart[blk] = Σ_rows −log p[y].
+template <typename T, int LPR>
+__device__ inline void ce_rows_lanes(T* zt, int zs, double* rowl, int m0, int M, int N, const int32_t (&yv)[2],
+                                     T* gz, int ldg, double* lpart, int blk, bool writer) {
+  constexpr int RPP = MM_NT / LPR;                               // rows per pass
+  const int t = threadIdx.x, k = t % LPR;
+#pragma unroll
+  for (int pass = 0; pass < 32 / RPP; ++pass) {
+    const int r = pass * RPP + t / LPR, m = m0 + r;
+    const bool kin = k < N;
+    const T z = kin ? zt[r * zs + k] : T(0);
+    T mx = kin ? z : -INFINITY;
+#pragma unroll
+    for (int w = LPR / 2; w >= 1; w >>= 1) {                      // NaN propagates as in np.max
+      const T o = __shfl_xor(mx, w, LPR);
+      mx = (o > mx || o != o) ? o : mx;
+    }
+    T e = kin ? exp(z - mx) : T(0);
+#pragma unroll
+    for (int w = LPR / 2; w >= 1; w >>= 1) e += __shfl_xor(e, w, LPR);
+    const T ls = log(e);
+    const int lab = yv[pass];
+    double l = (kin && k == lab && m < M) ? -(double)((z - mx) - ls) : 0.0;
+    if (kin) {
+      T g = T(0);
+      if (m < M) {
+        g = exp((z - mx) - ls);
+        if (k == lab) g -= T(1);
+        g = g / (T)M;
+        if (writer) gz[(size_t)m * ldg + k] = g;
+      }
+      zt[r * zs + k] = g;
+    }
+#pragma unroll
+    for (int w = LPR / 2; w >= 1; w >>= 1) l += __shfl_xor(l, w, LPR);
+    if (k == 0) rowl[r] = l;
+  }
+  __syncthreads();
+  if (t == 0 && writer) {
+    double s = 0.0;
+    for (int r = 0; r < 32; ++r) s += rowl[r];
+    lpart[blk] = s;
+  }
+}
+
 // Layer-3 backward of one 32-row block from gz in LDS (zt[32][zs], N = n_out columns; rows past M
 // hold zeros):  ga2 = ((gz·W3)·m2)·[h2>0]·m1 and its column sums (b2 partial), column sums of gz
 // (b3 partial), and gzᵀ·d3 over the block's rows (W3 partial).  Threads own a column j and a row
 // group (rows ≡ g mod R, R = blockDim / n_mid); W3 is staged in LDS scratch `scr` when it fits.
 // Columns [jlo, jhi) of n_mid only (the workgroup's slice: the layer-3 kernel runs one workgroup per
 // (row block, column slice)); `first` marks the slice that also writes the b3 partial.
-template <typename T>
+template <typename T, int MK>
 __device__ inline void l3_backward(const MMArgs<T>& a, const T* zt, int zs, int m0, int blk, T* scr, int scr_n,
                                    int jlo, int jhi, bool first, int n_out = -1) {
   const int N = n_out >= 0 ? n_out : a.N, nm = a.n_mid, nj = jhi - jlo;
@@ -354,8 +427,8 @@ __device__ inline void l3_backward(const MMArgs<T>& a, const T* zt, int zs, int 
             const int r = min(r0 + c * R, rows - 1);
             const size_t i = (size_t)(m0 + r) * nm + j;
             hv[c] = a.h2[i];
-            m1v[c] = mval(a.ms, 1, i);
-            m2v[c] = mval(a.ms, 2, i);
+            m1v[c] = mval<T, MK>(a.ms, 1, i);
+            m2v[c] = mval<T, MK>(a.ms, 2, i);
             acc8[c] = T(0);
           }
 #pragma unroll 1
@@ -419,22 +492,22 @@ __device__ inline void l3_backward(const MMArgs<T>& a, const T* zt, int zs, int 
   }
 }
 
-template <typename T, int EPI>
+template <typename T, int EPI, int MK>
 __device__ inline void mm_epilogue(const MMArgs<T>& a, int m, int n, T v) {
   const size_t i = (size_t)m * a.ldc + n;
   if constexpr (EPI == MM_STORE) {
     a.C[i] = v;
   } else if constexpr (EPI == MM_L2) {                          // mlp.py:30-31
-    const T t = (v + a.bias[n]) * mval(a.ms, 1, i);
+    const T t = (v + a.bias[n]) * mval<T, MK>(a.ms, 1, i);
     const T h = t > T(0) ? t : T(0);
     a.C[i] = h;
-    a.C2[i] = h * mval(a.ms, 2, i);
+    a.C2[i] = h * mval<T, MK>(a.ms, 2, i);
   } else if constexpr (EPI == MM_UPD) {
     apply_upd(a.u, a.upd_mode, i, v);
   }
 }
 
-template <typename T, int EPI, int AOP, int BOP, int TA, int TB, int AV, int BV>
+template <typename T, int EPI, int AOP, int BOP, int TA, int TB, int AV, int BV, int MK>
 __global__ __launch_bounds__(MM_NT) void k_mm(MMArgs<T> a) {
   using M = mfma16<T>;
   __shared__ T red[MM_NW][32][33];
@@ -456,14 +529,19 @@ __global__ __launch_bounds__(MM_NT) void k_mm(MMArgs<T> a) {
   // loaded before the GEMM's own operands, so the epilogue never waits on memory
   MRaw<T> pm1[2], pm2[2];
   T pb2v[2], pw3v[2], pb3v = T(0);
+  int32_t yv[2] = {0, 0};
   if constexpr (EPI == MM_L23) {
+    // labels of the rows this thread handles in the cross-entropy (ce_rows_lanes)
+    const int lpr = a.N3 <= 16 ? 16 : 32, rpp = MM_NT / lpr;
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) yv[pass] = a.y[min(m0 + pass * rpp + tid / lpr, a.M - 1)];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int e = tid + MM_NT * u, mm = e >> 5, nn = e & 31, m = m0 + mm, n = n0 + nn;
       const bool ok = m < a.M && n < a.N;
       const size_t i = ok ? (size_t)m * a.ldc + n : 0;
-      pm1[u] = mraw(a.ms, 1, i);
-      pm2[u] = mraw(a.ms, 2, i);
+      pm1[u] = mraw<T, MK>(a.ms, 1, i);
+      pm2[u] = mraw<T, MK>(a.ms, 2, i);
       pb2v[u] = a.bias[ok ? n : 0];
       const int o = e >> 5, c = e & 31;
       const bool okw = o < a.N3 && n0 + c < a.N;
@@ -471,6 +549,7 @@ __global__ __launch_bounds__(MM_NT) void k_mm(MMArgs<T> a) {
     }
     pb3v = a.bias3[tid < a.N3 ? tid : 0];
   }
+  stamp(7);
   const int Kq = ((a.K + 16 * MM_NW - 1) / (16 * MM_NW)) * 16;   // k range per wave (multiple of 16)
   const int kb = wave * Kq, ke = min(a.K, kb + Kq);
   typename M::acc_t acc[2][2];
@@ -481,29 +560,43 @@ __global__ __launch_bounds__(MM_NT) void k_mm(MMArgs<T> a) {
   // three chunks in flight (register ring), then one MFMA batch per chunk
   T av[3][4][2], bv[3][4][2];
   auto load = [&](int s, int k0) {
-    load_chunk<T, AOP, TA, AV>(av[s], a.A, a.lda, m0, a.M, k0, ke, lr, lg, a.ms, a.b1);
-    load_chunk<T, BOP, !TB, BV>(bv[s], a.B, a.ldb, n0, a.N, k0, ke, lr, lg, a.ms, a.b1);
+    load_chunk<T, AOP, TA, AV, MK>(av[s], a.A, a.lda, m0, a.M, k0, ke, lr, lg, a.ms, a.b1);
+    load_chunk<T, BOP, !TB, BV, MK>(bv[s], a.B, a.ldb, n0, a.N, k0, ke, lr, lg, a.ms, a.b1);
   };
-  auto mfma = [&](int s) {
+  auto mfma = [&](int s, int k0) {
+    if constexpr (EPI == MM_L23 && AOP == OP_H1) {
+      // h1 of the k range of this WG's own column slice (one writer per element) for the kernels
+      // that need h1 after this forward (layer-1 backward gate, W2 gradient)
+      if (a.h1out) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int r = m0 + 16 * i + lr, k = k0 + kmap<T>(u, lg);
+            if (r < a.M && k < ke && k >= n0 && k < n0 + 32) a.h1out[(size_t)r * a.lda + k] = av[s][u][i];
+          }
+      }
+    }
 #pragma unroll
     for (int u = 0; u < 4; ++u)
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = M::fma(av[s][u][i], bv[s][u][j], acc[i][j]);
+    if (s == 0) stamp(8);
   };
   if (kb < ke) load(0, kb);
   if (kb + 16 < ke) load(1, kb + 16);
   if (kb + 32 < ke) load(2, kb + 32);
   for (int k0 = kb; k0 < ke; k0 += 48) {
-    mfma(0);
+    mfma(0, k0);
     if (k0 + 48 < ke) load(0, k0 + 48);
     if (k0 + 16 < ke) {
-      mfma(1);
+      mfma(1, k0 + 16);
       if (k0 + 64 < ke) load(1, k0 + 64);
     }
     if (k0 + 32 < ke) {
-      mfma(2);
+      mfma(2, k0 + 32);
       if (k0 + 80 < ke) load(2, k0 + 80);
     }
   }
@@ -513,7 +606,9 @@ __global__ __launch_bounds__(MM_NT) void k_mm(MMArgs<T> a) {
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int q = 0; q < 4; ++q) red[wave][16 * i + M::row(lane, q)][16 * j + lr] = acc[i][j][q];
+  stamp(9);
   __syncthreads();
+  stamp(10);
 #pragma unroll
   for (int u = 0; u < 1024 / MM_NT; ++u) {
     const int e = tid + MM_NT * u, mm = e >> 5, nn = e & 31;
@@ -527,18 +622,25 @@ __global__ __launch_bounds__(MM_NT) void k_mm(MMArgs<T> a) {
       T g = T(0);
       if (m < a.M && n < a.N) {
         const size_t i = (size_t)m * a.ldc + n;
-        const T m0v = mval(a.ms, 0, i);
-        g = (v * ((a.H[i] + a.b1[n]) * m0v > T(0) ? T(1) : T(0))) * m0v;
+        if (a.H1) {
+          // (xw + b1)·m0 > 0 ⟺ h1 > 0, and then m0 = scale; where h1 = 0 the product is ±0 either way
+          // (the sign of v·0), so this is the reference's value without reading m0 again
+          const bool pos = a.H1[i] > T(0);
+          g = (v * (pos ? T(1) : T(0))) * (pos ? a.ms.scale : T(0));
+        } else {
+          const T m0v = mval<T, MK>(a.ms, 0, i);
+          g = (v * ((a.H[i] + a.b1[n]) * m0v > T(0) ? T(1) : T(0))) * m0v;
+        }
         a.C[i] = g;
       }
       red[0][mm][nn] = g;
     } else if constexpr (EPI == MM_L23) {                      // mlp.py:30-31; the tile stays in LDS
       T d = T(0), h = T(0), m1 = T(0), m2 = T(0);
-      mpin(pm1[u]);
-      mpin(pm2[u]);
+      mpin<T, MK>(pm1[u]);
+      mpin<T, MK>(pm2[u]);
       if (m < a.M && n < a.N) {
-        m1 = mfin(a.ms, pm1[u]);
-        m2 = mfin(a.ms, pm2[u]);
+        m1 = mfin<T, MK>(a.ms, pm1[u]);
+        m2 = mfin<T, MK>(a.ms, pm2[u]);
         const T t = (v + pb2v[u]) * m1;
         h = t > T(0) ? t : T(0);
         d = h * m2;
@@ -554,7 +656,7 @@ __global__ __launch_bounds__(MM_NT) void k_mm(MMArgs<T> a) {
       red[4][mm][nn] = m1;
       red[5][mm][nn] = m2;
     } else {
-      if (m < a.M && n < a.N) mm_epilogue<T, EPI>(a, m, n, v);
+      if (m < a.M && n < a.N) mm_epilogue<T, EPI, MK>(a, m, n, v);
     }
   }
   if constexpr (EPI == MM_L3CE) {
@@ -564,7 +666,7 @@ __global__ __launch_bounds__(MM_NT) void k_mm(MMArgs<T> a) {
     __syncthreads();
     const int cw = (a.n_mid + gridDim.y - 1) / gridDim.y;
     const int jlo = min(a.n_mid, (int)blockIdx.y * cw), jhi = min(a.n_mid, jlo + cw);
-    l3_backward<T>(a, &red[0][0][0], 33, m0, blockIdx.x, &red[1][0][0], (MM_NW - 1) * 32 * 33, jlo, jhi, first);
+    l3_backward<T, MK>(a, &red[0][0][0], 33, m0, blockIdx.x, &red[1][0][0], (MM_NW - 1) * 32 * 33, jlo, jhi, first);
   }
   if constexpr (EPI == MM_L23) {
     // Layer 3 of this row block, in the same launch: z = d3·W3ᵀ + b3 (mlp.py:31) needs all n_mid
@@ -613,7 +715,8 @@ __global__ __launch_bounds__(MM_NT) void k_mm(MMArgs<T> a) {
     __syncthreads();
     stamp(4);
     const bool first = s == 0;
-    ce_rows<T>(zt, 33, rowl, m0, a.M, No, a.y, a.gz, No, a.lpart, rb, first);
+    if (No <= 16) ce_rows_lanes<T, 16>(zt, 33, rowl, m0, a.M, No, yv, a.gz, No, a.lpart, rb, first);
+    else ce_rows_lanes<T, 32>(zt, 33, rowl, m0, a.M, No, yv, a.gz, No, a.lpart, rb, first);
     __syncthreads();
     stamp(5);
     // layer-3 backward of the slice's columns, all operands in LDS (gz in zt, W3 slice in w3s, the
@@ -667,7 +770,7 @@ __global__ __launch_bounds__(MM_NT) void k_mm(MMArgs<T> a) {
 
 // Layer 3 for n_out > 32: xw-free logits d3·W3ᵀ already stored in z; one 32-row block per
 // workgroup, rows (+ b3) staged in dynamic LDS, then the same cross-entropy and layer-3 backward.
-template <typename T>
+template <typename T, int MK>
 __global__ __launch_bounds__(MM_NT) void k_l3_wide(MMArgs<T> a, const T* z) {
   extern __shared__ unsigned char dsm[];
   double* rowl = reinterpret_cast<double*>(dsm);
@@ -682,7 +785,7 @@ __global__ __launch_bounds__(MM_NT) void k_l3_wide(MMArgs<T> a, const T* z) {
   __syncthreads();
   ce_rows<T>(zt, zs, rowl, m0, a.M, N, a.y, a.C, a.ldc, a.lpart, blockIdx.x);
   __syncthreads();
-  l3_backward<T>(a, zt, zs, m0, blockIdx.x, scr, MM_NT, 0, a.n_mid, true);
+  l3_backward<T, MK>(a, zt, zs, m0, blockIdx.x, scr, MM_NT, 0, a.n_mid, true);
 }
 
 // Keep flags of F forwards (blockIdx.y = forward f, Philox slot MASK_SLOT0 + f), 3·mn per forward.
@@ -849,6 +952,7 @@ struct MlpNet {
   int B, n_in, n_mid, n_out, nlb;
   const T* X; const int32_t* y;
   T *xw, *h2, *d3, *z, *gz, *ga2, *ga1;
+  T* h1 = nullptr; bool h1_valid = false;   // h1 of the last fused forward (when its sub-step needs it)
   T *pb1, *pb2, *pb3, *pw3;              // gradient partials of b1, b2, b3, W3 ([nlb][...])
   hipStream_t st;
   bool xw_valid = false;
@@ -888,10 +992,20 @@ hipError_t mm(MlpNet<T>& net, MMArgs<T>& a) {
   const bool av = !TA && h1ok && kvec && vec_ok(a.A, a.lda, sizeof(T));
   const bool bv = TB && kvec && vec_ok(a.B, a.ldb, sizeof(T));
   hipStream_t st = net.st;
-  if (av && bv) hipLaunchKernelGGL((k_mm<T, EPI, AOP, BOP, TA, TB, !TA, TB>), grid, blk, 0, st, a);
-  else if (av) hipLaunchKernelGGL((k_mm<T, EPI, AOP, BOP, TA, TB, !TA, 0>), grid, blk, 0, st, a);
-  else if (bv) hipLaunchKernelGGL((k_mm<T, EPI, AOP, BOP, TA, TB, 0, TB>), grid, blk, 0, st, a);
-  else hipLaunchKernelGGL((k_mm<T, EPI, AOP, BOP, TA, TB, 0, 0>), grid, blk, 0, st, a);
+  auto go = [&](auto mkc) {
+    constexpr int MK = decltype(mkc)::value;
+    if (av && bv) hipLaunchKernelGGL((k_mm<T, EPI, AOP, BOP, TA, TB, !TA, TB, MK>), grid, blk, 0, st, a);
+    else if (av) hipLaunchKernelGGL((k_mm<T, EPI, AOP, BOP, TA, TB, !TA, 0, MK>), grid, blk, 0, st, a);
+    else if (bv) hipLaunchKernelGGL((k_mm<T, EPI, AOP, BOP, TA, TB, 0, TB, MK>), grid, blk, 0, st, a);
+    else hipLaunchKernelGGL((k_mm<T, EPI, AOP, BOP, TA, TB, 0, 0, MK>), grid, blk, 0, st, a);
+  };
+  constexpr bool masked = AOP == OP_H1 || BOP == OP_H1 || EPI == MM_L2 || EPI == MM_L3CE || EPI == MM_GA1 ||
+                          EPI == MM_L23;
+  if constexpr (!masked) go(std::integral_constant<int, MK_NONE>{});
+  else if (a.ms.slot) go(std::integral_constant<int, MK_PHILOX>{});
+  else if (a.ms.keep) go(std::integral_constant<int, MK_KEEP>{});
+  else if (a.ms.vals) go(std::integral_constant<int, MK_VALS>{});
+  else go(std::integral_constant<int, MK_NONE>{});
   return hipGetLastError();
 }
 
@@ -901,7 +1015,7 @@ void mm_set(MMArgs<T>& a, int M, int N, int K, const T* A, int lda, int ta, cons
 }
 
 // What the layer-3 kernel produces besides the loss
-struct L3Want { bool ga2, pb2, pb3, pw3; };
+struct L3Want { bool ga2, pb2, pb3, pw3, h1 = false; };
 
 // Forward with masks `ms` at parameters q (+ the requested layer-3 backward pieces); loss partials
 // into lpart (null: no loss); logits (optional) stored without b3.  Layer 1 only when xw is stale.
@@ -910,6 +1024,7 @@ hipError_t mlp_forward(MlpNet<T>& net, T* const* q, const MaskSrc<T>& ms, double
                        T* logits = nullptr) {
   const int B = net.B, nm = net.n_mid;
   hipError_t e;
+  net.h1_valid = false;
   if (!net.xw_valid) {                                        // xw = X·W1ᵀ
     MMArgs<T> a{};
     mm_set<T>(a, B, nm, net.n_in, net.X, net.n_in, 0, q[0], net.n_in, 1, net.xw, nm);
@@ -928,6 +1043,8 @@ hipError_t mlp_forward(MlpNet<T>& net, T* const* q, const MaskSrc<T>& ms, double
     a.pb3 = w.pb3 ? net.pb3 : nullptr;
     a.pw3 = w.pw3 ? net.pw3 : nullptr;
     a.C = nullptr; a.C2 = nullptr;                             // h2 / d3 stay in LDS
+    a.h1out = w.h1 ? net.h1 : nullptr;
+    net.h1_valid = w.h1;
     a.gx = net.gx; a.gx_bytes = net.gx_bytes; a.ep = gx_next_epoch(net.ctx); a.abort_flag = net.abort_flag;
     a.force_abort = net.l23_count == net.force_abort;
     if (net.prof && net.l23_count < net.prof_cap)
@@ -967,7 +1084,10 @@ hipError_t mlp_forward(MlpNet<T>& net, T* const* q, const MaskSrc<T>& ms, double
   a.pend = net.pend;
   net.pend.mode = UPD_NONE;
   const size_t lds = 32 * sizeof(double) + ((size_t)MM_NT + (size_t)32 * (net.n_out + 1)) * sizeof(T);
-  hipLaunchKernelGGL(k_l3_wide<T>, dim3(net.nlb), dim3(MM_NT), lds, net.st, a, (const T*)net.z);
+  if (a.ms.slot) hipLaunchKernelGGL((k_l3_wide<T, MK_PHILOX>), dim3(net.nlb), dim3(MM_NT), lds, net.st, a, (const T*)net.z);
+  else if (a.ms.keep) hipLaunchKernelGGL((k_l3_wide<T, MK_KEEP>), dim3(net.nlb), dim3(MM_NT), lds, net.st, a, (const T*)net.z);
+  else if (a.ms.vals) hipLaunchKernelGGL((k_l3_wide<T, MK_VALS>), dim3(net.nlb), dim3(MM_NT), lds, net.st, a, (const T*)net.z);
+  else hipLaunchKernelGGL((k_l3_wide<T, MK_NONE>), dim3(net.nlb), dim3(MM_NT), lds, net.st, a, (const T*)net.z);
   return hipGetLastError();
 }
 
@@ -976,6 +1096,7 @@ hipError_t mlp_ga1(MlpNet<T>& net, T* const* q, const MaskSrc<T>& ms, bool want_
   MMArgs<T> a{};
   mm_set<T>(a, net.B, net.n_mid, net.n_mid, net.ga2, net.n_mid, 0, q[2], net.n_mid, 0, net.ga1, net.n_mid);
   a.ms = ms; a.H = net.xw; a.b1 = q[1];
+  a.H1 = net.h1_valid ? net.h1 : nullptr;
   a.colpart = want_pb1 ? net.pb1 : nullptr;
   return mm<T, MM_GA1, 0, 0>(net, a);
 }
@@ -987,6 +1108,10 @@ hipError_t mlp_wgrad(MlpNet<T>& net, T* const* q, const MaskSrc<T>& ms, int v, i
   MMArgs<T> a{};
   a.upd_mode = mode; a.u = u;
   if (v == 2) {                                               // ga2ᵀ·h1
+    if (net.h1_valid) {                                       // h1 stored by the fused forward
+      mm_set<T>(a, nm, nm, B, net.ga2, nm, 1, net.h1, nm, 0, nullptr, nm);
+      return mm<T, MM_UPD, 1, 0>(net, a);
+    }
     mm_set<T>(a, nm, nm, B, net.ga2, nm, 1, net.xw, nm, 0, nullptr, nm);
     a.ms = ms; a.b1 = q[1];
     return mm<T, MM_UPD, 1, 0, OP_PLAIN, OP_H1>(net, a);
@@ -1026,7 +1151,7 @@ int net_fuse(hmcx_ctx* ctx, MlpNet<T>& net) {
   const int S = (net.n_mid + 31) / 32;
   if (off || ctx->mlp_nofuse || net.n_out > 32 || S > 16) return HMCX_OK;
   int per_cu = 0;
-  const void* kfn = (const void*)k_mm<T, MM_L23, OP_H1, OP_PLAIN, 0, 1, 1, 1>;
+  const void* kfn = (const void*)k_mm<T, MM_L23, OP_H1, OP_PLAIN, 0, 1, 1, 1, MK_PHILOX>;
   HMCX_HIP(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, MM_NT, 0));
   if ((long)per_cu * ctx->num_cus < (long)net.nlb * S) return HMCX_OK;
   const size_t need = (size_t)net.nlb * S * 32 * net.n_out * 16;
@@ -1049,7 +1174,7 @@ int net_fuse(hmcx_ctx* ctx, MlpNet<T>& net) {
 template <typename T>
 void mlp_workspace(Workspace& ws, MlpNet<T>& net) {
   const size_t mn = (size_t)net.B * net.n_mid;
-  net.xw = ws.take<T>(mn); net.h2 = ws.take<T>(mn); net.d3 = ws.take<T>(mn);
+  net.xw = ws.take<T>(mn); net.h2 = ws.take<T>(mn); net.d3 = ws.take<T>(mn); net.h1 = ws.take<T>(mn);
   net.ga2 = ws.take<T>(mn); net.ga1 = ws.take<T>(mn);
   net.z = ws.take<T>((size_t)net.B * net.n_out); net.gz = ws.take<T>((size_t)net.B * net.n_out);
   net.pb1 = ws.take<T>((size_t)net.nlb * net.n_mid);
@@ -1080,7 +1205,7 @@ int mlp_grad_t(hmcx_ctx* ctx, const void* X, const int32_t* y, int B, int n_in, 
   double* lpart;
   do { ws.reset(); mlp_workspace<T>(ws, net); lpart = ws.take<double>(net.nlb); } while (ws.retry());
   if (ws.failed) return HMCX_ENOMEM;
-  const MaskSrc<T> ms{(const T*)masks, nullptr, T(1), B * n_mid};
+  const MaskSrc<T> ms{(const T*)masks, nullptr, T(1), B * n_mid, 0, 0, 0, 0};
   if (masks && (uintptr_t)masks % 16) net.vec_masks = false;
   T* q[6];
   for (int v = 0; v < 6; ++v) q[v] = (T*)par->p[v];
@@ -1114,7 +1239,7 @@ int mlp_loss_t(hmcx_ctx* ctx, const void* X, const int32_t* y, int B, int n_in, 
   double* lpart;
   do { ws.reset(); mlp_workspace<T>(ws, net); lpart = ws.take<double>(net.nlb); } while (ws.retry());
   if (ws.failed) return HMCX_ENOMEM;
-  const MaskSrc<T> ms{(const T*)masks, nullptr, T(1), B * n_mid};
+  const MaskSrc<T> ms{(const T*)masks, nullptr, T(1), B * n_mid, 0, 0, 0, 0};
   if (masks && (uintptr_t)masks % 16) net.vec_masks = false;
   T* q[6];
   for (int v = 0; v < 6; ++v) q[v] = (T*)par->p[v];
@@ -1156,6 +1281,15 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
     maxF = std::max(maxF, 6 * s->n_iter[si] + 2);
   }
   const bool philox_masks = s->mask_mode == HMCX_NOISE_PHILOX;
+  // Philox masks: the flags of a whole step stored once by k_mlp_keep and loaded by the kernels
+  // (default), or drawn inside the kernels where they are read (HMCX_MLP_MASKS=philox).  Measured on
+  // one box at config 3 (tools/gpu_r03_mlp_env.sh): 7.22 k leapfrog/s stored vs 6.38 k drawn — the
+  // draws sit on the layer-2 GEMM's critical path; stored h1 for the W1 / b1 / W2 backward
+  // (HMCX_MLP_H1=1) recovers most of it when drawn (6.76 k) and changes nothing when stored (7.19 k).
+  const char* mk_env = getenv("HMCX_MLP_MASKS");
+  const bool keep_arr = philox_masks && !(mk_env && !strcmp(mk_env, "philox"));
+  const char* h1_env = getenv("HMCX_MLP_H1");
+  const bool store_h1 = philox_masks && h1_env && h1_env[0] == '1';    // m0 ∈ {0, scale} only for Philox masks
   if (philox_masks) {
     if (n3 % 4) net.vec_masks = false;
   } else {
@@ -1182,7 +1316,7 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
     lp_cur = ws.take<double>(net.nlb);
     lp_new = ws.take<double>(net.nlb);
     lp_scr = ws.take<double>(net.nlb);
-    if (philox_masks) keep = ws.take<uint8_t>((size_t)maxF * n3);
+    if (keep_arr) keep = ws.take<uint8_t>((size_t)maxF * n3);
     accf = ws.take<int32_t>(1);
   } while (ws.retry());
   if (ws.failed) return HMCX_ENOMEM;
@@ -1205,13 +1339,17 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
     const int n = s->n_iter[si], F = 6 * n + 2;
     const uint32_t step_id = s->step_base + (uint32_t)si;
     const double* nz = s->noise_mode == HMCX_NOISE_BUFFER ? s->noise + s->noise_off[si] : nullptr;
-    if (philox_masks) {
+    if (philox_masks && keep_arr) {
       hipLaunchKernelGGL(k_mlp_keep, dim3((unsigned)(((n3 + 3) / 4 + 255) / 256), (unsigned)F), dim3(256), 0, st, keep,
                          n3, s->seed, s->chain, step_id);
     }
     auto masks_for = [&](int f) -> MaskSrc<T> {
-      if (philox_masks) return MaskSrc<T>{nullptr, keep + (size_t)f * n3, scale, mn};
-      return MaskSrc<T>{(const T*)s->masks + s->mask_off[si] + (size_t)f * n3, nullptr, scale, mn};
+      // PHILOX: the kernels draw the flags they read (MK_PHILOX, slot MASK_SLOT0 + f); with
+      // HMCX_MLP_MASKS=keep, k_mlp_keep stores the same flags once per step and the kernels load them
+      if (philox_masks && !keep_arr)
+        return MaskSrc<T>{nullptr, nullptr, scale, mn, s->seed, s->chain, step_id, MASK_SLOT0 + (uint32_t)f};
+      if (philox_masks) return MaskSrc<T>{nullptr, keep + (size_t)f * n3, scale, mn, 0, 0, 0, 0};
+      return MaskSrc<T>{(const T*)s->masks + s->mask_off[si] + (size_t)f * n3, nullptr, scale, mn, 0, 0, 0, 0};
     };
     // momentum (hmc.py:82-87), first drift into qa, Σp², Σθ² of the current state
     VarTab vt{};
@@ -1239,7 +1377,8 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
         u.noise = nz ? nz + (size_t)P * (it + 1) + off_v[v] : nullptr;   // BUFFER: one block of P per iteration
         u.seed = s->seed; u.chain = s->chain; u.step = step_id; u.slot = (uint32_t)(it + 1);
         u.e0 = (uint32_t)off_v[v];
-        const L3Want w{v <= 3, v == 3, v == 5, v == 4};
+        // h1 from the fused forward for the W1 / b1 / W2 sub-steps (HMCX_MLP_H1=0: recompute it)
+        const L3Want w{v <= 3, v == 3, v == 5, v == 4, store_h1 && v <= 2};
         HMCX_HIP(ctx, mlp_forward<T>(net, cur, ms, lp_scr, w));
         if (v <= 1) HMCX_HIP(ctx, mlp_ga1<T>(net, cur, ms, v == 1));
         if (v == 0 || v == 2) HMCX_HIP(ctx, mlp_wgrad<T>(net, cur, ms, v, UPD_SGHMC, u));

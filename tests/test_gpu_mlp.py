@@ -261,3 +261,143 @@ def test_mlp_log_prior_device_reduction(dtype, rtol):
     ref = om.mlp({"alpha": 0.05}, 30, 24, 7).log_prior({k: v.astype(np.float32 if dtype == torch.float32 else np.float64)
                                                          for k, v in par.items()})
     assert abs(m.log_prior(par) - ref) <= rtol * abs(ref)
+
+
+# ----------------------------------------------------------------------------- fused-launch timeouts
+def _mlp_f64_run(monkeypatch=None, force=None):
+    """The config-3 f64 trajectory of test_sghmc_mlp_config3_f64_trajectory_matches_oracle through
+    the sampler, optionally with HMCX_MLP_FORCE_ABORT (the given fused layer-2/3 launch of the first
+    call raises the MLP abort word and never publishes its partials)."""
+    mlp, sghmc = _mlp_cls()
+    n_in, n_mid, n_out, N, B = 784, 256, 10, 1000, 500
+    rs = np.random.RandomState(11)
+    X = rs.rand(N, n_in)
+    y = rs.randint(0, n_out, N)
+    start = {k: rs.normal(0, 0.05, s) for k, s in om.mlp_param_shapes(n_in, n_mid, n_out).items()}
+    get, one = _mask_stream(B, n_mid)
+    kw = dict(path_length=2e-3, step_size=1e-3, verbose=True)
+    m = mlp({"alpha": 0.01}, n_in, n_mid, n_out, dtype=torch.float64, device="cuda:0")
+    s = sghmc(m, start, noise='numpy', **kw)
+    s.mask_provider = get
+    s.trace, s.out = [], io.StringIO()
+    if force is not None:
+        monkeypatch.setenv("HMCX_MLP_FORCE_ABORT", str(force))
+    try:
+        np.random.seed(21)
+        post, logp = s.sample(epochs=1, burnin=1, batch_size=B, rng=np.random.RandomState(22), X_train=X, y_train=y)
+    finally:
+        if force is not None:
+            monkeypatch.delenv("HMCX_MLP_FORCE_ABORT")
+    return post, logp, s.trace, m
+
+
+def test_mlp_fused_timeout_is_recovered_in_process(monkeypatch, capfd):
+    """A fused MLP launch whose exchange times out (forced) makes its call report out_abort; the
+    sampler restores the state, re-runs the call unfused and continues: the trajectory equals the
+    undisturbed run's — bit-exact path lengths / accept flags, states within rel 1e-10 (the fused and
+    unfused launches differ only in the summation order of the logits)."""
+    ref_post, ref_logp, ref_tr, m = _mlp_f64_run()
+    try:
+        post, logp, tr, m = _mlp_f64_run(monkeypatch, force=3)
+        err = capfd.readouterr().err
+        assert "re-running the call unfused" in err
+        assert not m.ctx.mlp_fuse
+        assert [t["L"] for t in tr] == [t["L"] for t in ref_tr]
+        assert [t["accepted"] for t in tr] == [t["accepted"] for t in ref_tr]
+        for k in ref_post:
+            np.testing.assert_allclose(post[k], ref_post[k], rtol=1e-10, atol=1e-13)
+        np.testing.assert_allclose(logp, ref_logp, rtol=1e-10)
+    finally:
+        m.ctx.set_mlp_fuse(True)
+
+
+def test_mlp_timeout_leaves_softmax_persistent_path_alone(monkeypatch):
+    """The MLP abort word is its own: after a forced MLP timeout the persistent single-chain softmax
+    SGHMC kernel (which has its own sticky word) still runs and matches the oracle."""
+    from test_gpu_samplers import _run_gpu, _run_oracle
+    from oracle import inputs as gi
+    _, _, _, m = _mlp_f64_run(monkeypatch, force=0)
+    m.ctx.set_mlp_fuse(True)
+    c = gi.TRAJ_CONFIGS["sghmc_mnist"]
+    post_g, logp_g, tr_g, _ = _run_gpu(c, path=2)
+    m.ctx.set_sghmc_path(0)
+    post_r, logp_r, tr_r, _ = _run_oracle(c)
+    assert [t["accepted"] for t in tr_g] == [t["accepted"] for t in tr_r]
+    np.testing.assert_allclose(post_g["weights"], post_r["weights"], rtol=1e-9, atol=1e-12)
+
+
+def test_mlp_timeout_reported_through_c_abi_without_out_abort(monkeypatch):
+    """Plain C callers (out_abort = NULL) get an error from the call itself."""
+    from dropout_hamiltonian_montecarlo_amd import _native as nat
+    mlp, _ = _mlp_cls()
+    n_in, n_mid, n_out, B = 784, 256, 10, 500
+    m = mlp({"alpha": 0.01}, n_in, n_mid, n_out, dtype=torch.float32, device="cuda:0")
+    rs = np.random.RandomState(3)
+    X = torch.from_numpy(rs.rand(B, n_in)).to("cuda:0", torch.float32)
+    y = torch.from_numpy(rs.randint(0, n_out, B)).to("cuda:0", torch.int32)
+    par = [torch.from_numpy(v).to("cuda:0", torch.float32).contiguous() for v in m.init_params(2).values()]
+    row0, eps, n_iter, u = (np.zeros(1, np.int64), np.full(1, 1e-3), np.full(1, 2, np.int32), np.full(1, 0.5))
+    zoff = np.zeros(1, np.int64)
+    outs = torch.zeros(8, dtype=torch.float64, device="cuda:0")
+    acc = torch.zeros(1, dtype=torch.int32, device="cuda:0")
+    a = nat.MlpSghmcArgs()
+    a.dtype, a.B, a.n_in, a.n_mid, a.n_out, a.n_steps = m.code, B, n_in, n_mid, n_out, 1
+    for i in range(6):
+        a.order[i] = i
+    a.alpha = 0.01
+    a.X, a.y = nat.ptr(X), nat.ptr(y)
+    a.row0, a.eps = row0.ctypes.data_as(nat.c_i64p), eps.ctypes.data_as(nat.c_dblp)
+    a.n_iter, a.u_accept = n_iter.ctypes.data_as(nat.c_i32p), u.ctypes.data_as(nat.c_dblp)
+    a.noise_mode = a.mask_mode = nat.NOISE_PHILOX
+    a.noise_off = a.mask_off = zoff.ctypes.data_as(nat.c_i64p)
+    a.seed, a.chain, a.step_base = 1, 0, 0
+    for i in range(6):
+        a.par.p[i] = par[i].data_ptr()
+    a.out_A, a.out_accepted, a.out_loss = outs.data_ptr(), acc.data_ptr(), outs.data_ptr() + 8
+    monkeypatch.setenv("HMCX_MLP_FORCE_ABORT", "1")
+    assert m.ctx.lib.hmcx_mlp_sghmc_run(m.ctx.h, a) != 0
+    assert b"timed out" in m.ctx.lib.hmcx_last_error(m.ctx.h)
+    monkeypatch.delenv("HMCX_MLP_FORCE_ABORT")
+    assert m.ctx.lib.hmcx_mlp_sghmc_run(m.ctx.h, a) == 0          # the word was lowered
+    torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("variant", ["keep", "philox-h1"])
+def test_sampler_philox_masks_equal_api_masks(variant, monkeypatch):
+    """In Philox mode the sampler's dropout flags — stored once per step by k_mlp_keep (default) or
+    drawn inside the kernels where they are read (HMCX_MLP_MASKS=philox, with the backward reading
+    the stored h1 instead of the masks, HMCX_MLP_H1=1) — are the values hmcx_mlp_masks gives for the
+    same (seed, chain, step, slot): a run fed those API masks as buffers follows the Philox-mask run
+    bit for bit (float64, Philox noise in both)."""
+    if variant == "philox-h1":
+        monkeypatch.setenv("HMCX_MLP_MASKS", "philox")
+        monkeypatch.setenv("HMCX_MLP_H1", "1")
+    from dropout_hamiltonian_montecarlo_amd import _native as nat
+    mlp, sghmc = _mlp_cls()
+    n_in, n_mid, n_out, N, B = 784, 256, 10, 1000, 500
+    rs = np.random.RandomState(5)
+    X = rs.rand(N, n_in)
+    y = rs.randint(0, n_out, N)
+    m = mlp({"alpha": 0.01}, n_in, n_mid, n_out, dtype=torch.float64, device="cuda:0")
+    start = m.init_params(4)
+    kw = dict(path_length=3e-3, step_size=1e-3, verbose=False, noise='philox', seed=5, chain=3)
+
+    def api_masks(k, n):
+        out = torch.empty((n, 3, B, n_mid), dtype=torch.float64, device="cuda:0")
+        for f in range(n):
+            m.ctx.check(m.ctx.lib.hmcx_mlp_masks(m.ctx.h, m.code, B, n_mid, 5, 3, k & 0xFFFFFFFF,
+                                                 (nat.MLP_MASK_SLOT0 + f) & 0xFFFFFFFF, nat.ptr(out[f])),
+                        "hmcx_mlp_masks")
+        return out.cpu().numpy()
+
+    runs = []
+    for provider in (None, api_masks):
+        s = sghmc(m, start, **kw)
+        s.mask_provider = provider
+        s.trace, s.out = [], io.StringIO()
+        post, _ = s.sample(epochs=2, burnin=1, batch_size=B, X_train=X, y_train=y)
+        runs.append((post, [t["L"] for t in s.trace], [t["accepted"] for t in s.trace]))
+    (p1, L1, a1), (p2, L2, a2) = runs
+    assert L1 == L2 and a1 == a2 and max(L1) >= 2
+    for k in p1:
+        np.testing.assert_array_equal(p1[k], p2[k])
