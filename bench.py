@@ -394,6 +394,7 @@ def bench(args, parallel):
         local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    parallel.init_rccl(dev)          # data-plane RCCL communicator through libhmcx (no-op at one rank)
     from dropout_hamiltonian_montecarlo_amd.hamiltonian.models.gpu.softmax import softmax
     from dropout_hamiltonian_montecarlo_amd.hamiltonian.inference.gpu.sghmc import sghmc
 
@@ -471,7 +472,8 @@ def bench(args, parallel):
 
     # cross-chain diagnostics (untimed, after the timed region): DIAG_STEPS more steps of the same
     # chain return the state after every step (out_trace); per-parameter Welford mean / M2 and a
-    # thinned trace of every chain travel in ONE all-gather (RCCL over xGMI); rank 0 reports R̂,
+    # thinned trace of every chain travel in ONE all-gather (RCCL over xGMI through libhmcx's
+    # hmcx_allgather_chain_stats, parallel.py); rank 0 reports R̂,
     # split-R̂ and ESS per parameter.  The timed steps' log-likelihood trace is gathered too.
     s.record_steps = True
     wf = parallel.Welford((1, P))
@@ -545,7 +547,7 @@ def bench(args, parallel):
                         "source": "%d untimed steps after the timed region, state after every step; Welford "
                                   "mean/M2 per parameter and every %dth draw, one all_gather" % (DIAG_STEPS, DIAG_THIN),
                         "rhat_ll": float(np.ravel(diag["rhat"])[0]), "ess_ll": float(np.ravel(diag["ess"])[0]),
-                        "gather": "torch.distributed all_gather (%s)" % (parallel.backend_name() if parallel.dist.is_initialized() else "local")},
+                        "gather": parallel.backend_name() if parallel.dist.is_initialized() else "local"},
         "cpu_baseline": None,
         "chain_batched": batched,
         "mlp": mlp_out,

@@ -96,7 +96,9 @@ EXPORTS = ("hmcx_version", "hmcx_create", "hmcx_destroy", "hmcx_last_error", "hm
            "hmcx_sgld_run", "hmcx_hmc_mvn_run", "hmcx_mlp_masks", "hmcx_mlp_grad", "hmcx_mlp_loss",
            "hmcx_mlp_sghmc_run", "hmcx_logistic_grad", "hmcx_logistic_loglik", "hmcx_logistic_predict",
            "hmcx_sumsq", "hmcx_sgd_run", "hmcx_hmc_run", "hmcx_axpy", "hmcx_mvn_eval",
-           "hmcx_clear_abort", "hmcx_philox_schedule", "hmcx_host_wait", "hmcx_set_mlp_fuse")
+           "hmcx_clear_abort", "hmcx_philox_schedule", "hmcx_host_wait", "hmcx_set_mlp_fuse",
+           "hmcx_comm_unique_id", "hmcx_comm_init", "hmcx_comm_destroy", "hmcx_allgather_chain_stats",
+           "hmcx_allreduce_f64")
 
 _lib = None
 _lock = threading.Lock()
@@ -158,6 +160,12 @@ def load_library():
         lib.hmcx_mlp_sghmc_run.argtypes = [c_void_p, ctypes.POINTER(MlpSghmcArgs)]
         if hasattr(lib, "hmcx_set_mlp_fuse"):          # absent in older builds loaded for A/B runs
             lib.hmcx_set_mlp_fuse.argtypes = [c_void_p, c_int]
+        if hasattr(lib, "hmcx_comm_init"):
+            lib.hmcx_comm_unique_id.argtypes = [c_void_p]
+            lib.hmcx_comm_init.argtypes = [c_void_p, c_int, c_int, c_void_p, ctypes.POINTER(c_void_p)]
+            lib.hmcx_comm_destroy.argtypes = [c_void_p]
+            lib.hmcx_allgather_chain_stats.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_uint64]
+            lib.hmcx_allreduce_f64.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_uint64, c_int]
         lib.hmcx_logistic_grad.argtypes = [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
                                            c_void_p, c_void_p, c_double, c_void_p, c_void_p]
         lib.hmcx_logistic_loglik.argtypes = [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int,

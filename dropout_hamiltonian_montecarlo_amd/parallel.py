@@ -8,12 +8,19 @@ posteriors concatenated; all broken as shipped) becomes:
   chain_block) — the samplers key their Philox streams by chain0 + c, so blocks never overlap;
   each rank samples its chains on its own GPU with NO communication while sampling
   (embarrassingly parallel, SURVEY §8e);
-* after sampling, ONE all-gather (RCCL over xGMI when the backend is "nccl", gloo on CPU) moves
-  the per-chain summaries — per-parameter mean and Welford M2 over the draws, and a thinned
-  trace (the reference concatenates whole posteriors, sghmc_multicore.py:86-94) — to
-  every rank; rank 0 computes per-parameter R̂ / split-R̂ and ESS.
+* after sampling, ONE all-gather moves the per-chain summaries — per-parameter mean and Welford M2
+  over the draws, and a thinned trace (the reference concatenates whole posteriors,
+  sghmc_multicore.py:86-94) — to every rank; rank 0 computes per-parameter R̂ / split-R̂ and ESS.
 
-Rendezvous: torch.distributed env:// (RANK, WORLD_SIZE, MASTER_ADDR=127.0.0.1, MASTER_PORT).
+Two planes:
+
+* control — torch.distributed over gloo (env:// rendezvous: RANK, WORLD_SIZE, MASTER_ADDR=127.0.0.1,
+  MASTER_PORT): barriers, the uneven-block counts, and handing rank 0's RCCL unique id to the
+  other ranks.  No tensor data of the run goes through it on a GPU run;
+* data — RCCL over xGMI through libhmcx's C ABI (init_rccl → hmcx_comm_init; gather_summaries /
+  gather_traces → hmcx_allgather_chain_stats; allreduce_max / allreduce_sum → hmcx_allreduce_f64),
+  on the hmcx context's stream.  Without a GPU (CPU tests) or with HMCX_DIST_BACKEND=gloo (several
+  ranks sharing one GPU, which RCCL refuses) the same functions run over gloo.
 """
 import os
 
@@ -24,38 +31,97 @@ import torch.distributed as dist
 from . import diagnostics
 
 
-def init(backend=None):
-    """Initialise the process group from the environment; returns (rank, world, local_rank).
-    Backend: `backend`, else $HMCX_DIST_BACKEND, else "nccl" (RCCL) with a GPU and "gloo" without.
-    One rank normally runs without a process group; HMCX_DIST_FORCE=1 creates it anyway (a world-1
-    RCCL communicator: the collective path of the multi-GPU run, exercised on one GPU)."""
+_rccl = None          # the data-plane communicator (RcclComm) once init_rccl has made it
+
+
+def init(backend="gloo"):
+    """Initialise the control-plane process group (gloo) from the environment; returns (rank, world,
+    local_rank).  One rank normally runs without a process group; HMCX_DIST_FORCE=1 creates it anyway
+    (world 1: the collective path of the multi-GPU run, exercised on one GPU)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
     force = os.environ.get("HMCX_DIST_FORCE") == "1"
     if (world > 1 or force) and not dist.is_initialized():
-        if backend is None:
-            backend = os.environ.get("HMCX_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
-        if backend == "nccl":
-            torch.cuda.set_device(local)
-            dist.init_process_group(backend, device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
+        dist.init_process_group(backend)
     return rank, world, local
 
 
+class RcclComm:
+    """An RCCL communicator owned by libhmcx (include/hmcx.h hmcx_comm_*)."""
+
+    def __init__(self, ctx, handle, world, rank):
+        self.ctx, self.h, self.world, self.rank = ctx, handle, world, rank
+
+    def allgather(self, x):
+        """x: device float64 tensor [n] → [world, n] (rank order)."""
+        from ._native import ptr
+        x = x.contiguous()
+        out = torch.empty((self.world,) + tuple(x.shape), dtype=torch.float64, device=x.device)
+        self.ctx.bind_stream()
+        self.ctx.check(self.ctx.lib.hmcx_allgather_chain_stats(self.ctx.h, self.h, ptr(x), ptr(out), x.numel()),
+                       "hmcx_allgather_chain_stats")
+        return out
+
+    def allreduce(self, x, op):
+        from ._native import ptr
+        x = x.contiguous()
+        out = torch.empty_like(x)
+        self.ctx.bind_stream()
+        self.ctx.check(self.ctx.lib.hmcx_allreduce_f64(self.ctx.h, self.h, ptr(x), ptr(out), x.numel(),
+                                                       0 if op == "sum" else 1), "hmcx_allreduce_f64")
+        return out
+
+    def destroy(self):
+        if self.h is not None and self.h.value:
+            self.ctx.lib.hmcx_comm_destroy(self.h)
+        self.h = None
+
+
+def init_rccl(device):
+    """Create the data-plane RCCL communicator through libhmcx: rank 0 makes the unique id
+    (hmcx_comm_unique_id), the control plane hands it to every rank, each rank calls hmcx_comm_init
+    on its own GPU.  No-op without a process group or with HMCX_DIST_BACKEND=gloo (ranks sharing a
+    GPU, which RCCL refuses); returns the communicator or None."""
+    global _rccl
+    if _rccl is not None or not dist.is_initialized() or os.environ.get("HMCX_DIST_BACKEND") == "gloo":
+        return _rccl
+    import ctypes
+    from . import _native as nat
+    world, rank = dist.get_world_size(), dist.get_rank()
+    buf = ctypes.create_string_buffer(128)
+    if rank == 0:
+        rc = nat.load_library().hmcx_comm_unique_id(buf)
+        if rc != 0:
+            raise nat.HmcxError("hmcx_comm_unique_id failed (%d)" % rc)
+    obj = [buf.raw if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    buf = ctypes.create_string_buffer(obj[0], 128)
+    ctx = nat.context(device)
+    h = ctypes.c_void_p()
+    ctx.check(ctx.lib.hmcx_comm_init(ctx.h, world, rank, buf, ctypes.byref(h)), "hmcx_comm_init")
+    _rccl = RcclComm(ctx, h, world, rank)
+    return _rccl
+
+
 def finalize():
-    """Tear down the process group on every rank (each rank calls this, also when it has nothing
-    to report)."""
+    """Tear down the data-plane communicator and the process group on every rank (each rank calls
+    this, also when it has nothing to report)."""
+    global _rccl
+    if _rccl is not None:
+        torch.cuda.synchronize(_rccl.ctx.device)
+        _rccl.destroy()
+        _rccl = None
     if dist.is_initialized():
         dist.destroy_process_group()
 
 
 def backend_name():
+    if _rccl is not None:
+        return "RCCL over xGMI (libhmcx hmcx_allgather_chain_stats)"
     if not dist.is_initialized():
         return "none"
-    b = dist.get_backend()
-    return "nccl (RCCL over xGMI)" if b == "nccl" else b
+    return dist.get_backend()
 
 
 def chain_block(n_chains, rank, world):
@@ -79,27 +145,23 @@ def barrier():
         dist.barrier()
 
 
-def _dev(device):
-    """Collectives run on `device` with RCCL; gloo takes host tensors."""
-    if dist.is_initialized() and dist.get_backend() == "gloo":
-        return torch.device("cpu")
-    return device
+def _reduce(x, op, device):
+    if not dist.is_initialized():
+        return float(x)
+    if _rccl is not None:
+        t = torch.tensor([float(x)], dtype=torch.float64, device=_rccl.ctx.device)
+        return float(_rccl.allreduce(t, op).item())
+    t = torch.tensor([float(x)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
+    return float(t.item())
 
 
 def allreduce_max(x, device=None):
-    if not dist.is_initialized():
-        return float(x)
-    t = torch.tensor([float(x)], dtype=torch.float64, device=_dev(device))
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
+    return _reduce(x, "max", device)
 
 
 def allreduce_sum(x, device=None):
-    if not dist.is_initialized():
-        return float(x)
-    t = torch.tensor([float(x)], dtype=torch.float64, device=_dev(device))
-    dist.all_reduce(t, op=dist.ReduceOp.SUM)
-    return float(t.item())
+    return _reduce(x, "sum", device)
 
 
 def gather_objects(obj):
@@ -119,19 +181,18 @@ def gather_traces(local_traces, device=None):
     x = torch.as_tensor(np.ascontiguousarray(local_traces), dtype=torch.float64)
     if not dist.is_initialized():
         return x.numpy()
-    device = _dev(device)
     world = dist.get_world_size()
-    counts = torch.tensor([x.shape[0]], dtype=torch.int64, device=device)
-    allc = [torch.empty_like(counts) for _ in range(world)]
-    dist.all_gather(allc, counts)
-    allc = [int(c.item()) for c in allc]
+    allc = gather_objects(int(x.shape[0]))                       # control plane
     cmax = max(allc)
     if x.shape[0] < cmax:
         x = torch.cat([x, x.new_zeros((cmax - x.shape[0],) + tuple(x.shape[1:]))], dim=0)
-    x = x.to(device) if device is not None else x
-    out = [torch.empty_like(x) for _ in range(world)]
-    dist.all_gather(out, x)
-    return torch.cat([o[:c] for o, c in zip(out, allc)], dim=0).cpu().numpy()
+    if _rccl is not None:                                        # data plane: one RCCL all-gather
+        allx = _rccl.allgather(x.to(_rccl.ctx.device).reshape(-1)).reshape((world,) + tuple(x.shape)).cpu()
+        out = list(allx)
+    else:
+        out = [torch.empty_like(x) for _ in range(world)]
+        dist.all_gather(out, x)
+    return torch.cat([o[:c] for o, c in zip(out, allc)], dim=0).numpy()
 
 
 class Welford:

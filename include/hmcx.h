@@ -375,6 +375,26 @@ int hmcx_mlp_sghmc_run(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* a);
  * exchange; one more launch per forward) — the recovery path after out_abort; on = 1 restores it. */
 int hmcx_set_mlp_fuse(hmcx_ctx* ctx, int on);
 
+/* ------------------------------------------------------------------ cross-rank gather (RCCL)
+ * Replaces the reference's multi-chain result collection (hamiltonian/inference/cpu/
+ * sghmc_multicore.py:86-94: Pool.map of per-worker posteriors, concatenated on the parent;
+ * SURVEY §8(e)): one process per GPU samples its own chains with no communication, then ONE
+ * all-gather over RCCL (xGMI) moves every rank's per-chain summaries (per-parameter Welford mean /
+ * M2 and a thinned trace, packed by the caller) to every rank.  The communicator is created here
+ * from a unique id that rank 0 makes (hmcx_comm_unique_id) and the launcher hands to every rank
+ * (any out-of-band channel: the bench uses the torch.distributed gloo store).  Collectives run on
+ * the context's stream and return once enqueued. */
+typedef struct hmcx_comm hmcx_comm;
+#define HMCX_COMM_ID_BYTES 128
+int hmcx_comm_unique_id(void* id /* host [HMCX_COMM_ID_BYTES] */);
+int hmcx_comm_init(hmcx_ctx* ctx, int nranks, int rank, const void* id /* host */, hmcx_comm** out);
+int hmcx_comm_destroy(hmcx_comm* comm);
+/* recv[r][0..count) = send of rank r (device doubles; recv holds nranks·count) */
+int hmcx_allgather_chain_stats(hmcx_ctx* ctx, hmcx_comm* comm, const double* send, double* recv, uint64_t count);
+/* recv = elementwise sum (op 0) or max (op 1) over the ranks of send (device doubles): the bench's
+ * leapfrog total and max-over-ranks time */
+int hmcx_allreduce_f64(hmcx_ctx* ctx, hmcx_comm* comm, const double* send, double* recv, uint64_t count, int op);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,8 +1,10 @@
-"""The collective path of the multi-GPU bench on real hardware: bench.py launched by torchrun with
-one rank and HMCX_DIST_FORCE=1, so the process group is an RCCL ("nccl") communicator and the
-timing max/sum reductions and the per-parameter summary all-gather go through RCCL on the GPU
-(parallel.init, gather_summaries).  N > 1 ranks need one GPU each (the driver's 8-GPU run); the
-N = 2 logic itself is covered by the gloo tests in tests/test_parallel_cpu.py."""
+"""The collective path of the multi-GPU bench on real hardware.  The data collectives are RCCL
+through libhmcx's C ABI (include/hmcx.h hmcx_comm_* / hmcx_allgather_chain_stats /
+hmcx_allreduce_f64); torch.distributed (gloo) is only the control plane.  bench.py launched by
+torchrun with one rank and HMCX_DIST_FORCE=1 runs the timing max/sum reductions and the
+per-parameter summary all-gather through that communicator on the GPU.  N > 1 ranks need one GPU
+each (the driver's 8-GPU run); the N = 2 logic itself is covered by the gloo tests in
+tests/test_parallel_cpu.py and tests/test_bench_launch.py."""
 import json
 import os
 import socket
@@ -22,6 +24,33 @@ def _free_port():
         return s.getsockname()[1]
 
 
+def test_comm_c_abi_world1():
+    """hmcx_comm_unique_id → hmcx_comm_init (1 rank) → all-gather / sum / max → destroy, on the
+    context's stream."""
+    import ctypes
+    import torch
+    from dropout_hamiltonian_montecarlo_amd import _native as nat
+    ctx = nat.context(torch.device("cuda:0"))
+    buf = ctypes.create_string_buffer(128)
+    assert ctx.lib.hmcx_comm_unique_id(buf) == 0
+    h = ctypes.c_void_p()
+    ctx.check(ctx.lib.hmcx_comm_init(ctx.h, 1, 0, buf, ctypes.byref(h)), "hmcx_comm_init")
+    try:
+        x = torch.arange(1000, dtype=torch.float64, device="cuda:0") * 0.5
+        out = torch.empty(1000, dtype=torch.float64, device="cuda:0")
+        ctx.check(ctx.lib.hmcx_allgather_chain_stats(ctx.h, h, nat.ptr(x), nat.ptr(out), 1000), "allgather")
+        for op in (0, 1):
+            red = torch.empty(1000, dtype=torch.float64, device="cuda:0")
+            ctx.check(ctx.lib.hmcx_allreduce_f64(ctx.h, h, nat.ptr(x), nat.ptr(red), 1000, op), "allreduce")
+            torch.cuda.synchronize()
+            assert torch.equal(red, x)
+        torch.cuda.synchronize()
+        assert torch.equal(out, x)
+        assert ctx.lib.hmcx_comm_init(ctx.h, 1, 3, buf, ctypes.byref(ctypes.c_void_p())) != 0   # bad rank
+    finally:
+        assert ctx.lib.hmcx_comm_destroy(h) == 0
+
+
 def test_bench_world1_through_rccl():
     port = str(_free_port())
     env = dict(os.environ, HMCX_DIST_FORCE="1")
@@ -34,7 +63,7 @@ def test_bench_world1_through_rccl():
     line = json.loads(r.stdout.strip().splitlines()[-1])
     assert line["n_gpus"] == 1 and line["value"] > 0
     diag = line["diagnostics"]
-    assert "nccl" in diag["gather"], diag["gather"]
+    assert "hmcx_allgather_chain_stats" in diag["gather"], diag["gather"]
     pp = diag["per_parameter"]
     assert pp["chains"] == 1 and pp["params"] == 7850
     assert 0.5 < pp["rhat"]["median"] < 2.0
