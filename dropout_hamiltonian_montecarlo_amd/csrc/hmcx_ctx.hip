@@ -510,6 +510,7 @@ int hmcx_destroy(hmcx_ctx* ctx) {
   if (ctx->abort_host) (void)hipHostFree(ctx->abort_host);
   if (ctx->abort_dev) (void)hipFree(ctx->abort_dev);
   if (ctx->mlp_abort_dev) (void)hipFree(ctx->mlp_abort_dev);
+  if (ctx->sgld_abort_dev) (void)hipFree(ctx->sgld_abort_dev);
   if (ctx->zeros_dev) (void)hipFree(ctx->zeros_dev);
   if (ctx->gx_arena) (void)hipFree(ctx->gx_arena);
   for (auto& g : ctx->graveyard) {
@@ -894,6 +895,14 @@ int hmcx_sgld_run(hmcx_ctx* ctx, const hmcx_sampler_args* a) {
   if (!a->pW != !a->pb) return set_error(ctx, HMCX_EINVAL, "sgld: pW and pb must both be set or both NULL");
   if (a->n_steps == 0) return HMCX_OK;
   return run_traced(ctx, a, [ctx](const hmcx_sampler_args* s) {
+    if (sgld_p_eligible(ctx, s)) {
+      // one persistent launch per call; a timed-out hand-off left W / b untouched: the call is re-run
+      // on the three-launch path (same noise, same schedule)
+      bool aborted = false;
+      const int rc = s->dtype == HMCX_F64 ? sgld_p_t<double>(ctx, s, &aborted) : sgld_p_t<float>(ctx, s, &aborted);
+      if (rc || !aborted) return rc;
+      fprintf(stderr, "hmcx: persistent SGLD hand-off timed out; re-running the call on the three-launch path\n");
+    }
     if (sgld_wide_eligible(s))
       return s->dtype == HMCX_F64 ? sgld_wide_t<double>(ctx, s) : sgld_wide_t<float>(ctx, s);
     return s->dtype == HMCX_F64 ? sgld_run_t<double>(ctx, s) : sgld_run_t<float>(ctx, s);

@@ -331,7 +331,7 @@ __global__ void k_wreduce_ll(const double* llp, int n, double* out) {
 // ---------------------------------------------------------------- host
 bool sgld_wide_eligible(const hmcx_sampler_args* s) {
   const char* env = getenv("HMCX_SGLD_WIDE");
-  if (env && env[0] == '0') return false;
+  if (env && env[0] == '0') return false;        // 0: kernel-per-phase; 1: this path; 2: persistent
   if (s->C != 1 || s->K > 64 || s->K < 1 || s->B < 1 || s->D < 1) return false;
   // faster than the kernel-per-phase path for every single-chain shape measured (MNIST D=784,
   // K=10: 18.0 vs 20.5 µs per f64 step; config 5 D=2048, K=38: 26.4 vs 35.1 µs)

@@ -217,13 +217,16 @@ def test_sgld_wide_features_split_forward_vs_oracle(monkeypatch):
     np.testing.assert_allclose(logp_g, logp_r, rtol=1e-10)
 
 
-@pytest.mark.parametrize("K,D,B", [(38, 2048, 500), (10, 131, 77), (64, 300, 40), (17, 8, 5)])
-def test_sgld_wide_path_vs_oracle(K, D, B, monkeypatch):
-    """hmcx_wide.hip (one chain; chosen for 16 < K ≤ 64, forced here for every shape): float64
-    trajectory within rel 1e-9 of the oracle.  Covers BASELINE config 5's shape (D=2048, K=38,
-    B=500), a ragged shape (D not a multiple of the vector width, partial row block), the largest
-    class count and a D smaller than one MFMA k-step group."""
-    monkeypatch.setenv("HMCX_SGLD_WIDE", "1")
+@pytest.mark.parametrize("wide", ["1", "2"], ids=["three-launch", "persistent"])
+@pytest.mark.parametrize("K,D,B", [(38, 2048, 500), (10, 131, 77), (64, 300, 40), (17, 8, 5), (38, 2000, 130)])
+def test_sgld_wide_path_vs_oracle(K, D, B, wide, monkeypatch):
+    """The single-chain SGLD paths for wide shapes, forced here for every shape: hmcx_wide.hip (three
+    launches per step) and hmcx_sgld_p.hip (one persistent launch per call, the default at config 5).
+    float64 trajectory within rel 1e-9 of the oracle, printed loss lines identical.  Covers BASELINE
+    config 5's shape (D=2048, K=38, B=500), a ragged shape (D not a multiple of the vector width,
+    partial row block), the largest class count, a D smaller than one MFMA k-step group, and a
+    persistent grid with ragged row and feature blocks."""
+    monkeypatch.setenv("HMCX_SGLD_WIDE", wide)
     c = dict(kind="sgld", N=2 * B, B=B, D=D, K=K, alpha=0.01, step_size=1e-4, path_length=1.0,
              burnin=1, epochs=2, data_seed=41, np_seed=2, rng_seed=3)
     post_r, logp_r, _, log_r = _run_oracle(c)
@@ -234,15 +237,16 @@ def test_sgld_wide_path_vs_oracle(K, D, B, monkeypatch):
     assert [l for l in log_g.splitlines() if "loss" in l] == [l for l in log_r.splitlines() if "loss" in l]
 
 
+@pytest.mark.parametrize("wide", ["1", "2"], ids=["three-launch", "persistent"])
 @pytest.mark.parametrize("dtype", ["f64", "f32"])
-def test_sgld_wide_equals_kernel_path_philox(dtype, monkeypatch):
-    """Config 5 (D=2048, K=38, B=500): the wide path and the kernel-per-phase path consume the same
+def test_sgld_wide_equals_kernel_path_philox(dtype, wide, monkeypatch):
+    """Config 5 (D=2048, K=38, B=500): the wide paths and the kernel-per-phase path consume the same
     Philox noise, so they produce the same trajectory up to summation order (f64: rel 1e-9;
     f32: rel 1e-4 + 1e-7 absolute)."""
     c = dict(kind="sgld", N=1500, B=500, D=2048, K=38, alpha=0.01, step_size=1e-4, path_length=1.0,
              burnin=0, epochs=2, data_seed=43, np_seed=0, rng_seed=0)
     dt = torch.float64 if dtype == "f64" else torch.float32
-    monkeypatch.setenv("HMCX_SGLD_WIDE", "1")
+    monkeypatch.setenv("HMCX_SGLD_WIDE", wide)
     pw, lw, _, _ = _run_gpu(c, dtype=dt, noise="philox", seed=9)
     monkeypatch.setenv("HMCX_SGLD_WIDE", "0")
     ps, ls, _, _ = _run_gpu(c, dtype=dt, noise="philox", seed=9)
@@ -341,3 +345,20 @@ def test_sghmc_step_api_returns_momentum(path):
         assert any(acc) and not all(acc), acc            # both branches exercised
     finally:
         m.ctx.set_sghmc_path(0)
+
+
+def test_sgld_persistent_timeout_reruns_call(monkeypatch, capfd):
+    """HMCX_SGLD_FORCE_ABORT=1: the persistent SGLD launch's last workgroup leaves at step 0, the others
+    time out in their polls, W / b stay untouched and hmcx_sgld_run re-runs the call on the three-launch
+    path — the trajectory is still the oracle's (rel 1e-9), the printed loss lines identical."""
+    monkeypatch.setenv("HMCX_SGLD_WIDE", "2")
+    monkeypatch.setenv("HMCX_SGLD_FORCE_ABORT", "1")
+    c = dict(kind="sgld", N=1000, B=500, D=2048, K=38, alpha=0.01, step_size=1e-4, path_length=1.0,
+             burnin=1, epochs=1, data_seed=41, np_seed=2, rng_seed=3)
+    post_r, logp_r, _, log_r = _run_oracle(c)
+    post_g, logp_g, _, log_g = _run_gpu(c)
+    assert "persistent SGLD hand-off timed out" in capfd.readouterr().err
+    for v in ("weights", "bias"):
+        np.testing.assert_allclose(post_g[v], post_r[v], rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(logp_g, logp_r, rtol=1e-10)
+    assert [l for l in log_g.splitlines() if "loss" in l] == [l for l in log_r.splitlines() if "loss" in l]
