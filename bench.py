@@ -428,9 +428,13 @@ def bench(args, parallel):
         done += n
     torch.cuda.synchronize()
 
-    # timed region: exactly args.steps steps per chain
-    s.trace = []
+    # timed region: exactly args.steps steps per chain.  The per-step trace dicts of sample() are not
+    # kept here (the leapfrog count comes from the path lengths each call returns); HMCX_BENCH_TRACE=1
+    # keeps them as before (host-overhead A/B)
+    keep_trace = os.environ.get("HMCX_BENCH_TRACE") == "1"
+    s.trace = [] if keep_trace else None
     lls = []
+    Ls = []
     n_calls = 0
     model.ctx.set_timing(True)        # HIP events around each run's kernels, on the launch stream
     parallel.barrier()
@@ -444,12 +448,16 @@ def bench(args, parallel):
         n = min(CHUNK, args.steps - done)
         h = enqueue(n, args.warmup + done)
         if pending is not None:
-            lls.append(s._collect(pending).ll)
+            res = s._collect(pending)
+            lls.append(res.ll)
+            Ls.append(res.L)
         pending = h
         done += n
         n_calls += 1
     t_enq = time.perf_counter()
-    lls.append(s._collect(pending).ll)
+    res = s._collect(pending)
+    lls.append(res.ll)
+    Ls.append(res.L)
     t_col = time.perf_counter()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
@@ -465,7 +473,9 @@ def bench(args, parallel):
     kern_ms, kern_n = model.ctx.get_timing()
     model.ctx.set_timing(False)
 
-    lf_local = float(sum(max(0.0, t["L"] - 1) for t in s.trace))
+    lf_local = float(sum(np.maximum(0.0, np.asarray(L) - 1).sum() for L in Ls))
+    if keep_trace:
+        assert lf_local == float(sum(max(0.0, t["L"] - 1) for t in s.trace))
     t_max = parallel.allreduce_max(elapsed, device=dev)
     lf_total = parallel.allreduce_sum(lf_local, device=dev)
     value = lf_total / t_max * P

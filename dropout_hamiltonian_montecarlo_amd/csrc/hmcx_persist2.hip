@@ -52,6 +52,7 @@ struct Q2Args {
   void* W; void* b;
   char* arena;                              // granule arena (zeroed per call)
   int oXA, oXD, oXB, oXW, oXS;              // region offsets in granules
+  int oXC;                                  // commit round: one granule per workgroup
   int arena_bytes;
   int pad;                                  // line-aligned producer blocks (HMCX_P2_PAD, default on)
   unsigned ep0;                             // first round epoch of this launch (unique in the arena's life)
@@ -856,9 +857,18 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
   }
   prof.stamp(0);
   prof.flush();
-  // ---- committed state: owners write their weights, workgroup 0 the bias — unless a member timed
-  //      out (then no workgroup can have passed the last accept round, which needs every member's
-  //      write-through partial: an aborted launch leaves W/b as they were)
+  // ---- commit round: every workgroup publishes a 'done' granule and waits for all G before it
+  //      writes its slice.  A member that timed out anywhere never publishes, so every other member
+  //      times out here too: either every workgroup writes its slice of W/b or none does (checking
+  //      the abort word right before the stores alone left a window — members can see a late
+  //      granule at different times, e.g. under a misplaced team, HMCX_P2_XMAP=2)
+  ++ep;
+  if (tid == 0) put(rs, a.oXC + bid, 1.0, ep);
+  {
+    const bool ok = gather_st(rs, a.oXC, 1, G, 1, [](int) { return 0; }, ep, a.abort_flag, [](int, double) {});
+    if (!all_ok(ok, ish)) return;
+  }
+  // ---- committed state: owners write their weights, workgroup 0 the bias
   if (__hip_atomic_load(a.abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
   verdict.done = true;
   if (own) reinterpret_cast<T*>(a.W)[e_own] = wv;
@@ -932,7 +942,8 @@ int sghmc_p2_t(hmcx_ctx* ctx, const hmcx_sampler_args* s, const PersistPlan2& pl
   const long nXA = 2L * G * pl.Br * KC, nXD = 2L * G * p2_pad(KC + 1 + pl.Ro * KC, pad),
              nXB = 2L * G * p2_pad(KC + 1 + pl.Bf * KC, pad), nXW = 2L * G * p2_pad(pl.Fo * KC, pad),
              nXS = 2L * G * (pad ? 8 : 4);
-  const long ngran = nXA + nXD + nXB + nXW + nXS + 1;
+  const long nXC = G;
+  const long ngran = nXA + nXD + nXB + nXW + nXS + nXC + 1;
   if (ngran * 16 > 0x7fffffffL) return set_error(ctx, HMCX_EUNSUPPORTED, "persistent SGHMC: arena too large");
   int rc = abort_precheck(ctx);                  // an earlier launch's timeout, before enqueueing more
   if (rc) return rc;
@@ -950,6 +961,7 @@ int sghmc_p2_t(hmcx_ctx* ctx, const hmcx_sampler_args* s, const PersistPlan2& pl
   char* arena = ctx->gx_arena;
   unsigned rounds = 0;                           // ≤ 5 epochs per leapfrog iteration (it = -1 … L-1, accept)
   for (size_t i = 0; i < n; ++i) rounds += 5u * (unsigned)(std::max(s->n_iter[i], 0) + 2);
+  rounds += 1;                                   // the commit round
   unsigned ep0 = 1;
   if ((rc = gx_epochs(ctx, rounds, &ep0))) return rc;
   Q2Args a{};
@@ -997,6 +1009,7 @@ int sghmc_p2_t(hmcx_ctx* ctx, const hmcx_sampler_args* s, const PersistPlan2& pl
   a.arena = arena;
   a.oXA = 0; a.oXD = (int)nXA; a.oXB = (int)(nXA + nXD); a.oXW = (int)(nXA + nXD + nXB);
   a.oXS = (int)(nXA + nXD + nXB + nXW);
+  a.oXC = (int)(nXA + nXD + nXB + nXW + nXS);
   a.arena_bytes = (int)(ngran * 16);
   a.ep0 = ep0;
   a.pad = pad;

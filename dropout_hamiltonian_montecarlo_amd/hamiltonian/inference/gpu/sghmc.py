@@ -286,6 +286,9 @@ class sghmc(sgmcmc):
             res = RunResult(A.reshape(n_steps, C), acc.reshape(n_steps, C), ll.reshape(n_steps, C),
                             E.reshape(n_steps, C, 2), steps=steps)
         res.mom = h.get('out_mom')
+        Lk = h['keep'][-1]
+        if Lk is not None:                       # Philox: the path lengths the C call drew
+            res.L = Lk[:nsc].copy() if C == 1 else Lk[:nsc].reshape(n_steps, C).copy()
         if self.trace is not None:
             t0 = h['t0']
             if C == 1:                       # Python floats / bools straight from tolist()

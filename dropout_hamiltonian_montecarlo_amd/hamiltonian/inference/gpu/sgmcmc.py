@@ -37,8 +37,9 @@ from dropout_hamiltonian_montecarlo_amd._native import HmcxError, ptr
 class RunResult:
     """Per-step outputs of one libhmcx run call (host numpy arrays)."""
 
-    def __init__(self, A, accepted, ll, E=None, nlp=None, steps=None):
+    def __init__(self, A, accepted, ll, E=None, nlp=None, steps=None, L=None):
         self.A, self.accepted, self.ll, self.E, self.nlp = A, accepted, ll, E, nlp
+        self.L = L              # path length of every step ([n_steps] or [n_steps, C]) when known
         self.steps = steps      # [n_steps, C, P] state after every step (record_steps), else None
         self.mom = None         # device [C, P] momentum returned by the last step (sghmc.step), else None
 
