@@ -141,6 +141,55 @@ class sghmc(sgmcmc):
         return tpl[1]
 
     def _enqueue(self, state, data, rows, eps, rng, batch_size):
+        # the steady state of a Philox-mode sampler (what sample() and bench.py repeat): same data, state
+        # and step count as the previous call on this output slot — refill the rows / step sizes and go
+        q = self.__dict__.get('_quick')
+        if q is not None and not _HOST_PROF and self.noise == 'philox' and not self.record_steps \
+                and not self.__dict__.get('_want_mom'):
+            h = self._enqueue_quick(q, state, data, rows, eps)
+            if h is not None:
+                return h
+        return self._enqueue_full(state, data, rows, eps, rng, batch_size)
+
+    def _enqueue_quick(self, q, state, data, rows, eps):
+        """The cached fast path of _enqueue_full (same struct, same host arrays, same slot rotation):
+        only valid when the data / state tensors and the step count are those the cache was made for."""
+        n_steps = len(rows)
+        W, b = state['weights'], state['bias']
+        if (data[0] is not q['X'] or data[1] is not q['Y'] or W is not q['W'] or b is not q['b']
+                or self.trace is not None):
+            return None
+        ring = self._io_ring
+        i = self._io_next
+        slot = ring[i % self._IO_SLOTS]
+        ac = slot.get('acache')
+        if slot['busy'] is not None or ac is None or ac[1] is not slot['dev'] or n_steps > ac[6] \
+                or ac[0] != q['tkey'] or 36 * n_steps + 4 > slot['cap']:
+            return None
+        self._io_next = i + 1
+        _, _, a, r0b, epb, Lb, _, last_n = ac
+        r0b[:n_steps] = rows
+        epb[:n_steps] = eps
+        base = slot['base']
+        if last_n[0] != n_steps:
+            a.n_steps = n_steps
+            a.out_A, a.out_ll, a.out_E = base, base + 8 * n_steps, base + 16 * n_steps
+            a.out_accepted = base + 32 * n_steps
+            last_n[0] = n_steps
+        a.out_abort = base + 36 * n_steps
+        a.step_base = self.global_step & 0xFFFFFFFF
+        ctx = q['ctx']
+        ctx.bind_stream()
+        ctx.check(ctx.lib.hmcx_sghmc_run(ctx.h, a), "hmcx_sghmc_run")
+        self.global_step += n_steps
+        h = dict(slot=slot, dev=slot['dev'], host=slot['host'], hnp=slot['hnp'], hptr=slot['hptr'],
+                 nbytes=32 * n_steps + 4 * n_steps + 4, n_steps=n_steps, C=1, t0=0, ctx=ctx, out_steps=None,
+                 out_mom=None, args=a, keep=(r0b, epb, None, None, None, None, Lb[:n_steps]))
+        slot['busy'] = h
+        self._inflight.append(h)
+        return h
+
+    def _enqueue_full(self, state, data, rows, eps, rng, batch_size):
         """Prepare the schedule of len(rows) steps and enqueue them (one hmcx_sghmc_run call) without
         waiting: the call copies its outputs into a pinned host buffer behind its kernels (out_host,
         stream-ordered) and records an event behind them; _collect waits on that event only (hmcx_host_wait), so a caller may
@@ -259,6 +308,10 @@ class sghmc(sgmcmc):
                  args=a, keep=(row0, eps_a, n_iter, u, noise_off, noise_d, L_out if philox else None))
         slot['busy'] = h
         self.__dict__.setdefault('_inflight', []).append(h)
+        if fast and C == 1 and out_steps is None and out_mom is None:
+            self._quick = dict(X=Xd, Y=Yd, W=W, b=b, ctx=ctx,
+                               tkey=(Xd.data_ptr(), Yd.data_ptr(), W.data_ptr(), b.data_ptr(), batch_size, C,
+                                     self.path_length, self.seed, self.chain))
         return h
 
     def _collect(self, h):
