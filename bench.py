@@ -46,8 +46,9 @@ def parse():
     ap.add_argument("--path", choices=["auto", "kernels", "persistent"], default="auto")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="CPU-baseline time budget per baseline (0 = skip)")
-    ap.add_argument("--batched-chains", type=int, default=2048,
-                    help="chains per GPU of the secondary chain-batched measurement (0 = skip)")
+    ap.add_argument("--batched-chains", type=int, default=8192,
+                    help="chains per GPU of the secondary chain-batched measurement (0 = skip); the line also "
+                         "reports 2048 chains (round 2's operating point) as a sweep point")
     ap.add_argument("--mlp-steps", type=int, default=40,
                     help="SGHMC steps of the secondary config-3 MLP measurement (0 = skip)")
     ap.add_argument("--sgld-steps", type=int, default=400,
@@ -244,18 +245,19 @@ MLP_P = 256 * 784 + 256 + 256 * 256 + 256 + 10 * 256 + 10          # 269,322
 MLP_FLOP_PER_LEAPFROG = 1.0193e9             # SURVEY §8d "M": minimal-recompute schedule, B = 500
 
 
-def mlp_measure(X, lab, n_steps, rank):
+def mlp_measure(X, lab, n_steps, rank, dtype="f32"):
     """Secondary measurement, BASELINE config 3: MNIST MLP 784-256-256-10 SGHMC, batch 500, one
-    chain, float32 (Chainer's default dtype), device Philox noise and dropout masks, through the
-    fused hmcx_mlp_sghmc_run."""
+    chain, float32 (Chainer's default dtype; dtype="f64" for the parity dtype's figure), device
+    Philox noise and dropout masks, through the fused hmcx_mlp_sghmc_run."""
     import torch
     from dropout_hamiltonian_montecarlo_amd.hamiltonian.models.gpu.mlp import mlp
     from dropout_hamiltonian_montecarlo_amd.hamiltonian.inference.gpu.sghmc import sghmc
-    m = mlp({"alpha": ALPHA}, *MLP_SHAPE, dtype=torch.float32)
+    tdt = torch.float32 if dtype == "f32" else torch.float64
+    m = mlp({"alpha": ALPHA}, *MLP_SHAPE, dtype=tdt)
     s = sghmc(m, m.init_params(1), path_length=5e-3, step_size=EPS, noise="philox", seed=11, chain=rank)
     s.out = io.StringIO()
     state = s._init_state()
-    Xd = torch.as_tensor(X).to(m.device, torch.float32).contiguous()
+    Xd = torch.as_tensor(X).to(m.device, tdt).contiguous()
     yd = torch.as_tensor(lab).to(m.device, torch.int32).contiguous()
     nb = N_DATA // B
     rows = [(i % nb) * B for i in range(n_steps)]
@@ -273,11 +275,11 @@ def mlp_measure(X, lab, n_steps, rank):
     lf = float(sum(max(0.0, t["L"] - 1) for t in s.trace))
     achieved = MLP_FLOP_PER_LEAPFROG * lf / (kms * 1e-3) / 1e12
     out = {"workload": "MNIST MLP 784-256-256-10 SGHMC, batch 500, 1 chain (BASELINE config 3)",
-           "dtype": "f32", "param_dim": MLP_P, "steps": n_steps, "leapfrogs": lf,
+           "dtype": dtype, "param_dim": MLP_P, "steps": n_steps, "leapfrogs": lf,
            "leapfrogs_per_s": lf / dt, "value": lf / dt * MLP_P, "unit": "leapfrog-steps/s x param-dim",
            "accept_rate": float(np.mean(res.accepted)),
-           "roofline": {"bound": "mfma", "achieved": achieved, "peak": MFMA_PEAK_TFLOPS["f32"], "unit": "TFLOP/s",
-                        "frac": achieved / MFMA_PEAK_TFLOPS["f32"], "device_ms": kms,
+           "roofline": {"bound": "mfma", "achieved": achieved, "peak": MFMA_PEAK_TFLOPS[dtype], "unit": "TFLOP/s",
+                        "frac": achieved / MFMA_PEAK_TFLOPS[dtype], "device_ms": kms,
                         "kernel": "all kernels of one hmcx_mlp_sghmc_run call (k_mm GEMMs + step kernels)",
                         "flop_per_leapfrog": MLP_FLOP_PER_LEAPFROG}}
     return out
@@ -508,11 +510,17 @@ def bench(args, parallel):
     if args.batched_chains > 0:
         model.ctx.set_sghmc_path(0)
         batched = batched_chains(model, X, Y, data, args.batched_chains, 24, rank)
+        if args.batched_chains != 2048:       # round 2's operating point, for comparison
+            b2 = batched_chains(model, X, Y, data, 2048, 24, rank)
+            batched["sweep"] = {"2048": {"frac": b2["roofline"]["frac"], "leapfrogs_per_s": b2["leapfrogs_per_s"]},
+                                str(args.batched_chains): {"frac": batched["roofline"]["frac"],
+                                                           "leapfrogs_per_s": batched["leapfrogs_per_s"]}}
         parallel.barrier()
     mlp_out = None
     if args.mlp_steps > 0:
         lab = np.argmax(Y, axis=1)
         mlp_out = mlp_measure(X, lab, args.mlp_steps, rank)
+        mlp_out["f64"] = mlp_measure(X, lab, args.mlp_steps, rank, dtype="f64")   # the parity dtype's cost
         parallel.barrier()
     v_out = None
     if args.sgld_steps > 0:
