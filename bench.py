@@ -193,15 +193,22 @@ def _cpu_baseline(X, Y, budget_s):
             "lf_per_s": lf / t_total}
 
 
+def pmc_file(dtype, path):
+    import glob
+    fs = sorted(glob.glob(os.path.join(REPO, "profiles", "pmc_r[0-9][0-9]_%s_%s.json" % (dtype, path))))
+    return os.path.relpath(fs[-1], REPO) if fs else None
+
+
 def pmc_traffic(dtype, path, leapfrogs_per_launch):
     """Fabric bytes per launch of the dominant kernel, from the committed rocprofv3 PMC run of the
-    driver's call shape (profiles/pmc_r02_<dtype>_<path>.json, tools/gpu_r02_pmc.sh): 2·FETCH_SIZE +
+    driver's call shape (the newest profiles/pmc_rNN_<dtype>_<path>.json, tools/gpu_r02_pmc.sh): 2·FETCH_SIZE +
     WRITE_SIZE of the timed launches (MI355X_MICROARCH.md: FETCH_SIZE counts half of 16-byte
     streaming reads) per leapfrog of those launches, times the leapfrogs of this run's launch — the
     exchange rounds, which carry almost all of the traffic, are per leapfrog."""
-    f = os.path.join(REPO, "profiles", "pmc_r02_%s_%s.json" % (dtype, path))
-    if not os.path.exists(f):
+    f = pmc_file(dtype, path)
+    if f is None:
         return None
+    f = os.path.join(REPO, f)
     with open(f) as fh:
         per_lf = json.load(fh).get("traffic_bytes_per_leapfrog")
     return None if per_lf is None else per_lf * leapfrogs_per_launch
@@ -557,7 +564,7 @@ def bench(args, parallel):
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                      "frac": achieved / peak, "traffic": pmc_traffic(args.dtype, path, lf_local / n_calls),
                      "traffic_source": "PMC 2*FETCH_SIZE+WRITE_SIZE per leapfrog of the driver-shape launch "
-                                       "(profiles/pmc_r02_%s_%s.json) x leapfrogs per launch of this run" % (args.dtype, path),
+                                       "(%s) x leapfrogs per launch of this run" % pmc_file(args.dtype, path),
                      "kernel": ("k_sghmc_p2<%s,10> (one launch per call: %d call(s) of <= %d steps)" % (
                          "double" if args.dtype == "f64" else "float", n_calls, CHUNK)) if path == "persistent"
                      else "kernel-per-phase sequence of each call (%d call(s) of <= %d steps)" % (n_calls, CHUNK),
