@@ -487,6 +487,11 @@ int hmcx_create(int device, hmcx_ctx** out) {
     c->num_cus = ncu;
   if (hipDeviceGetAttribute(&lds, hipDeviceAttributeSharedMemPerBlockOptin, device) == hipSuccess && lds > 0)
     c->lds_max = (size_t)lds;
+  // the Philox schedule of a call is drawn into these: sized for a whole epoch of steps up front, so
+  // a call does not reallocate them (the first call of a new, larger step count did)
+  c->sched_L.reserve(4096);
+  c->sched_n.reserve(4096);
+  c->sched_u.reserve(4096);
   *out = c;
   return HMCX_OK;
 }
