@@ -515,7 +515,6 @@ int hmcx_destroy(hmcx_ctx* ctx) {
   if (ctx->abort_host) (void)hipHostFree(ctx->abort_host);
   if (ctx->abort_dev) (void)hipFree(ctx->abort_dev);
   if (ctx->mlp_abort_dev) (void)hipFree(ctx->mlp_abort_dev);
-  if (ctx->sgld_abort_dev) (void)hipFree(ctx->sgld_abort_dev);
   if (ctx->zeros_dev) (void)hipFree(ctx->zeros_dev);
   if (ctx->gx_arena) (void)hipFree(ctx->gx_arena);
   for (auto& g : ctx->graveyard) {
@@ -551,8 +550,8 @@ int hmcx_clear_abort(hmcx_ctx* ctx) {
 
 int hmcx_set_sghmc_path(hmcx_ctx* ctx, int path) {
   HMCX_GUARD_CTX(ctx);
-  if (path < 0 || path > 3)
-    return set_error(ctx, HMCX_EINVAL, "path must be 0 (auto), 1 (kernels), 2 (persistent 2-D), 3 (row space)");
+  if (path < 0 || path > 2)
+    return set_error(ctx, HMCX_EINVAL, "path must be 0 (auto), 1 (kernels), 2 (persistent)");
   ctx->sghmc_path = path;
   return HMCX_OK;
 }
@@ -862,7 +861,7 @@ int hmcx_sghmc_run(hmcx_ctx* ctx, const hmcx_sampler_args* a_in) {
   if (a->n_steps == 0) return HMCX_OK;
   const bool p2 = sghmc_p2_selected(ctx, a);
   // the 2-D persistent path fills out_host itself (no device abort copy); the others are copied here
-  const bool host_by_kernel = p2 && !(a->dtype == HMCX_F64 && sghmc_rs_selected(ctx, a));
+  const bool host_by_kernel = p2;
   if (a->out_abort && !p2) HMCX_HIP(ctx, hipMemsetAsync(a->out_abort, 0, sizeof(int32_t), ctx->stream));
   if (a->out_trace && p2)   // the persistent kernel stores the trace rows itself
     rc = a->dtype == HMCX_F64 ? sghmc_run_t<double>(ctx, a) : sghmc_run_t<float>(ctx, a);
@@ -900,14 +899,6 @@ int hmcx_sgld_run(hmcx_ctx* ctx, const hmcx_sampler_args* a) {
   if (!a->pW != !a->pb) return set_error(ctx, HMCX_EINVAL, "sgld: pW and pb must both be set or both NULL");
   if (a->n_steps == 0) return HMCX_OK;
   return run_traced(ctx, a, [ctx](const hmcx_sampler_args* s) {
-    if (sgld_p_eligible(ctx, s)) {
-      // one persistent launch per call; a timed-out hand-off left W / b untouched: the call is re-run
-      // on the three-launch path (same noise, same schedule)
-      bool aborted = false;
-      const int rc = s->dtype == HMCX_F64 ? sgld_p_t<double>(ctx, s, &aborted) : sgld_p_t<float>(ctx, s, &aborted);
-      if (rc || !aborted) return rc;
-      fprintf(stderr, "hmcx: persistent SGLD hand-off timed out; re-running the call on the three-launch path\n");
-    }
     if (sgld_wide_eligible(s))
       return s->dtype == HMCX_F64 ? sgld_wide_t<double>(ctx, s) : sgld_wide_t<float>(ctx, s);
     return s->dtype == HMCX_F64 ? sgld_run_t<double>(ctx, s) : sgld_run_t<float>(ctx, s);

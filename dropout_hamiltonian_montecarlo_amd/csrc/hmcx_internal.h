@@ -61,7 +61,6 @@ struct hmcx_ctx {
   unsigned abort_next = 0;
   // fused MLP launches (hmcx_mlp.hip MM_L23): their own abort word, reported per call (out_abort)
   int* mlp_abort_dev = nullptr;
-  int* sgld_abort_dev = nullptr;       // persistent SGLD (hmcx_sgld_p.hip): checked and lowered by its call
   int mlp_nofuse = 0;                  // hmcx_set_mlp_fuse(ctx, 0): the sampler runs unfused
 };
 constexpr int ABORT_SLOTS = 64;
@@ -228,12 +227,9 @@ template <typename T> int sghmc_run_t(hmcx_ctx*, const hmcx_sampler_args*);
 template <typename T> int hmc_run_t(hmcx_ctx*, const hmcx_hmc_args*);
 template <typename T> int axpy_t(hmcx_ctx*, int, int64_t, double, const void*, void*);
 bool sghmc_p2_selected(hmcx_ctx*, const hmcx_sampler_args*);   // hmcx_softmax.hip
-bool sghmc_rs_selected(hmcx_ctx*, const hmcx_sampler_args*);   // hmcx_rowspace.hip
 template <typename T> int sgld_run_t(hmcx_ctx*, const hmcx_sampler_args*);
-bool sgld_wide_eligible(const hmcx_sampler_args*);       // hmcx_wide.hip: one chain, K ≤ 64
+bool sgld_wide_eligible(const hmcx_sampler_args*);       // hmcx_wide.hip: K ≤ 64 (C > 1: K > 16)
 template <typename T> int sgld_wide_t(hmcx_ctx*, const hmcx_sampler_args*);
-bool sgld_p_eligible(hmcx_ctx*, const hmcx_sampler_args*);        // hmcx_sgld_p.hip: one persistent launch
-template <typename T> int sgld_p_t(hmcx_ctx*, const hmcx_sampler_args*, bool* aborted);
 int hmc_mvn_run(hmcx_ctx*, const hmcx_hmc_mvn_args*);
 int mvn_eval(hmcx_ctx*, int, int, const double*, const double*, double, const double*, double*, double*);
 template <typename T> int mlp_grad_t(hmcx_ctx*, const void*, const int32_t*, int, int, int, int,

@@ -1,5 +1,5 @@
-// hmcx_p2x.h — tagged-granule exchange shared by the persistent single-chain SGHMC kernels
-// (hmcx_persist2.hip: 2-D teams; hmcx_rowspace.hip: row-space leapfrog).  Every value travels as
+// hmcx_p2x.h — tagged-granule exchange of the persistent single-chain SGHMC kernel
+// (hmcx_persist2.hip: 2-D teams) and shared DPP reductions.  Every value travels as
 // one 16-byte granule {lo32, epoch, hi32, epoch} written by ONE buffer_store_dwordx4 and re-read
 // until both epoch words match (cdna_hip_programming.md §6 G16, recipe R2); spins are bounded
 // (QTIMEOUT) and raise the context's sticky abort word.

@@ -14,8 +14,4 @@ struct PersistPlan2 {
 PersistPlan2 plan_p2(int B, int D, int K, size_t tsize, int num_cus, size_t lds_max);
 template <typename T> int sghmc_p2_t(hmcx_ctx*, const hmcx_sampler_args*, const PersistPlan2&);
 
-// hmcx_rowspace.hip: f64 single chain, the leapfrog in row space (one all-gather per iteration).
-bool sghmc_rs_selected(hmcx_ctx* ctx, const hmcx_sampler_args* s);
-int sghmc_rs_t(hmcx_ctx* ctx, const hmcx_sampler_args* s);
-
 }  // namespace hmcx

@@ -1418,7 +1418,6 @@ int sghmc_batch_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
 // True when sghmc_run_t serves this call with k_sghmc_p2, which writes out_trace itself.
 bool sghmc_p2_selected(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
   if (s->C != 1 || ctx->sghmc_path == 1) return false;
-  if (sghmc_rs_selected(ctx, s)) return true;                  // hmcx_rowspace.hip stores its trace too
   const size_t ts = s->dtype == HMCX_F64 ? sizeof(double) : sizeof(float);
   return plan_p2(s->B, s->D, s->K, ts, ctx->num_cus, ctx->lds_max).ok;
 }
@@ -1427,9 +1426,6 @@ template <typename T>
 int sghmc_run_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
   const int B = s->B, D = s->D, K = s->K, C = s->C, N = C * K;
   if (C == 1 && ctx->sghmc_path != 1) {   // single chain: persistent kernels
-    if constexpr (sizeof(T) == sizeof(double))
-      if (sghmc_rs_selected(ctx, s)) return sghmc_rs_t(ctx, s);   // row space (hmcx_rowspace.hip)
-    if (ctx->sghmc_path == 3) return set_error(ctx, HMCX_EUNSUPPORTED, "row-space SGHMC: shape not supported");
     const PersistPlan2 p2 = plan_p2(B, D, K, sizeof(T), ctx->num_cus, ctx->lds_max);
     if (p2.ok) return sghmc_p2_t<T>(ctx, s, p2);
     if (ctx->sghmc_path == 2) return set_error(ctx, HMCX_EUNSUPPORTED, "persistent SGHMC: shape not supported");

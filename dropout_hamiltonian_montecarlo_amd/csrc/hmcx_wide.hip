@@ -1,22 +1,26 @@
-// hmcx_wide.hip — single-chain SGLD (any K ≤ 64; designed for BASELINE config 5: PlantVillage-like
-// conv features, D = 2048, K = 38, batch 500), three launches per step.
+// hmcx_wide.hip — SGLD for wide softmax shapes (K ≤ 64 classes; designed for BASELINE config 5:
+// PlantVillage-like conv features, D = 2048, K = 38, batch 500), one or several chains, three
+// launches per step.
 //
 // Mathematics and op order: cpu/sgld.py:31-46 (p = N(0,(2ε)²) then p += −½ε·g, q += p) with the
 // gradient of cpu/softmax.py:38-61 (clip, softmax, diff = y − ŷ, g = −(Xᵀ·diff − αW)), as in the
-// kernel-per-phase path of hmcx_softmax.hip; only the tiling differs.
+// kernel-per-phase path of hmcx_softmax.hip; only the tiling differs.  C chains share the minibatch
+// (W [D][C·K] chain-interleaved, b [C][K], as at the C ABI); every kernel has a chain grid dimension.
 //
-//   k_wfwd   grid (row blocks of 32, D slices of ≤128): the X tile [32 × Dz] and the weight slice
-//            [Dz × 16·KB] are staged through LDS with 16-byte loads, every wave runs all 2·KB MFMA
-//            tiles over a quarter of the slice, the four partials are summed in wave order and the
-//            slice's partial logits go to slab[z][B][16·KB].
-//   k_wsoft  one wave per minibatch row, lane = class: Σ_z slab (fixed order), + b, clip, softmax
-//            by wave butterflies (every lane ends with identical bits), diff = y − ŷ, column-sum and
-//            log-likelihood partials per 4-row block.
-//   k_wgrad  grid = 16-feature tiles: Xᵀ·diff over the whole minibatch on MFMA (rows split over the
-//            four waves, summed in wave order), then the fused SGLD update of the tile's weights;
-//            block 0 also finishes the bias from the column-sum partials.
-// The kernel-per-phase path served this shape with 16-row forward tiles whose epilogue walks the
-// K = 38 classes serially; here the class dimension lives in the lanes.
+//   k_wfwd   grid (row blocks of 32, D slices of ≤ 128, chains): operands straight into registers
+//            (no LDS staging): wave w owns 32 features of the slice, in k-step j lane (lr, lg) holds
+//            feature 32w + 8lg + j of its rows — one batch of loads, then 2·KB·8 MFMAs; the four
+//            waves' partials are summed in wave order into slab[z][c][B][16·KB].
+//   k_wsoft  one wave per minibatch row and chain, lane = class: Σ_z slab (fixed order), + b, clip,
+//            softmax by DPP row reductions + two cross-row shuffles (every lane ends with identical
+//            bits), diff = y − ŷ, column-sum and log-likelihood partials per 4-row block.
+//   k_wgrad  grid (1 + KB·⌈D/16⌉, chains): block 0 finishes the bias from the column sums; block
+//            1 + cls·ntile + t owns feature tile t × class tile cls (16 × 16 weights) and computes
+//            its Xᵀ·diff over the whole minibatch (8 waves split the rows, summed in wave order) —
+//            no cross-workgroup reduction — then updates those weights in place.  Its loads are
+//            issued before the Philox noise is drawn, so the noise hides in their latency.
+// Measured (config 5, f64, one chain, MI355X): 22.8 µs per step against 29.1 for the previous
+// LDS-staged forward + one-workgroup-per-feature-tile gradient.
 #include "hmcx_common.h"
 #include "hmcx_internal.h"
 #include "hmcx_p2x.h"
@@ -26,158 +30,57 @@
 
 namespace hmcx {
 
-constexpr int WTH = 256;        // threads per workgroup (4 waves)
+constexpr int WTH = 256;        // threads per workgroup of k_wfwd / k_wsoft (4 waves)
 constexpr int WRB = 32;         // forward row block
-#ifndef HMCX_WDZ
-#define HMCX_WDZ 128
-#endif
-#ifndef HMCX_GNW
-#define HMCX_GNW 8
-#endif
-constexpr int WDZ = HMCX_WDZ;   // forward D slice (max)
+constexpr int WDZ = 128;        // forward D slice (max): 4 waves × 32 features
 constexpr int WSR = 4;          // rows per k_wsoft workgroup (one per wave)
-constexpr int GNW = HMCX_GNW;   // k_wgrad waves: 8 so that its D/16 workgroups cover every SIMD
+constexpr int GNW = 8;          // k_wgrad waves (rows of the minibatch split over them)
 constexpr int GTH = GNW * 64;
 
 template <typename T> struct WideArgs {
   const T* X; const T* Y; T* W; T* b;
   T* pW; T* pb;                          // non-null: GPU-file momentum update (gpu/sgld.py:11-20)
-  int B, D, K, KP, S, Dz, nSB;           // nSB: k_wsoft blocks
+  int B, D, K, KP, S, Dz, nSB, C;        // nSB: k_wsoft blocks per chain; C: chains
   T* slab; T* diff; T* csp; double* llp;
   T alpha, noise_scale, m_half_eps, clip_hi, clip_lo;
   int want_diff;                         // k_wsoft: 1 = diff + colsum (gradient), 0 = ll only
-  int noise_mode; const double* noise; int64_t noff; int P;
-  uint64_t seed; uint32_t chain, step;
+  int noise_mode; const double* noise; const int64_t* noff;   // BUFFER: noise[noff[c] + e]
+  uint64_t seed; uint32_t chain, step;   // PHILOX: keyed by chain + c
   unsigned long long* prof;              // HMCX_WIDE_PROF: per-workgroup s_memrealtime stamps (WPH each)
   int wt;                                // slab / diff stored write-through (sc1; HMCX_WIDE_WT=0: plain)
 };
 
-// a store that leaves the XCD's L2 (sc1: written through, the line dropped) or a plain one
+// a store that leaves the XCD's L2 (sc1: written through, the line dropped) or a plain one: the
+// slab and diff are read by the next launch on other XCDs, so writing them through shortens the
+// end-of-kernel write-back (1.79 vs 2.22 µs between k_wfwd and k_wsoft)
 template <typename T> __device__ inline void wstore(T* p, T v, int wt) {
   if (wt) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   else *p = v;
 }
 
-constexpr int WPH = 8;                   // stamps per workgroup and launch
+constexpr int WPH = 8;                   // stamps per workgroup and launch (one chain only)
 #define WSTAMP(ph)                                                                                  \
   do {                                                                                              \
     if (a.prof && threadIdx.x == 0)                                                                 \
       a.prof[(size_t)(blockIdx.y * gridDim.x + blockIdx.x) * WPH + (ph)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 
-// ---------------------------------------------------------------- partial logits
+// ---------------------------------------------------------------- partial logits, register operands
 template <typename T, int KB>
 __global__ __launch_bounds__(WTH) void k_wfwd(WideArgs<T> a) {
   using M = mfma16<T>;
   constexpr int KP = 16 * KB;
-  constexpr int XP = WDZ + (sizeof(T) == 8 ? 2 : 1);       // conflict-free row pitches
-  constexpr int WP = KP + (sizeof(T) == 8 ? 2 : 1);
-  __shared__ __align__(16) T Xs[WRB * XP];
-  constexpr int WSN = WDZ * WP > 4 * WRB * KP ? WDZ * WP : 4 * WRB * KP;   // also the reduction area
-  __shared__ __align__(16) T Ws[WSN];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lg = lane >> 4;
-  const int m0 = blockIdx.x * WRB, z = blockIdx.y;
-  const int dlo = min(a.D, z * a.Dz), dhi = min(a.D, dlo + a.Dz), nd = dhi - dlo;
-  const int nrow = min(WRB, a.B - m0), K = a.K;
-  WSTAMP(0);
-
-  // ---- stage X[m0:+32, dlo:dhi] and W[dlo:dhi, 0:K], zero padded to [32][WDZ] / [WDZ][KP].
-  // Every load is unconditional (out-of-range slots read a clamped valid address and are zeroed
-  // afterwards) and all of a thread's loads are issued before the first LDS store: one memory
-  // round trip for the whole tile (a load under a branch makes hipcc wait for each one).
-  constexpr int NXE = WRB * WDZ / WTH;                       // X elements per thread
-  constexpr int NWE = WDZ * KP / WTH;                        // W elements per thread
-  const T* xsrc = a.X + (size_t)m0 * a.D + dlo;
-  const T* wsrc = a.W + (size_t)dlo * K;                     // the slice is contiguous: nd·K values
-  T xr[NXE], wr[NWE];
-#pragma unroll
-  for (int u = 0; u < NXE; ++u) {
-    const int e = tid + u * WTH, i = e / WDZ, j = e % WDZ;
-    const bool ok = i < nrow && j < nd;
-    xr[u] = xsrc[ok ? (size_t)i * a.D + j : 0];
-    if (!ok) xr[u] = T(0);
-  }
-#pragma unroll
-  for (int u = 0; u < NWE; ++u) {
-    const int e = tid + u * WTH, i = e / KP, k = e % KP;
-    const bool ok = i < nd && k < K;
-    wr[u] = wsrc[ok ? i * K + k : 0];
-    if (!ok) wr[u] = T(0);
-  }
-  WSTAMP(1);
-#pragma unroll
-  for (int u = 0; u < NXE; ++u) {
-    const int e = tid + u * WTH;
-    Xs[(e / WDZ) * XP + e % WDZ] = xr[u];
-  }
-#pragma unroll
-  for (int u = 0; u < NWE; ++u) {
-    const int e = tid + u * WTH;
-    Ws[(e / KP) * WP + e % KP] = wr[u];
-  }
-  WSTAMP(2);
-  __syncthreads();
-  WSTAMP(3);
-
-  // ---- MFMA: wave w takes k-steps [w·Q, (w+1)·Q) of the slice for all 2·KB tiles
-  const int nks = (nd + 3) / 4, Q = (nks + 3) / 4;
-  const int k0 = wave * Q, k1 = min(nks, k0 + Q);
-  typename M::acc_t acc[2][KB];
-#pragma unroll
-  for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-    for (int nb = 0; nb < KB; ++nb) acc[mt][nb] = M::zero();
-  for (int ks = k0; ks < k1; ++ks) {
-    const int kk = ks * 4 + lg;
-    const T a0 = Xs[lr * XP + kk], a1 = Xs[(16 + lr) * XP + kk];
-    T bv[KB];
-#pragma unroll
-    for (int nb = 0; nb < KB; ++nb) bv[nb] = Ws[kk * WP + nb * 16 + lr];
-#pragma unroll
-    for (int nb = 0; nb < KB; ++nb) {
-      acc[0][nb] = M::fma(a0, bv[nb], acc[0][nb]);
-      acc[1][nb] = M::fma(a1, bv[nb], acc[1][nb]);
-    }
-  }
-  WSTAMP(4);
-  __syncthreads();                                           // staging buffers become the reduction area
-  T* red = Ws;                                               // [4][32][KP] ⊂ Ws
-#pragma unroll
-  for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-    for (int nb = 0; nb < KB; ++nb)
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        red[(wave * WRB + mt * 16 + M::row(lane, q)) * KP + nb * 16 + lr] = acc[mt][nb][q];
-  __syncthreads();
-  WSTAMP(5);
-  T* out = a.slab + ((size_t)z * a.B + m0) * KP;
-  for (int e = tid; e < nrow * KP; e += WTH) {
-    const T v = ((red[e] + red[WRB * KP + e]) + red[2 * WRB * KP + e]) + red[3 * WRB * KP + e];
-    out[e] = v;
-  }
-  WSTAMP(6);
-}
-
-// ---------------------------------------------------------------- partial logits, register operands
-// Same grid and slab as k_wfwd, no LDS staging: wave w owns features [dlo + 32w, dlo + 32w + 32) of
-// the slice, and in k-step j lane (lr, lg) holds feature 32w + 8lg + j (A and B use the same
-// permutation of the k index, so the product is unchanged up to summation order).  Each lane's
-// operands are its rows' 8 consecutive features and those features' weight rows: one batch of
-// loads straight into registers, then 2·KB·8 MFMAs back to back.
-template <typename T, int KB>
-__global__ __launch_bounds__(WTH) void k_wfwd2(WideArgs<T> a) {
-  using M = mfma16<T>;
-  constexpr int KP = 16 * KB;
   __shared__ __align__(16) T red[4 * WRB * KP];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lg = lane >> 4;
-  const int m0 = blockIdx.x * WRB, z = blockIdx.y;
+  const int m0 = blockIdx.x * WRB, z = blockIdx.y, ch = blockIdx.z;
   const int dlo = min(a.D, z * a.Dz), dhi = min(a.D, dlo + a.Dz);
-  const int nrow = min(WRB, a.B - m0), K = a.K;
+  const int nrow = min(WRB, a.B - m0), K = a.K, NW = a.C * K;
+  const T* Wc = a.W + (size_t)ch * K;                        // chain ch's columns of W [D][C·K]
   WSTAMP(0);
   const int f0 = dlo + 32 * wave + 8 * lg;
   const int fsafe = dlo < a.D ? dlo : 0;
   T xa[2][8], wb[8][KB];
+  // every load unconditional (clamped address, zeroed after the batch): one memory round trip
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt) {
     const int i = mt * 16 + lr;
@@ -190,7 +93,7 @@ __global__ __launch_bounds__(WTH) void k_wfwd2(WideArgs<T> a) {
 #pragma unroll
     for (int nb = 0; nb < KB; ++nb) {
       const int c = nb * 16 + lr;
-      wb[j][nb] = a.W[(f0 + j < dhi && c < K) ? (size_t)(f0 + j) * K + c : 0];
+      wb[j][nb] = Wc[(f0 + j < dhi && c < K) ? (size_t)(f0 + j) * NW + c : 0];
     }
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt)
@@ -226,7 +129,7 @@ __global__ __launch_bounds__(WTH) void k_wfwd2(WideArgs<T> a) {
   WSTAMP(3);
   __syncthreads();
   WSTAMP(4);
-  T* out = a.slab + ((size_t)z * a.B + m0) * KP;
+  T* out = a.slab + (((size_t)z * a.C + ch) * a.B + m0) * KP;
   for (int e = tid; e < nrow * KP; e += WTH) {
     const T v = ((red[e] + red[WRB * KP + e]) + red[2 * WRB * KP + e]) + red[3 * WRB * KP + e];
     wstore(out + e, v, a.wt);
@@ -236,9 +139,8 @@ __global__ __launch_bounds__(WTH) void k_wfwd2(WideArgs<T> a) {
 }
 
 // Wave-wide all-reductions: every step combines a symmetric pair of lanes, so all lanes hold the
-// same bits and the result is deterministic.
-// Within each 16-lane row by DPP (g16_*: xor 1, xor 2, half mirror, mirror), then across the four
-// rows by two shuffles (xor 16, xor 32): 2 cross-lane permutes per value instead of 6.
+// same bits and the result is deterministic.  Within each 16-lane row by DPP (g16_*: xor 1, xor 2,
+// half mirror, mirror), then across the four rows by two shuffles (xor 16, xor 32).
 template <typename T> __device__ inline T wave_sum(T v) {
   v = g16_sum2(v);
   v += __shfl_xor(v, 16, 64);
@@ -257,7 +159,7 @@ template <typename T>
 __global__ __launch_bounds__(WTH) void k_wsoft(WideArgs<T> a) {
   __shared__ T cs[WSR][64];
   __shared__ double ll[WSR];
-  const int tid = threadIdx.x, k = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, k = tid & 63, wave = tid >> 6, ch = blockIdx.y;
   const int row = blockIdx.x * WSR + wave, K = a.K, KP = a.KP;
   const bool rv = row < a.B, kv = rv && k < K;
   WSTAMP(0);
@@ -266,19 +168,20 @@ __global__ __launch_bounds__(WTH) void k_wsoft(WideArgs<T> a) {
   if (rv) {
     // Σ_z slab[z] in slab order; the slab loads go out in batches of 16 (unconditional: lanes
     // k ≥ K read their row's padding columns, which exist in every slab)
-    const T* sp = a.slab + (size_t)row * KP + min(k, KP - 1);
+    const size_t zstride = (size_t)a.C * a.B * KP;
+    const T* sp = a.slab + ((size_t)ch * a.B + row) * KP + min(k, KP - 1);
     T xw = T(0);
     for (int s0 = 0; s0 < a.S; s0 += 16) {
       T v[16];
 #pragma unroll
-      for (int q = 0; q < 16; ++q) v[q] = sp[(size_t)min(s0 + q, a.S - 1) * a.B * KP];
+      for (int q = 0; q < 16; ++q) v[q] = sp[(size_t)min(s0 + q, a.S - 1) * zstride];
 #pragma unroll
       for (int q = 0; q < 16; ++q)
         if (s0 + q < a.S) xw = (s0 + q == 0) ? v[q] : xw + v[q];
     }
     if (wave == 0) WSTAMP(1);
     const int kc = min(k, K - 1);
-    const T bk = a.b[kc], yk = a.Y[(size_t)row * K + kc];                                 // unconditional loads
+    const T bk = a.b[ch * K + kc], yk = a.Y[(size_t)row * K + kc];                        // unconditional loads
     const T zz = kv ? clipz(xw + bk, a.clip_hi, a.clip_lo) : (T)-__builtin_inf();          // softmax.py:39-41
     const T m = wave_max(zz);
     const T e = kv ? exp(zz - m) : T(0);                                                  // softmax.py:34
@@ -286,7 +189,7 @@ __global__ __launch_bounds__(WTH) void k_wsoft(WideArgs<T> a) {
     const T y = kv ? yk : T(0);
     if (a.want_diff) {
       d = kv ? y - e / s : T(0);                                                          // softmax.py:52
-      if (k < KP) wstore(a.diff + (size_t)row * KP + k, d, a.wt);
+      if (k < KP) wstore(a.diff + ((size_t)ch * a.B + row) * KP + k, d, a.wt);
     } else {
       const T lse = log(s) + m;                                                           // softmax.py:18-20
       t = kv ? (double)(y * (zz - lse)) : 0.0;
@@ -300,153 +203,33 @@ __global__ __launch_bounds__(WTH) void k_wsoft(WideArgs<T> a) {
   if (a.want_diff) {
     if (tid < K) {
       const T v = ((cs[0][tid] + cs[1][tid]) + cs[2][tid]) + cs[3][tid];
-      a.csp[(size_t)blockIdx.x * K + tid] = v;
+      a.csp[((size_t)ch * a.nSB + blockIdx.x) * K + tid] = v;
     }
   } else if (tid == 0) {
-    a.llp[blockIdx.x] = ((ll[0] + ll[1]) + ll[2]) + ll[3];
+    a.llp[(size_t)ch * a.nSB + blockIdx.x] = ((ll[0] + ll[1]) + ll[2]) + ll[3];
   }
   WSTAMP(3);
 }
 
 template <typename T>
-__device__ inline double wide_noise(const WideArgs<T>& a, uint32_t e) {
-  if (a.noise_mode == HMCX_NOISE_BUFFER) return a.noise[a.noff + e];
-  return (double)philox_normal_t<T>(a.seed, a.chain, a.step, 0u, e);
+__device__ inline double wide_noise(const WideArgs<T>& a, int ch, uint32_t e) {
+  if (a.noise_mode == HMCX_NOISE_BUFFER) return a.noise[a.noff[ch] + e];
+  return (double)philox_normal_t<T>(a.seed, a.chain + (uint32_t)ch, a.step, 0u, e);
 }
 
 // ---------------------------------------------------------------- Xᵀ·diff + SGLD update
-template <typename T, int KB>
-__global__ __launch_bounds__(GTH) void k_wgrad(WideArgs<T> a) {
-  using M = mfma16<T>;
-  constexpr int KP = 16 * KB;
-  constexpr int EPT = (16 * KP + GTH - 1) / GTH;
-  __shared__ T red[GNW][16][KP + 1];
-  __shared__ T csh[GTH];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lg = lane >> 4;
-  const int d0 = blockIdx.x * 16, K = a.K, B = a.B;
-  const bool dok = d0 + lr < a.D;
-  WSTAMP(0);
-
-  // epilogue operands and noise first: their latency overlaps the GEMM
-  T wreg[EPT], zreg[EPT], preg[EPT];
-  const bool gpu_var = a.pW != nullptr;
-  const T* psrc = gpu_var ? a.pW : a.W;                      // pointer-selected: no load under a branch
-#pragma unroll
-  for (int q = 0; q < EPT; ++q) {
-    const int e = tid + q * GTH, i = e / KP, k = e - (e / KP) * KP;
-    const bool ok = e < 16 * KP && d0 + i < a.D && k < K;
-    const uint32_t el = ok ? (uint32_t)((d0 + i) * K + k) : 0u;
-    wreg[q] = a.W[el];                                       // unconditional (clamped) load
-    preg[q] = psrc[el];
-    zreg[q] = (T)wide_noise(a, el);
-    if (!ok) wreg[q] = zreg[q] = preg[q] = T(0);
-  }
-  WSTAMP(1);
-
-  // rows [w·Bw, (w+1)·Bw) of the minibatch on wave w, 16 k-steps of operands in flight; loads are
-  // unconditional (clamped row / feature, zeroed after the load) so they all go out together.
-  // Even and odd k-steps accumulate separately (2·KB independent MFMA chains), summed at the end.
-  constexpr int U = 16;
-  const int nks = (B + 3) / 4, Q = (nks + GNW - 1) / GNW;
-  const int kb0 = wave * Q, kb1 = min(nks, kb0 + Q);
-  const int dcol = dok ? d0 + lr : 0;
-  typename M::acc_t acc[2][KB];
-#pragma unroll
-  for (int nb = 0; nb < KB; ++nb) acc[0][nb] = acc[1][nb] = M::zero();
-  for (int ks = kb0; ks < kb1; ks += U) {
-    T av[U], bv[U][KB];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int row = (ks + u) * 4 + lg;
-      const bool ok = ks + u < kb1 && row < B;
-      const size_t rr = ok ? (size_t)row : 0;
-      av[u] = a.X[rr * a.D + dcol];
-#pragma unroll
-      for (int nb = 0; nb < KB; ++nb) bv[u][nb] = a.diff[rr * KP + nb * 16 + lr];
-      if (!(ok && dok)) av[u] = T(0);
-      if (!ok)
-#pragma unroll
-        for (int nb = 0; nb < KB; ++nb) bv[u][nb] = T(0);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-      for (int nb = 0; nb < KB; ++nb) acc[u & 1][nb] = M::fma(av[u], bv[u][nb], acc[u & 1][nb]);
-  }
-  WSTAMP(2);
-#pragma unroll
-  for (int nb = 0; nb < KB; ++nb)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) acc[0][nb][q] = acc[0][nb][q] + acc[1][nb][q];
-#pragma unroll
-  for (int nb = 0; nb < KB; ++nb)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) red[wave][M::row(lane, q)][nb * 16 + lr] = acc[0][nb][q];
-  __syncthreads();
-  WSTAMP(3);
-
-#pragma unroll
-  for (int q = 0; q < EPT; ++q) {
-    const int e = tid + q * GTH, i = e / KP, k = e - (e / KP) * KP;
-    if (e >= 16 * KP || d0 + i >= a.D || k >= K) continue;
-    T dot = red[0][i][k];
-#pragma unroll
-    for (int w = 1; w < GNW; ++w) dot += red[w][i][k];
-    const T gr = -(dot - a.alpha * wreg[q]);                                  // softmax.py:57-58
-    T p = a.noise_scale * zreg[q];                                            // sgld.py:43-46
-    if (gpu_var) p = p * preg[q];                                             // gpu/sgld.py:18
-    p = p + a.m_half_eps * gr;                                                // sgld.py:37
-    if (gpu_var) a.pW[(size_t)(d0 + i) * K + k] = p;
-    a.W[(size_t)(d0 + i) * K + k] = wreg[q] + p;                              // sgld.py:38
-  }
-  WSTAMP(4);
-
-  if (blockIdx.x == 0) {   // bias: Σ_rows(y − ŷ) from the k_wsoft partials (softmax.py:55,59-60)
-    // group g sums row blocks g, g+4, … in order; 16 loads in flight per batch
-    const int j = tid % 64, g = min(tid / 64, 3), jc = min(j, K - 1);   // groups 0-3 (threads ≥ 256 idle)
-    T s = T(0);
-    for (int r0 = g; r0 < a.nSB; r0 += 64) {
-      T v[16];
-#pragma unroll
-      for (int q = 0; q < 16; ++q) v[q] = a.csp[(size_t)min(r0 + 4 * q, a.nSB - 1) * K + jc];
-#pragma unroll
-      for (int q = 0; q < 16; ++q)
-        if (r0 + 4 * q < a.nSB) s = (r0 + 4 * q == g) ? v[q] : s + v[q];
-    }
-    if (j >= K || tid >= 256) s = T(0);
-    csh[tid] = s;
-    __syncthreads();
-    if (tid < K) {
-      const T cs = ((csh[tid] + csh[64 + tid]) + csh[128 + tid]) + csh[192 + tid];
-      const T bb = a.b[tid];
-      const T gr = -(cs - a.alpha * bb);
-      T p = a.noise_scale * (T)wide_noise(a, (uint32_t)(a.D * K + tid));
-      if (gpu_var) p = p * a.pb[tid];                                         // gpu/sgld.py:18
-      p = p + a.m_half_eps * gr;
-      if (gpu_var) a.pb[tid] = p;
-      a.b[tid] = bb + p;
-    }
-  }
-  WSTAMP(5);
-}
-
-// ---------------------------------------------------------------- Xᵀ·diff per (feature tile, class tile) + SGLD update
-// grid = 1 + KB·⌈D/16⌉: block 0 does the bias from the k_wsoft column sums; block 1 + c·ntile + t owns
-// feature tile t × class tile c (16 × 16 weights) and computes its Xᵀ·diff over the WHOLE minibatch —
-// no cross-workgroup reduction; 8 waves split the rows (summed in wave order) and the tile's weights
-// are updated in place (cpu/sgld.py:31-46).  The blocks of one feature tile are ntile apart, so they
-// share an XCD (and the X columns in its L2) when ntile % 8 == 0.  Every load a thread needs is
-// issued before the Philox noise is drawn, so the noise hides in their latency.
 template <typename T>
-__device__ inline void wide_bias(const WideArgs<T>& a, T* csh) {
+__device__ inline void wide_bias(const WideArgs<T>& a, int ch, T* csh) {
   const int tid = threadIdx.x;
   const int K = a.K;
   const int j = tid % 64, g = min(tid / 64, 3), jc = min(j, K - 1);
+  const T* cp = a.csp + (size_t)ch * a.nSB * K;
   T s = T(0);
+  // group g sums row blocks g, g + 4, … in order; 16 loads in flight per batch
   for (int r0 = g; r0 < a.nSB; r0 += 64) {
     T v[16];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) v[q] = a.csp[(size_t)min(r0 + 4 * q, a.nSB - 1) * K + jc];
+    for (int q = 0; q < 16; ++q) v[q] = cp[(size_t)min(r0 + 4 * q, a.nSB - 1) * K + jc];
 #pragma unroll
     for (int q = 0; q < 16; ++q)
       if (r0 + 4 * q < a.nSB) s = (r0 + 4 * q == g) ? v[q] : s + v[q];
@@ -455,40 +238,44 @@ __device__ inline void wide_bias(const WideArgs<T>& a, T* csh) {
   csh[tid] = s;
   __syncthreads();
   if (tid < K) {
+    const int bi = ch * K + tid;
     const T cs = ((csh[tid] + csh[64 + tid]) + csh[128 + tid]) + csh[192 + tid];
-    const T bb = a.b[tid];
+    const T bb = a.b[bi];
     const T gr = -(cs - a.alpha * bb);                                       // softmax.py:55,59-60
-    T p = a.noise_scale * (T)wide_noise(a, (uint32_t)(a.D * K + tid));
-    if (a.pW != nullptr) p = p * a.pb[tid];                                  // gpu/sgld.py:18
-    p = p + a.m_half_eps * gr;
-    if (a.pW != nullptr) a.pb[tid] = p;
-    a.b[tid] = bb + p;
+    T p = a.noise_scale * (T)wide_noise(a, ch, (uint32_t)(a.D * K + tid));   // sgld.py:43-46
+    if (a.pW != nullptr) p = p * a.pb[bi];                                   // gpu/sgld.py:18
+    p = p + a.m_half_eps * gr;                                               // sgld.py:37
+    if (a.pW != nullptr) a.pb[bi] = p;
+    a.b[bi] = bb + p;                                                        // sgld.py:38
   }
 }
 
 template <typename T>
-__global__ __launch_bounds__(GTH) void k_wgrad2(WideArgs<T> a) {
+__global__ __launch_bounds__(GTH) void k_wgrad(WideArgs<T> a) {
   using M = mfma16<T>;
   __shared__ T red[GNW][16][17];
   __shared__ T csh[GTH];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lg = lane >> 4;
+  const int ch = blockIdx.y;
   WSTAMP(0);
   if (blockIdx.x == 0) {
-    wide_bias(a, csh);
+    wide_bias(a, ch, csh);
     WSTAMP(1); WSTAMP(2); WSTAMP(3); WSTAMP(4); WSTAMP(5);
     return;
   }
   const int ntile = (a.D + 15) / 16;
-  const int c = (blockIdx.x - 1) / ntile, t = (blockIdx.x - 1) - c * ntile;
-  const int d0 = t * 16, K = a.K, B = a.B, KP = a.KP;
+  const int cls = (blockIdx.x - 1) / ntile, t = (blockIdx.x - 1) - cls * ntile;
+  const int d0 = t * 16, K = a.K, B = a.B, KP = a.KP, NW = a.C * K;
   const bool dok = d0 + lr < a.D;
   const int dcol = dok ? d0 + lr : 0;
   const int nks = (B + 3) / 4, Q = (nks + GNW - 1) / GNW;
   const int kb0 = wave * Q, kb1 = min(nks, kb0 + Q);
-  // my epilogue element: feature d0 + tid / 16, class 16c + tid % 16 (threads 0-255)
-  const int ei = tid >> 4, ek = c * 16 + (tid & 15);
+  const T* dg = a.diff + (size_t)ch * B * KP + cls * 16 + lr;
+  // my epilogue element: feature d0 + tid / 16, class 16·cls + tid % 16 (threads 0-255)
+  const int ei = tid >> 4, ek = cls * 16 + (tid & 15);
   const bool eok = tid < 256 && d0 + ei < a.D && ek < K;
-  const uint32_t el = eok ? (uint32_t)((d0 + ei) * K + ek) : 0u;
+  const uint32_t el = eok ? (uint32_t)((d0 + ei) * K + ek) : 0u;            // element of the chain's P
+  const size_t wi = eok ? (size_t)(d0 + ei) * NW + (size_t)ch * K + ek : 0;  // its place in W [D][C·K]
   const bool gpu_var = a.pW != nullptr;
   const T* psrc = gpu_var ? a.pW : a.W;
   constexpr int U = 16;
@@ -503,15 +290,15 @@ __global__ __launch_bounds__(GTH) void k_wgrad2(WideArgs<T> a) {
       const bool ok = ks + u < kb1 && row < B;
       const size_t rr = ok ? (size_t)row : 0;
       av[u] = a.X[rr * a.D + dcol];
-      bv[u] = a.diff[rr * KP + c * 16 + lr];
+      bv[u] = dg[rr * KP];
       if (!(ok && dok)) av[u] = T(0);
       if (!ok) bv[u] = T(0);
     }
     if (first) {                       // epilogue operands and noise while the first batch is in flight
       first = false;
-      wv = a.W[el];
-      pv = psrc[el];
-      zv = (T)wide_noise(a, el);
+      wv = a.W[wi];
+      pv = psrc[wi];
+      zv = (T)wide_noise(a, ch, el);
       WSTAMP(1);
     }
 #pragma unroll
@@ -533,103 +320,99 @@ __global__ __launch_bounds__(GTH) void k_wgrad2(WideArgs<T> a) {
     T p = a.noise_scale * zv;                                                  // sgld.py:43-46
     if (gpu_var) p = p * pv;                                                   // gpu/sgld.py:18
     p = p + a.m_half_eps * gr;                                                 // sgld.py:37
-    if (gpu_var) a.pW[el] = p;
-    a.W[el] = wv + p;                                                          // sgld.py:38
+    if (gpu_var) a.pW[wi] = p;
+    a.W[wi] = wv + p;                                                          // sgld.py:38
   }
   WSTAMP(4);
   WSTAMP(5);
 }
 
-__global__ void k_wreduce_ll(const double* llp, int n, double* out) {
+__global__ void k_wreduce_ll(const double* llp, int n, double* out) {   // block = chain
   __shared__ double sh[256];
+  const double* p = llp + (size_t)blockIdx.x * n;
   double s = 0.0;
-  for (int i = threadIdx.x; i < n; i += 256) s += llp[i];
+  for (int i = threadIdx.x; i < n; i += 256) s += p[i];
   sh[threadIdx.x] = s;
   __syncthreads();
   for (int m = 128; m > 0; m >>= 1) {
     if ((int)threadIdx.x < m) sh[threadIdx.x] += sh[threadIdx.x + m];
     __syncthreads();
   }
-  if (threadIdx.x == 0) *out = sh[0];
+  if (threadIdx.x == 0) out[blockIdx.x] = sh[0];
 }
 
 // ---------------------------------------------------------------- host
 bool sgld_wide_eligible(const hmcx_sampler_args* s) {
   const char* env = getenv("HMCX_SGLD_WIDE");
-  if (env && env[0] == '0') return false;        // 0: kernel-per-phase; 1: this path; 2: persistent
-  if (s->C != 1 || s->K > 64 || s->K < 1 || s->B < 1 || s->D < 1) return false;
-  // faster than the kernel-per-phase path for every single-chain shape measured (MNIST D=784,
-  // K=10: 18.0 vs 20.5 µs per f64 step; config 5 D=2048, K=38: 26.4 vs 35.1 µs)
-  return true;
-}
-
-// kernel generation: 2 (default) = k_wfwd2 / k_wgrad2, 1 = k_wfwd / k_wgrad (HMCX_WIDE_V=1)
-static int wide_version() {
-  static const int v = getenv("HMCX_WIDE_V") ? atoi(getenv("HMCX_WIDE_V")) : 2;
-  return v == 1 ? 1 : 2;
+  if (env && env[0] == '0') return false;        // 0: kernel-per-phase path
+  if (s->K > 64 || s->K < 1 || s->B < 1 || s->D < 1 || s->C < 1 || s->C > 65535) return false;
+  // one chain: faster than the kernel-per-phase path for every shape measured (MNIST D=784, K=10:
+  // 18.0 vs 20.5 µs per f64 step; config 5: 22.8 vs 35.1 µs).  Several chains: when a chain's K
+  // classes fill most of the 16-wide class tiles (K > 16); at K = 10 the kernel-per-phase path packs
+  // the chains' columns together instead
+  return s->C == 1 || s->K > 16 || (env && env[0] == '1');
 }
 
 template <typename T, int KB>
-static void launch_wide(const WideArgs<T>& a, hipStream_t st, int which) {
-  const dim3 gf((a.B + WRB - 1) / WRB, a.S);
-  if (wide_version() == 1) {
-    if (which == 0) hipLaunchKernelGGL((k_wfwd<T, KB>), gf, dim3(WTH), 0, st, a);
-    else hipLaunchKernelGGL((k_wgrad<T, KB>), dim3((a.D + 15) / 16), dim3(GTH), 0, st, a);
-  } else {
-    if (which == 0) hipLaunchKernelGGL((k_wfwd2<T, KB>), gf, dim3(WTH), 0, st, a);
-    else hipLaunchKernelGGL((k_wgrad2<T>), dim3(1 + KB * ((a.D + 15) / 16)), dim3(GTH), 0, st, a);
-  }
+static void launch_fwd_kb(const WideArgs<T>& a, hipStream_t st) {
+  hipLaunchKernelGGL((k_wfwd<T, KB>), dim3((a.B + WRB - 1) / WRB, a.S, a.C), dim3(WTH), 0, st, a);
 }
 template <typename T>
-static void launch_wide_kb(const WideArgs<T>& a, hipStream_t st, int which) {
+static void launch_fwd(const WideArgs<T>& a, hipStream_t st) {
   switch (a.KP / 16) {
-    case 1: launch_wide<T, 1>(a, st, which); break;
-    case 2: launch_wide<T, 2>(a, st, which); break;
-    case 3: launch_wide<T, 3>(a, st, which); break;
-    default: launch_wide<T, 4>(a, st, which); break;
+    case 1: launch_fwd_kb<T, 1>(a, st); break;
+    case 2: launch_fwd_kb<T, 2>(a, st); break;
+    case 3: launch_fwd_kb<T, 3>(a, st); break;
+    default: launch_fwd_kb<T, 4>(a, st); break;
   }
 }
 
 template <typename T>
 int sgld_wide_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
-  const int B = s->B, D = s->D, K = s->K, KP = (K + 15) / 16 * 16;
+  const int B = s->B, D = s->D, K = s->K, C = s->C, KP = (K + 15) / 16 * 16;
   const int S = (D + WDZ - 1) / WDZ, Dz = ((D + S - 1) / S + 3) / 4 * 4;
   const int nSB = (B + WSR - 1) / WSR;
-  // HMCX_WIDE_PROF=<file>: stamps of the first PROF_CAP steps' three launches, appended to <file>
-  // after the call (header: steps, workgroups of k_wfwd, k_wsoft, k_wgrad, WPH; tools/wide_prof_summary.py)
-  static const char* prof_path = getenv("HMCX_WIDE_PROF");
   const int ntile = (D + 15) / 16;
-  const int GF = ((B + WRB - 1) / WRB) * S, GS = nSB, GG = wide_version() == 1 ? ntile : 1 + (KP / 16) * ntile,
-            GALL = GF + GS + GG;
-  const int nprof = prof_path ? std::min(s->n_steps, 64) : 0;
+  const size_t nsc = (size_t)s->n_steps * C;
+  // HMCX_WIDE_PROF=<file> (one chain): stamps of the first 64 steps' three launches, appended to
+  // <file> after the call (header: steps, workgroups of k_wfwd, k_wsoft, k_wgrad, WPH;
+  // tools/wide_prof_summary.py)
+  static const char* prof_path = getenv("HMCX_WIDE_PROF");
+  const int GF = ((B + WRB - 1) / WRB) * S, GS = nSB, GG = 1 + (KP / 16) * ntile, GALL = GF + GS + GG;
+  const int nprof = (prof_path && C == 1) ? std::min(s->n_steps, 64) : 0;
+  const bool buf = s->noise_mode == HMCX_NOISE_BUFFER;
   Workspace ws(ctx);
   T *slab, *diff, *csp;
   double* llp;
+  int64_t* d_noff = nullptr;
   unsigned long long* prof = nullptr;
   do {
     ws.reset();
-    slab = ws.take<T>((size_t)S * B * KP);
-    diff = ws.take<T>((size_t)B * KP);
-    csp = ws.take<T>((size_t)nSB * K);
-    llp = ws.take<double>((size_t)nSB);
+    slab = ws.take<T>((size_t)S * C * B * KP);
+    diff = ws.take<T>((size_t)C * B * KP);
+    csp = ws.take<T>((size_t)C * nSB * K);
+    llp = ws.take<double>((size_t)C * nSB);
+    if (buf) d_noff = ws.take<int64_t>(nsc);
     if (nprof) prof = ws.take<unsigned long long>((size_t)nprof * GALL * WPH);
   } while (ws.retry());
   if (ws.failed) return HMCX_ENOMEM;
   int rc;
   begin_call(ctx);
+  if (buf && (rc = upload(ctx, d_noff, s->noise_off, nsc * sizeof(int64_t)))) return rc;
   WideArgs<T> a{};
   a.W = (T*)s->W; a.b = (T*)s->b; a.pW = (T*)s->pW; a.pb = (T*)s->pb;
-  a.B = B; a.D = D; a.K = K; a.KP = KP; a.S = S; a.Dz = Dz; a.nSB = nSB;
+  a.B = B; a.D = D; a.K = K; a.KP = KP; a.S = S; a.Dz = Dz; a.nSB = nSB; a.C = C;
   a.slab = slab; a.diff = diff; a.csp = csp; a.llp = llp;
   a.alpha = (T)s->alpha;
   a.clip_hi = (T)CLIP_HI; a.clip_lo = (T)CLIP_LO;
-  a.noise_mode = s->noise_mode; a.noise = s->noise; a.P = D * K + K;
+  a.noise_mode = s->noise_mode; a.noise = s->noise;
   a.seed = s->seed; a.chain = s->chain0;
   static const int wt_env = getenv("HMCX_WIDE_WT") ? atoi(getenv("HMCX_WIDE_WT")) : 1;
   a.wt = wt_env;
   if ((rc = timing_begin(ctx, ctx->stream))) return rc;
   GraphScope gs(ctx);
   hipStream_t st = ctx->stream;
+  const dim3 ggrid(GG, C), sgrid(nSB, C);
   for (int i = 0; i < s->n_steps; ++i) {
     a.X = (const T*)s->X + (size_t)s->row0[i] * D;
     a.Y = (const T*)s->Y + (size_t)s->row0[i] * K;
@@ -637,22 +420,22 @@ int sgld_wide_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
     a.noise_scale = (T)(2.0 * eps);                                   // sgld.py:43
     a.m_half_eps = (T)(-0.5 * eps);                                   // sgld.py:37
     a.step = s->step_base + (uint32_t)i;
-    a.noff = s->noise_mode == HMCX_NOISE_BUFFER ? s->noise_off[i] : 0;
+    a.noff = buf ? d_noff + (size_t)i * C : nullptr;
     a.want_diff = 1;
     unsigned long long* pr = i < nprof ? prof + (size_t)i * GALL * WPH : nullptr;
     a.prof = pr;
-    launch_wide_kb<T>(a, st, 0);
+    launch_fwd<T>(a, st);
     a.prof = pr ? pr + (size_t)GF * WPH : nullptr;
-    hipLaunchKernelGGL(k_wsoft<T>, dim3(nSB), dim3(WTH), 0, st, a);
+    hipLaunchKernelGGL(k_wsoft<T>, sgrid, dim3(WTH), 0, st, a);
     a.prof = pr ? pr + (size_t)(GF + GS) * WPH : nullptr;
-    launch_wide_kb<T>(a, st, 1);
+    hipLaunchKernelGGL(k_wgrad<T>, ggrid, dim3(GTH), 0, st, a);
     a.prof = nullptr;
     HMCX_HIP(ctx, hipGetLastError());
     if (s->want_ll && s->want_ll[i] && s->out_ll) {                   // sgmcmc.py:61 logging
       a.want_diff = 0;
-      launch_wide_kb<T>(a, st, 0);
-      hipLaunchKernelGGL(k_wsoft<T>, dim3(nSB), dim3(WTH), 0, st, a);
-      hipLaunchKernelGGL(k_wreduce_ll, dim3(1), dim3(256), 0, st, (const double*)llp, nSB, s->out_ll + i);
+      launch_fwd<T>(a, st);
+      hipLaunchKernelGGL(k_wsoft<T>, sgrid, dim3(WTH), 0, st, a);
+      hipLaunchKernelGGL(k_wreduce_ll, dim3(C), dim3(256), 0, st, (const double*)llp, nSB, s->out_ll + (size_t)i * C);
       HMCX_HIP(ctx, hipGetLastError());
     }
   }

@@ -106,3 +106,38 @@ def test_batched_chains_f32_equal_single_chain_runs():
         np.testing.assert_allclose(logp_b[ch], logp_1, rtol=1e-4)
         scale = np.abs(post_1["weights"]).max() + 1e-3
         assert np.abs(post_b["weights"][ch] - post_1["weights"]).max() <= 1e-3 * scale
+
+
+SGLD_WIDE = dict(kind="sgld", N=300, B=100, D=300, K=38, alpha=0.01, step_size=1e-4, path_length=1.0,
+                 burnin=1, epochs=2, data_seed=61, np_seed=2, rng_seed=3)
+
+
+@pytest.mark.parametrize("chains", [2, 5])
+def test_wide_sgld_replica_chains_match_oracle(chains):
+    """SGLD with several chains at a config-5-like class count (K = 38): the wide path
+    (hmcx_wide.hip, a chain grid dimension in every kernel) in replica mode — every chain replays the
+    reference's streams, so every chain must reproduce the oracle's single-chain trajectory (float64
+    within rel 1e-9) and its printed log-likelihoods."""
+    c = SGLD_WIDE
+    post_r, logp_r, _, _ = _run_oracle(c)
+    post_g, logp_g, _ = _run_chains(c, chains)
+    assert post_g["weights"].shape == (chains, c["epochs"], c["D"], c["K"])
+    for ch in range(chains):
+        for v in ("weights", "bias"):
+            np.testing.assert_allclose(post_g[v][ch], post_r[v], rtol=1e-9, atol=1e-12)
+        np.testing.assert_allclose(logp_g[ch], logp_r, rtol=1e-10)
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_wide_sgld_chains_equal_single_chain_runs(dtype):
+    """Philox noise: chain c of a 4-chain wide SGLD run (D = 2048, K = 38: BASELINE config 5's shape)
+    equals the single-chain run keyed by chain c (f64 rel 1e-9; f32 rel 1e-4 — summation order is the
+    same, only the chain layout of W differs)."""
+    c = dict(SGLD_WIDE, N=1000, B=500, D=2048, burnin=0, epochs=2)
+    post_b, logp_b, _ = _run_chains(c, 4, dtype=dtype, noise="philox", seed=13, chain=6)
+    tol = dict(rtol=1e-9, atol=1e-12) if dtype == torch.float64 else dict(rtol=1e-4, atol=1e-6)
+    for ch in (0, 3):
+        post_1, logp_1, _ = _run_chains(c, 1, dtype=dtype, noise="philox", seed=13, chain=6 + ch)
+        for v in ("weights", "bias"):
+            np.testing.assert_allclose(post_b[v][ch], post_1[v], **tol)
+        np.testing.assert_allclose(logp_b[ch], logp_1, rtol=1e-9 if dtype == torch.float64 else 1e-4)

@@ -53,12 +53,12 @@ def test_ragged_shapes_vs_oracle(kind, N, B, D, K):
     c = dict(kind=kind, N=N, B=B, D=D, K=K, alpha=0.05, step_size=0.01 if kind == "sghmc" else 1e-3,
              path_length=0.05, burnin=1, epochs=2, data_seed=71, np_seed=3, rng_seed=4)
     post_r, logp_r, tr_r, log_r = _run(c, gpu=False)
-    paths = (0, 1, 2, 3) if kind == "sghmc" else (0,)
+    paths = (0, 1, 2) if kind == "sghmc" else (0,)
     for path in paths:
         try:
             post_g, logp_g, tr_g, log_g = _run(c, gpu=True, path=path)
         except Exception as e:                     # persistent kernel: shape outside its plan
-            if path in (2, 3) and "not supported" in str(e):
+            if path == 2 and "not supported" in str(e):
                 continue
             raise
         if kind == "sghmc":

@@ -5,7 +5,7 @@ completion of cpu/sghmc.py:36): Python's ``min(1, nan)`` returns 1, so a NaN pro
 accepted and the chain carries NaN from then on.  A single NaN weight in start_p makes every logit,
 gradient and energy NaN (the logit clip of softmax.py:39-41 keeps NaN).  Each kernel must then
 report A = 1, accept every step, keep the oracle's path lengths, and end in the same NaN pattern:
-the persistent single-chain kernels (hmcx_persist2.hip, hmcx_rowspace.hip), the kernel-per-phase path (hmcx_softmax.hip)
+the persistent single-chain kernel (hmcx_persist2.hip), the kernel-per-phase path (hmcx_softmax.hip)
 and the chain-batched GEMMs (hmcx_batch.h, C = 16 replica chains)."""
 import io
 
@@ -60,8 +60,7 @@ def _gpu(c, path, chains=1):
 
 
 @pytest.mark.parametrize("name,path,chains", [("sghmc_small", 1, 1), ("sghmc_small", 2, 1),
-                                              ("sghmc_mnist", 2, 1), ("sghmc_small", 3, 1),
-                                              ("sghmc_mnist", 3, 1), ("sghmc_small", 0, 16)])
+                                              ("sghmc_mnist", 2, 1), ("sghmc_small", 0, 16)])
 def test_nan_energy_accepted(name, path, chains):
     c = gi.TRAJ_CONFIGS[name]
     post_r, logp_r, tr_r = _oracle(c)

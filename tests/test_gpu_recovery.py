@@ -37,7 +37,7 @@ def _restore_path():
     nat.context(torch.device("cuda:0")).set_sghmc_path(0)
 
 
-@pytest.mark.parametrize("name,path", [("sghmc_small", 2), ("sghmc_mnist", 2), ("sghmc_mnist", 3)])
+@pytest.mark.parametrize("name,path", [("sghmc_small", 2), ("sghmc_mnist", 2)])
 def test_forced_abort_is_recovered_in_process(name, path, monkeypatch, capfd):
     """HMCX_P2_FORCE_ABORT=1: in every persistent launch the last workgroup gives up at step 1
     (the other workgroups then abort in their polls) — the first epoch's call and the one already
