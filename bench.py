@@ -201,7 +201,7 @@ def pmc_file(dtype, path):
 
 def pmc_traffic(dtype, path, leapfrogs_per_launch):
     """Fabric bytes per launch of the dominant kernel, from the committed rocprofv3 PMC run of the
-    driver's call shape (the newest profiles/pmc_rNN_<dtype>_<path>.json, tools/gpu_r02_pmc.sh): 2·FETCH_SIZE +
+    driver's call shape (the newest profiles/pmc_rNN_<dtype>_<path>.json, tools/gpu_pmc_headline.sh): 2·FETCH_SIZE +
     WRITE_SIZE of the timed launches (MI355X_MICROARCH.md: FETCH_SIZE counts half of 16-byte
     streaming reads) per leapfrog of those launches, times the leapfrogs of this run's launch — the
     exchange rounds, which carry almost all of the traffic, are per leapfrog."""

@@ -3,7 +3,7 @@
 # FETCH_SIZE and WRITE_SIZE in separate passes (TCC slot limits), summarised per leapfrog.
 set -o pipefail
 R=$(pwd)
-TAG=${TAG:-r02}
+TAG=${TAG:-r03}
 STEPS=${STEPS:-20}
 WARM=${WARM:-5}
 mkdir -p gpurun_out

@@ -13,6 +13,6 @@ timeout -k 10 300 python bench.py --cpu-seconds 0 --batched-chains 0 --mlp-steps
 python3 -c "import json; d=json.load(open('gpurun_out/bench_s600.json')); print('s600', d['value'], d['ms_per_step'], d['roofline']['launch_ms'])"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_s20 -o run --output-format csv -- python3 $R/bench.py --steps 20 --warmup 5 --cpu-seconds 0 > $R/gpurun_out/bench_prof.json 2> $R/gpurun_out/prof.err || { echo prof failed; tail $R/gpurun_out/prof.err; exit 1; }
-cd $R && TAG=r02f bash tools/gpu_r02_pmc.sh || exit 1
+cd $R && TAG=r02f bash tools/gpu_pmc_headline.sh || exit 1
 CS=2048 bash tools/gpu_pmc_batch.sh || exit 1
 python3 tools/pmc_batch_summary.py gpurun_out/pmcb "python3 tools/probe_batch.py 2048" gpurun_out/pmc_r02_batched_sq.json

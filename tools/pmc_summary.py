@@ -1,4 +1,4 @@
-"""Summarise the two rocprofv3 PMC passes of tools/gpu_r02_pmc.sh into profiles/pmc_<tag>_<dtype>_<path>.json
+"""Summarise the two rocprofv3 PMC passes of tools/gpu_pmc_headline.sh into profiles/pmc_<tag>_<dtype>_<path>.json
 (read by bench.py's roofline 'traffic').
 
     python tools/pmc_summary.py gpurun_out/pmcf gpurun_out/pmcw "k_sghmc_p2<double, 10>" gpurun_out/bench_pmcf.json \
@@ -52,7 +52,7 @@ def main():
         "config": "python bench.py --steps %d --warmup %d (f64, B=500, D=784, K=10): %d timed launch(es), "
                   "%.0f leapfrogs" % (steps, b["warmup"], calls, lf),
         "collection": "rocprofv3 --kernel-trace --pmc FETCH_SIZE, then a separate pass with --pmc WRITE_SIZE "
-                      "(tools/gpu_r02_pmc.sh); summarised by tools/pmc_summary.py",
+                      "(tools/gpu_pmc_headline.sh); summarised by tools/pmc_summary.py",
         "fetch_size_kb_per_launch": fetch,
         "write_size_kb_per_launch": write,
         "timed_launches": calls,
