@@ -13,12 +13,14 @@
 //            waves' partials are summed in wave order into slab[z][c][B][16·KB].
 //   k_wsoft  one wave per minibatch row and chain, lane = class: Σ_z slab (fixed order), + b, clip,
 //            softmax by DPP row reductions + two cross-row shuffles (every lane ends with identical
-//            bits), diff = y − ŷ, column-sum and log-likelihood partials per 4-row block.
-//   k_wgrad  grid (1 + KB·⌈D/16⌉, chains): block 0 finishes the bias from the column sums; block
-//            1 + cls·ntile + t owns feature tile t × class tile cls (16 × 16 weights) and computes
-//            its Xᵀ·diff over the whole minibatch (8 waves split the rows, summed in wave order) —
-//            no cross-workgroup reduction — then updates those weights in place.  Its loads are
-//            issued before the Philox noise is drawn, so the noise hides in their latency.
+//            bits), diff = y − ŷ (gradient pass) or the log-likelihood partial per 4-row block
+//            (logging pass).
+//   k_wgrad  grid (G·⌈D/16⌉, chains): block g·ntile + t owns feature tile t × class group g
+//            (16 × ⌈K/2⌉ weights; one group when K ≤ 16) and computes its Xᵀ·diff over the whole
+//            minibatch (8 waves split the rows, summed in wave order) — no cross-workgroup
+//            reduction — then updates those weights in place; feature tile 0 of each group also
+//            sums its diff columns and updates the group's biases.  Its loads are issued before the
+//            Philox noise is drawn, so the noise hides in their latency.
 // Measured (config 5, f64, one chain, MI355X): 22.8 µs per step against 29.1 for the previous
 // LDS-staged forward + one-workgroup-per-feature-tile gradient.
 #include "hmcx_common.h"
@@ -41,7 +43,7 @@ template <typename T> struct WideArgs {
   const T* X; const T* Y; T* W; T* b;
   T* pW; T* pb;                          // non-null: GPU-file momentum update (gpu/sgld.py:11-20)
   int B, D, K, KP, S, Dz, nSB, C;        // nSB: k_wsoft blocks per chain; C: chains
-  T* slab; T* diff; T* csp; double* llp;
+  T* slab; T* diff; double* llp;
   T alpha, noise_scale, m_half_eps, clip_hi, clip_lo;
   int want_diff;                         // k_wsoft: 1 = diff + colsum (gradient), 0 = ll only
   int noise_mode; const double* noise; const int64_t* noff;   // BUFFER: noise[noff[c] + e]
@@ -157,7 +159,6 @@ template <typename T> __device__ inline T wave_max(T v) {                  // Na
 // ---------------------------------------------------------------- softmax rows
 template <typename T>
 __global__ __launch_bounds__(WTH) void k_wsoft(WideArgs<T> a) {
-  __shared__ T cs[WSR][64];
   __shared__ double ll[WSR];
   const int tid = threadIdx.x, k = tid & 63, wave = tid >> 6, ch = blockIdx.y;
   const int row = blockIdx.x * WSR + wave, K = a.K, KP = a.KP;
@@ -196,17 +197,11 @@ __global__ __launch_bounds__(WTH) void k_wsoft(WideArgs<T> a) {
       t = wave_sum(t);
     }
   }
-  cs[wave][k] = d;
-  if (k == 0) ll[wave] = t;
   WSTAMP(2);
-  __syncthreads();
-  if (a.want_diff) {
-    if (tid < K) {
-      const T v = ((cs[0][tid] + cs[1][tid]) + cs[2][tid]) + cs[3][tid];
-      a.csp[((size_t)ch * a.nSB + blockIdx.x) * K + tid] = v;
-    }
-  } else if (tid == 0) {
-    a.llp[(size_t)ch * a.nSB + blockIdx.x] = ((ll[0] + ll[1]) + ll[2]) + ll[3];
+  if (!a.want_diff) {                  // the logging pass: ll partial of the block's rows
+    if (k == 0) ll[wave] = t;
+    __syncthreads();
+    if (tid == 0) a.llp[(size_t)ch * a.nSB + blockIdx.x] = ((ll[0] + ll[1]) + ll[2]) + ll[3];
   }
   WSTAMP(3);
 }
@@ -218,81 +213,78 @@ __device__ inline double wide_noise(const WideArgs<T>& a, int ch, uint32_t e) {
 }
 
 // ---------------------------------------------------------------- Xᵀ·diff + SGLD update
-template <typename T>
-__device__ inline void wide_bias(const WideArgs<T>& a, int ch, T* csh) {
-  const int tid = threadIdx.x;
-  const int K = a.K;
-  const int j = tid % 64, g = min(tid / 64, 3), jc = min(j, K - 1);
-  const T* cp = a.csp + (size_t)ch * a.nSB * K;
-  T s = T(0);
-  // group g sums row blocks g, g + 4, … in order; 16 loads in flight per batch
-  for (int r0 = g; r0 < a.nSB; r0 += 64) {
-    T v[16];
-#pragma unroll
-    for (int q = 0; q < 16; ++q) v[q] = cp[(size_t)min(r0 + 4 * q, a.nSB - 1) * K + jc];
-#pragma unroll
-    for (int q = 0; q < 16; ++q)
-      if (r0 + 4 * q < a.nSB) s = (r0 + 4 * q == g) ? v[q] : s + v[q];
-  }
-  if (j >= K || tid >= 256) s = T(0);
-  csh[tid] = s;
-  __syncthreads();
-  if (tid < K) {
-    const int bi = ch * K + tid;
-    const T cs = ((csh[tid] + csh[64 + tid]) + csh[128 + tid]) + csh[192 + tid];
-    const T bb = a.b[bi];
-    const T gr = -(cs - a.alpha * bb);                                       // softmax.py:55,59-60
-    T p = a.noise_scale * (T)wide_noise(a, ch, (uint32_t)(a.D * K + tid));   // sgld.py:43-46
-    if (a.pW != nullptr) p = p * a.pb[bi];                                   // gpu/sgld.py:18
-    p = p + a.m_half_eps * gr;                                               // sgld.py:37
-    if (a.pW != nullptr) a.pb[bi] = p;
-    a.b[bi] = bb + p;                                                        // sgld.py:38
-  }
+// Class grouping of k_wgrad: K ≤ 16 → one group; otherwise two groups of ⌈K/2⌉ classes (config 5:
+// 2 × 19), each NT = ⌈group/16⌉ MFMA column tiles.  One workgroup per (feature tile, group): 256 of
+// them at config 5, one per CU, with the same bytes and MFMAs each (three 16-class tiles gave 385
+// workgroups, 129 CUs with two and twice the load traffic and MFMA issue of the others).  The bias
+// gradient Σ_rows diff falls out of the same diff loads; feature tile 0 of each group applies it (no
+// bias block, no column-sum partials from k_wsoft).
+struct WGroups { int G, GW, NT; };
+__host__ __device__ inline WGroups wide_groups(int K) {
+  if (K <= 16) return {1, K, 1};
+  const int gw = (K + 1) / 2;
+  return {2, gw, (gw + 15) / 16};
 }
 
-template <typename T>
+template <typename T, int NT, int U>
 __global__ __launch_bounds__(GTH) void k_wgrad(WideArgs<T> a) {
   using M = mfma16<T>;
-  __shared__ T red[GNW][16][17];
-  __shared__ T csh[GTH];
+  __shared__ T red[GNW][16][NT * 16 + 1];
+  __shared__ T cs[GNW][NT * 16];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lg = lane >> 4;
   const int ch = blockIdx.y;
   WSTAMP(0);
-  if (blockIdx.x == 0) {
-    wide_bias(a, ch, csh);
-    WSTAMP(1); WSTAMP(2); WSTAMP(3); WSTAMP(4); WSTAMP(5);
-    return;
-  }
   const int ntile = (a.D + 15) / 16;
-  const int cls = (blockIdx.x - 1) / ntile, t = (blockIdx.x - 1) - cls * ntile;
+  const WGroups gr = wide_groups(a.K);
+  const int grp = blockIdx.x / ntile, t = blockIdx.x - grp * ntile;
   const int d0 = t * 16, K = a.K, B = a.B, KP = a.KP, NW = a.C * K;
+  const int c0 = grp * gr.GW, c1 = min(K, c0 + gr.GW);        // my classes [c0, c1)
   const bool dok = d0 + lr < a.D;
   const int dcol = dok ? d0 + lr : 0;
   const int nks = (B + 3) / 4, Q = (nks + GNW - 1) / GNW;
   const int kb0 = wave * Q, kb1 = min(nks, kb0 + Q);
-  const T* dg = a.diff + (size_t)ch * B * KP + cls * 16 + lr;
-  // my epilogue element: feature d0 + tid / 16, class 16·cls + tid % 16 (threads 0-255)
-  const int ei = tid >> 4, ek = cls * 16 + (tid & 15);
-  const bool eok = tid < 256 && d0 + ei < a.D && ek < K;
+  // diff [C][B][KP] read through a range-checked buffer: a column outside [c0, c1) or a row past the
+  // minibatch gets an out-of-range offset and reads 0 without a memory request (the padded classes of
+  // a group cost no bytes)
+  const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(
+      a.diff + (size_t)ch * B * KP, 0, B * KP * (int)sizeof(T), 0x00020000);
+  int col[NT];
+  bool cok[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    col[j] = c0 + j * 16 + lr;
+    cok[j] = col[j] < c1;
+  }
+  // my epilogue element: feature d0 + tid / GW, class c0 + tid % GW (threads 0 … 16·GW − 1)
+  const int ei = tid / gr.GW, ek = c0 + (tid - (tid / gr.GW) * gr.GW);
+  const bool eok = tid < 16 * gr.GW && d0 + ei < a.D && ek < c1;
   const uint32_t el = eok ? (uint32_t)((d0 + ei) * K + ek) : 0u;            // element of the chain's P
   const size_t wi = eok ? (size_t)(d0 + ei) * NW + (size_t)ch * K + ek : 0;  // its place in W [D][C·K]
   const bool gpu_var = a.pW != nullptr;
   const T* psrc = gpu_var ? a.pW : a.W;
-  constexpr int U = 16;
-  typename M::acc_t acc0 = M::zero(), acc1 = M::zero();
+  typename M::acc_t acc[NT];
+  T csum[NT];                          // Σ_rows diff of my columns (the bias gradient, softmax.py:59)
+#pragma unroll
+  for (int j = 0; j < NT; ++j) { acc[j] = M::zero(); csum[j] = T(0); }
   T wv = T(0), pv = T(0), zv = T(0);
   bool first = true;
   for (int ks = kb0; ks < kb1 || first; ks += U) {
-    T av[U], bv[U];
+    T av[U], bv[U][NT];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int row = (ks + u) * 4 + lg;
       const bool ok = ks + u < kb1 && row < B;
       const size_t rr = ok ? (size_t)row : 0;
       av[u] = a.X[rr * a.D + dcol];
-      bv[u] = dg[rr * KP];
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int off = (ok && cok[j]) ? (row * KP + col[j]) * (int)sizeof(T) : 0x7fffffff;
+        if constexpr (sizeof(T) == 8)
+          bv[u][j] = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(drs, off, 0, 0));
+        else
+          bv[u][j] = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(drs, off, 0, 0));
+      }
       if (!(ok && dok)) av[u] = T(0);
-      if (!ok) bv[u] = T(0);
     }
     if (first) {                       // epilogue operands and noise while the first batch is in flight
       first = false;
@@ -302,24 +294,48 @@ __global__ __launch_bounds__(GTH) void k_wgrad(WideArgs<T> a) {
       WSTAMP(1);
     }
 #pragma unroll
-    for (int u = 0; u < U; u += 2) {
-      acc0 = M::fma(av[u], bv[u], acc0);
-      acc1 = M::fma(av[u + 1], bv[u + 1], acc1);
-    }
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        acc[j] = M::fma(av[u], bv[u][j], acc[j]);
+        csum[j] += bv[u][j];
+      }
   }
   WSTAMP(2);
 #pragma unroll
-  for (int q = 0; q < 4; ++q) red[wave][M::row(lane, q)][lr] = acc0[q] + acc1[q];
+  for (int j = 0; j < NT; ++j) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) red[wave][M::row(lane, q)][j * 16 + lr] = acc[j][q];
+    // the four row groups of a column (lanes lr, lr + 16, lr + 32, lr + 48), symmetric pairs
+    T v = csum[j];
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    if (lg == 0) cs[wave][j * 16 + lr] = v;
+  }
   __syncthreads();
   WSTAMP(3);
-  if (eok) {
-    T dot = red[0][ei][tid & 15];
+  if (t == 0 && tid < c1 - c0) {       // feature tile 0 of each group also finishes the group's biases
+    const int c = c0 + tid, bi = ch * K + c;
+    T colsum = cs[0][tid];
 #pragma unroll
-    for (int w = 1; w < GNW; ++w) dot += red[w][ei][tid & 15];
-    const T gr = -(dot - a.alpha * wv);                                        // softmax.py:57-58
+    for (int w = 1; w < GNW; ++w) colsum += cs[w][tid];
+    const T bb = a.b[bi];
+    const T gb = -(colsum - a.alpha * bb);                                   // softmax.py:55,59-60
+    T p = a.noise_scale * (T)wide_noise(a, ch, (uint32_t)(a.D * K + c));     // sgld.py:43-46
+    if (gpu_var) p = p * a.pb[bi];                                           // gpu/sgld.py:18
+    p = p + a.m_half_eps * gb;                                               // sgld.py:37
+    if (gpu_var) a.pb[bi] = p;
+    a.b[bi] = bb + p;                                                        // sgld.py:38
+  }
+  if (eok) {
+    const int cc = ek - c0;
+    T dot = red[0][ei][cc];
+#pragma unroll
+    for (int w = 1; w < GNW; ++w) dot += red[w][ei][cc];
+    const T gr_ = -(dot - a.alpha * wv);                                       // softmax.py:57-58
     T p = a.noise_scale * zv;                                                  // sgld.py:43-46
     if (gpu_var) p = p * pv;                                                   // gpu/sgld.py:18
-    p = p + a.m_half_eps * gr;                                                 // sgld.py:37
+    p = p + a.m_half_eps * gr_;                                                // sgld.py:37
     if (gpu_var) a.pW[wi] = p;
     a.W[wi] = wv + p;                                                          // sgld.py:38
   }
@@ -378,11 +394,12 @@ int sgld_wide_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
   // <file> after the call (header: steps, workgroups of k_wfwd, k_wsoft, k_wgrad, WPH;
   // tools/wide_prof_summary.py)
   static const char* prof_path = getenv("HMCX_WIDE_PROF");
-  const int GF = ((B + WRB - 1) / WRB) * S, GS = nSB, GG = 1 + (KP / 16) * ntile, GALL = GF + GS + GG;
+  const WGroups wg = wide_groups(K);
+  const int GF = ((B + WRB - 1) / WRB) * S, GS = nSB, GG = wg.G * ntile, GALL = GF + GS + GG;
   const int nprof = (prof_path && C == 1) ? std::min(s->n_steps, 64) : 0;
   const bool buf = s->noise_mode == HMCX_NOISE_BUFFER;
   Workspace ws(ctx);
-  T *slab, *diff, *csp;
+  T *slab, *diff;
   double* llp;
   int64_t* d_noff = nullptr;
   unsigned long long* prof = nullptr;
@@ -390,7 +407,6 @@ int sgld_wide_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
     ws.reset();
     slab = ws.take<T>((size_t)S * C * B * KP);
     diff = ws.take<T>((size_t)C * B * KP);
-    csp = ws.take<T>((size_t)C * nSB * K);
     llp = ws.take<double>((size_t)C * nSB);
     if (buf) d_noff = ws.take<int64_t>(nsc);
     if (nprof) prof = ws.take<unsigned long long>((size_t)nprof * GALL * WPH);
@@ -402,7 +418,7 @@ int sgld_wide_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
   WideArgs<T> a{};
   a.W = (T*)s->W; a.b = (T*)s->b; a.pW = (T*)s->pW; a.pb = (T*)s->pb;
   a.B = B; a.D = D; a.K = K; a.KP = KP; a.S = S; a.Dz = Dz; a.nSB = nSB; a.C = C;
-  a.slab = slab; a.diff = diff; a.csp = csp; a.llp = llp;
+  a.slab = slab; a.diff = diff; a.llp = llp;
   a.alpha = (T)s->alpha;
   a.clip_hi = (T)CLIP_HI; a.clip_lo = (T)CLIP_LO;
   a.noise_mode = s->noise_mode; a.noise = s->noise;
@@ -428,7 +444,16 @@ int sgld_wide_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
     a.prof = pr ? pr + (size_t)GF * WPH : nullptr;
     hipLaunchKernelGGL(k_wsoft<T>, sgrid, dim3(WTH), 0, st, a);
     a.prof = pr ? pr + (size_t)(GF + GS) * WPH : nullptr;
-    hipLaunchKernelGGL(k_wgrad<T>, ggrid, dim3(GTH), 0, st, a);
+    // one chain: 16 k-steps of loads per batch (one batch at B = 500, one workgroup per CU);
+    // several chains: 8 per batch, so that two workgroups fit on a CU (C = 8 at config 5: 92.7 → see
+    // DESIGN §5.4)
+    if (wg.NT == 1) {
+      if (C == 1) hipLaunchKernelGGL((k_wgrad<T, 1, 16>), ggrid, dim3(GTH), 0, st, a);
+      else hipLaunchKernelGGL((k_wgrad<T, 1, 8>), ggrid, dim3(GTH), 0, st, a);
+    } else {
+      if (C == 1) hipLaunchKernelGGL((k_wgrad<T, 2, 16>), ggrid, dim3(GTH), 0, st, a);
+      else hipLaunchKernelGGL((k_wgrad<T, 2, 8>), ggrid, dim3(GTH), 0, st, a);
+    }
     a.prof = nullptr;
     HMCX_HIP(ctx, hipGetLastError());
     if (s->want_ll && s->want_ll[i] && s->out_ll) {                   // sgmcmc.py:61 logging
