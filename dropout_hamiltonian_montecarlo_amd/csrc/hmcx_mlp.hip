@@ -40,7 +40,7 @@ namespace hmcx {
 
 // Mask slots live above the noise slots (0 = momentum, it+1 = iteration it) of the same counter space.
 constexpr uint32_t MASK_SLOT0 = 0x80000000u;
-constexpr int NPART = 32;     // blocks per variable in the energy partial sums
+constexpr int NPART = 256;    // blocks per variable (grid.x) and energy partials per variable
 constexpr int MM_NW = 8;      // waves per k_mm workgroup; the K range is split over them
 constexpr int MM_NT = MM_NW * 64;
 
@@ -148,12 +148,13 @@ template <typename T> struct Pending {
   const T* part;
   Upd<T> u;
 };
+// bid / nb: this workgroup's index among the nb workgroups that share the work
 template <typename T>
-__device__ inline void run_pending(const Pending<T>& pd) {
+__device__ inline void run_pending(const Pending<T>& pd, int bid, int nb) {
   if (pd.mode == UPD_NONE) return;
-  const int nthr = gridDim.x * gridDim.y * blockDim.x;
+  const int nthr = nb * blockDim.x;
   constexpr int PB = 16;                                       // partials loaded per batch
-  for (int i = (blockIdx.y * gridDim.x + blockIdx.x) * blockDim.x + threadIdx.x; i < pd.n; i += nthr) {
+  for (int i = bid * blockDim.x + threadIdx.x; i < pd.n; i += nthr) {
     // all loads of a batch go out before the (in-order) sum: one memory round trip per 16
     // partials instead of one per partial
     T s = T(0);
@@ -168,8 +169,24 @@ __device__ inline void run_pending(const Pending<T>& pd) {
     apply_upd(pd.u, pd.mode, i, s);
   }
 }
+// The pending updates a launch applies first (up to four: the bias / W3 sub-steps of one batched
+// iteration).  A batched launch (blockIdx.z = problem) runs them in an extra plane of workgroups of
+// their own, z = number of problems, beside the problems.
+constexpr int MAXPEND = 4;
+template <typename T> struct PendSet {
+  Pending<T> p[MAXPEND];
+  int n;
+};
 template <typename T>
-__global__ __launch_bounds__(256) void k_pending(Pending<T> pd) { run_pending(pd); }
+__device__ inline void run_pendset(const PendSet<T>& ps, int bid, int nb) {
+#pragma unroll
+  for (int j = 0; j < MAXPEND; ++j)
+    if (j < ps.n) run_pending(ps.p[j], bid, nb);
+}
+template <typename T>
+__global__ __launch_bounds__(256) void k_pending(PendSet<T> ps) {
+  run_pendset(ps, (int)(blockIdx.y * gridDim.x + blockIdx.x), (int)(gridDim.x * gridDim.y));
+}
 
 enum MMEpi { MM_STORE = 0, MM_L2 = 1, MM_L3CE = 2, MM_GA1 = 3, MM_UPD = 4, MM_L23 = 5 };
 enum MMOp { OP_PLAIN = 0, OP_H1 = 1 };
@@ -190,7 +207,7 @@ template <typename T> struct MMArgs {
   const T* W3; const T* h2; const T* d3; int n_mid;
   T* ga2; T* pb2; T* pb3; T* pw3;
   int upd_mode; Upd<T> u;            // MM_UPD
-  Pending<T> pend;                   // run first, by the whole grid
+  PendSet<T> pend;                   // run first, by the whole grid
   // MM_L23 (layer 2 + layer 3 in one launch): the 32 × n_out logit partials of the column-slice
   // workgroups of one row block meet in a tagged-granule arena (see k_mm)
   char* gx; int gx_bytes; unsigned ep; int* abort_flag;
@@ -201,6 +218,23 @@ template <typename T> struct MMArgs {
   unsigned long long* prof;          // HMCX_MLP_PROF: per-workgroup s_memrealtime stamps of the MM_L23 phases
 };
 constexpr int L23_NPH = 12;          // stamps per workgroup and launch (prof)
+
+// Batched launches: several independent problems of one kernel in one grid, problem = blockIdx.z.
+// The sub-steps of one leapfrog iteration are independent of each other (see mlp_sghmc_t), so their
+// fused forwards (MM_L23) and layer-1 backwards (MM_GA1) go out as one launch each; a problem
+// overrides the operands, masks and outputs of the shared MMArgs (dimensions, X, labels, xw shared).
+constexpr int MAXPROB = 6;
+template <typename T> struct MMProb {
+  const T* A; const T* B; T* C;
+  const T* b1; const T* bias; const T* W3; const T* bias3;
+  MaskSrc<T> ms;
+  T* ga2; T* pb2; T* pb3; T* pw3; T* gz; double* lpart; T* colpart;
+  char* gx;                          // MM_L23: the problem's own region of the granule arena
+};
+template <typename T> struct MMProbs {
+  MMProb<T> p[MAXPROB];
+  int n;                             // 0: a plain launch
+};
 
 template <typename T, int OP>
 __device__ inline T op_apply(T x, T mask, T bias) {
@@ -507,18 +541,48 @@ __device__ inline void mm_epilogue(const MMArgs<T>& a, int m, int n, T v) {
   }
 }
 
+// The workgroup's place in its (sub-)grid: a dual launch (k_mm2) runs two grids in one.
+struct Blk { int x, y, z, gx, gy; };
+
 template <typename T, int EPI, int AOP, int BOP, int TA, int TB, int AV, int BV, int MK>
-__global__ __launch_bounds__(MM_NT) void k_mm(MMArgs<T> a) {
+__device__ __forceinline__ void mm_body(const MMArgs<T>& a, const MMProbs<T>& pr, const Blk bk,
+                                        T (&red)[MM_NW][32][33], double* rowl) {
   using M = mfma16<T>;
-  __shared__ T red[MM_NW][32][33];
-  __shared__ double rowl[32];
-  // MM_L23 runs the pending update while its logit partials travel (below); nothing in this launch
-  // reads what it writes (the momentum and the NEXT iteration's position buffer of another variable)
-  if constexpr (EPI != MM_L23) run_pending(a.pend);
+  const int pbid0 = bk.y * bk.gx + bk.x, nb0 = bk.gx * bk.gy;
+  // MM_L23 runs the pending updates while its logit partials travel (below); nothing in this launch
+  // reads what they write (the momentum and the NEXT iteration's position buffer of other variables).
+  // A batched launch runs them in its extra plane (z = pr.n) and nowhere else.
+  if (pr.n > 0) {
+    if ((int)bk.z == pr.n) {
+      run_pendset(a.pend, pbid0, nb0);
+      return;
+    }
+  } else if constexpr (EPI != MM_L23) {
+    run_pendset(a.pend, pbid0, nb0);
+  }
+  // batched launch (pr.n > 0): the problem of this workgroup (bk.z) supplies the operands, masks
+  // and outputs; the kernel argument block itself is never copied (a local MMArgs would live in scratch)
+  const MMProb<T>* pp = pr.n > 0 ? &pr.p[bk.z] : nullptr;
+  const T* const oA = pp ? pp->A : a.A;
+  const T* const oB = pp ? pp->B : a.B;
+  T* const oC = pp ? pp->C : a.C;
+  const T* const ob1 = pp ? pp->b1 : a.b1;
+  const T* const obias = pp ? pp->bias : a.bias;
+  const T* const oW3 = pp ? pp->W3 : a.W3;
+  const T* const obias3 = pp ? pp->bias3 : a.bias3;
+  const MaskSrc<T> oms = pp ? pp->ms : a.ms;
+  T* const oga2 = pp ? pp->ga2 : a.ga2;
+  T* const opb2 = pp ? pp->pb2 : a.pb2;
+  T* const opb3 = pp ? pp->pb3 : a.pb3;
+  T* const opw3 = pp ? pp->pw3 : a.pw3;
+  T* const ogz = pp ? pp->gz : a.gz;
+  double* const olpart = pp ? pp->lpart : a.lpart;
+  T* const ocolpart = pp ? pp->colpart : a.colpart;
+  char* const ogx = pp ? pp->gx : a.gx;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lg = lane >> 4;
-  // MM_L3CE: blockIdx.y is the n_mid column slice of the layer-3 backward (N = n_out ≤ 32: one tile)
-  const int m0 = blockIdx.x * 32, n0 = EPI == MM_L3CE ? 0 : blockIdx.y * 32;
-  const int pbid = blockIdx.y * gridDim.x + blockIdx.x;
+  // MM_L3CE: bk.y is the n_mid column slice of the layer-3 backward (N = n_out ≤ 32: one tile)
+  const int m0 = bk.x * 32, n0 = EPI == MM_L3CE ? 0 : bk.y * 32;
+  const int pbid = bk.y * bk.gx + bk.x;
   auto stamp = [&](int ph) {
     if constexpr (EPI == MM_L23)
       if (a.prof && tid == 0) a.prof[(size_t)pbid * L23_NPH + ph] = __builtin_amdgcn_s_memrealtime();
@@ -540,14 +604,14 @@ __global__ __launch_bounds__(MM_NT) void k_mm(MMArgs<T> a) {
       const int e = tid + MM_NT * u, mm = e >> 5, nn = e & 31, m = m0 + mm, n = n0 + nn;
       const bool ok = m < a.M && n < a.N;
       const size_t i = ok ? (size_t)m * a.ldc + n : 0;
-      pm1[u] = mraw<T, MK>(a.ms, 1, i);
-      pm2[u] = mraw<T, MK>(a.ms, 2, i);
-      pb2v[u] = a.bias[ok ? n : 0];
+      pm1[u] = mraw<T, MK>(oms, 1, i);
+      pm2[u] = mraw<T, MK>(oms, 2, i);
+      pb2v[u] = obias[ok ? n : 0];
       const int o = e >> 5, c = e & 31;
       const bool okw = o < a.N3 && n0 + c < a.N;
-      pw3v[u] = a.W3[okw ? (size_t)o * a.n_mid + n0 + c : 0];
+      pw3v[u] = oW3[okw ? (size_t)o * a.n_mid + n0 + c : 0];
     }
-    pb3v = a.bias3[tid < a.N3 ? tid : 0];
+    pb3v = obias3[tid < a.N3 ? tid : 0];
   }
   stamp(7);
   const int Kq = ((a.K + 16 * MM_NW - 1) / (16 * MM_NW)) * 16;   // k range per wave (multiple of 16)
@@ -560,8 +624,8 @@ __global__ __launch_bounds__(MM_NT) void k_mm(MMArgs<T> a) {
   // three chunks in flight (register ring), then one MFMA batch per chunk
   T av[3][4][2], bv[3][4][2];
   auto load = [&](int s, int k0) {
-    load_chunk<T, AOP, TA, AV, MK>(av[s], a.A, a.lda, m0, a.M, k0, ke, lr, lg, a.ms, a.b1);
-    load_chunk<T, BOP, !TB, BV, MK>(bv[s], a.B, a.ldb, n0, a.N, k0, ke, lr, lg, a.ms, a.b1);
+    load_chunk<T, AOP, TA, AV, MK>(av[s], oA, a.lda, m0, a.M, k0, ke, lr, lg, oms, ob1);
+    load_chunk<T, BOP, !TB, BV, MK>(bv[s], oB, a.ldb, n0, a.N, k0, ke, lr, lg, oms, ob1);
   };
   auto mfma = [&](int s, int k0) {
     if constexpr (EPI == MM_L23 && AOP == OP_H1) {
@@ -617,7 +681,7 @@ __global__ __launch_bounds__(MM_NT) void k_mm(MMArgs<T> a) {
 #pragma unroll
     for (int w = 1; w < MM_NW; ++w) v += red[w][mm][nn];
     if constexpr (EPI == MM_L3CE) {
-      red[0][mm][nn] = (n < a.N) ? v + a.bias[n] : T(0);     // logits of the block (one writer each)
+      red[0][mm][nn] = (n < a.N) ? v + obias[n] : T(0);     // logits of the block (one writer each)
     } else if constexpr (EPI == MM_GA1) {                      // (ga2·W2)·[(xw + b1)·m0 > 0]·m0
       T g = T(0);
       if (m < a.M && n < a.N) {
@@ -626,12 +690,12 @@ __global__ __launch_bounds__(MM_NT) void k_mm(MMArgs<T> a) {
           // (xw + b1)·m0 > 0 ⟺ h1 > 0, and then m0 = scale; where h1 = 0 the product is ±0 either way
           // (the sign of v·0), so this is the reference's value without reading m0 again
           const bool pos = a.H1[i] > T(0);
-          g = (v * (pos ? T(1) : T(0))) * (pos ? a.ms.scale : T(0));
+          g = (v * (pos ? T(1) : T(0))) * (pos ? oms.scale : T(0));
         } else {
-          const T m0v = mval<T, MK>(a.ms, 0, i);
-          g = (v * ((a.H[i] + a.b1[n]) * m0v > T(0) ? T(1) : T(0))) * m0v;
+          const T m0v = mval<T, MK>(oms, 0, i);
+          g = (v * ((a.H[i] + ob1[n]) * m0v > T(0) ? T(1) : T(0))) * m0v;
         }
-        a.C[i] = g;
+        oC[i] = g;
       }
       red[0][mm][nn] = g;
     } else if constexpr (EPI == MM_L23) {                      // mlp.py:30-31; the tile stays in LDS
@@ -639,14 +703,14 @@ __global__ __launch_bounds__(MM_NT) void k_mm(MMArgs<T> a) {
       mpin<T, MK>(pm1[u]);
       mpin<T, MK>(pm2[u]);
       if (m < a.M && n < a.N) {
-        m1 = mfin<T, MK>(a.ms, pm1[u]);
-        m2 = mfin<T, MK>(a.ms, pm2[u]);
+        m1 = mfin<T, MK>(oms, pm1[u]);
+        m2 = mfin<T, MK>(oms, pm2[u]);
         const T t = (v + pb2v[u]) * m1;
         h = t > T(0) ? t : T(0);
         d = h * m2;
-        if (a.C) {                                              // h2 / d3 are dead in the fused sampler
+        if (oC) {                                              // h2 / d3 are dead in the fused sampler
           const size_t i = (size_t)m * a.ldc + n;
-          a.C[i] = h;
+          oC[i] = h;
           a.C2[i] = d;
         }
       }
@@ -655,29 +719,31 @@ __global__ __launch_bounds__(MM_NT) void k_mm(MMArgs<T> a) {
       red[3][mm][nn] = h;
       red[4][mm][nn] = m1;
       red[5][mm][nn] = m2;
+    } else if constexpr (EPI == MM_STORE) {
+      if (m < a.M && n < a.N) oC[(size_t)m * a.ldc + n] = v;
     } else {
       if (m < a.M && n < a.N) mm_epilogue<T, EPI, MK>(a, m, n, v);
     }
   }
   if constexpr (EPI == MM_L3CE) {
     __syncthreads();
-    const bool first = blockIdx.y == 0;
-    ce_rows<T>(&red[0][0][0], 33, rowl, m0, a.M, a.N, a.y, a.C, a.ldc, a.lpart, blockIdx.x, first);
+    const bool first = bk.y == 0;
+    ce_rows<T>(&red[0][0][0], 33, rowl, m0, a.M, a.N, a.y, oC, a.ldc, olpart, bk.x, first);
     __syncthreads();
-    const int cw = (a.n_mid + gridDim.y - 1) / gridDim.y;
-    const int jlo = min(a.n_mid, (int)blockIdx.y * cw), jhi = min(a.n_mid, jlo + cw);
-    l3_backward<T, MK>(a, &red[0][0][0], 33, m0, blockIdx.x, &red[1][0][0], (MM_NW - 1) * 32 * 33, jlo, jhi, first);
+    const int cw = (a.n_mid + bk.gy - 1) / bk.gy;
+    const int jlo = min(a.n_mid, (int)bk.y * cw), jhi = min(a.n_mid, jlo + cw);
+    l3_backward<T, MK>(a, &red[0][0][0], 33, m0, bk.x, &red[1][0][0], (MM_NW - 1) * 32 * 33, jlo, jhi, first);
   }
   if constexpr (EPI == MM_L23) {
     // Layer 3 of this row block, in the same launch: z = d3·W3ᵀ + b3 (mlp.py:31) needs all n_mid
-    // columns, which the S = gridDim.y column-slice workgroups of the block hold.  Each publishes
+    // columns, which the S = bk.gy column-slice workgroups of the block hold.  Each publishes
     // its 32 × n_out partial (own 32 columns, k order within the slice) as 16-byte granules
     // {lo32, ep, hi32, ep} with write-through (sc1) stores; every member reads all S partials of
     // every (row, class) and sums them in slice order — the all-reduce by redundant reads of
     // hmcx_persist2.hip — then runs the cross-entropy of the block (slice 0 writes loss and gz) and
     // the layer-3 backward of its own columns.  The epoch is new per launch and the arena only ever
     // holds granules of earlier launches, so no stale value can match.
-    const int No = a.N3, S = gridDim.y, s = blockIdx.y, rb = blockIdx.x;
+    const int No = a.N3, S = bk.gy, s = bk.y, rb = bk.x;
     T* d3t = &red[0][0][0];                                      // [32][33] d3 of the tile
     T* w3s = &red[1][0][0];                                      // [n_out][32] W3 columns of the slice
     T* zt = &red[2][0][0];                                       // [32][33] logits, then gz
@@ -691,7 +757,7 @@ __global__ __launch_bounds__(MM_NT) void k_mm(MMArgs<T> a) {
     }
     if (tid < No) b3s[tid] = pb3v;
     __syncthreads();
-    const __amdgpu_buffer_rsrc_t rs = gx_rsrc(a.gx, a.gx_bytes);
+    const __amdgpu_buffer_rsrc_t rs = gx_rsrc(ogx, a.gx_bytes);
     const int items = 32 * No;
     const int base_rb = rb * S * items;
     if (a.force_abort && pbid == 0 && tid == 0)                  // test knob: this launch never completes
@@ -704,7 +770,7 @@ __global__ __launch_bounds__(MM_NT) void k_mm(MMArgs<T> a) {
       gx_put(rs, base_rb + s * items + tid, (double)zp, a.ep);
     }
     stamp(2);
-    run_pending(a.pend);                                         // while the partials travel
+    if (pr.n == 0) run_pendset(a.pend, pbid0, nb0);                          // while the partials travel
     stamp(3);
     if (tid < items) {
       const int r = tid / No, o = tid - r * No;
@@ -715,8 +781,8 @@ __global__ __launch_bounds__(MM_NT) void k_mm(MMArgs<T> a) {
     __syncthreads();
     stamp(4);
     const bool first = s == 0;
-    if (No <= 16) ce_rows_lanes<T, 16>(zt, 33, rowl, m0, a.M, No, yv, a.gz, No, a.lpart, rb, first);
-    else ce_rows_lanes<T, 32>(zt, 33, rowl, m0, a.M, No, yv, a.gz, No, a.lpart, rb, first);
+    if (No <= 16) ce_rows_lanes<T, 16>(zt, 33, rowl, m0, a.M, No, yv, ogz, No, olpart, rb, first);
+    else ce_rows_lanes<T, 32>(zt, 33, rowl, m0, a.M, No, yv, ogz, No, olpart, rb, first);
     __syncthreads();
     stamp(5);
     // layer-3 backward of the slice's columns, all operands in LDS (gz in zt, W3 slice in w3s, the
@@ -733,38 +799,77 @@ __global__ __launch_bounds__(MM_NT) void k_mm(MMArgs<T> a) {
       t = t * red[4][r][c];
       const bool ok2 = r < rows && n0 + c < nm;
       gat[r * 33 + c] = ok2 ? t : T(0);
-      if (ok2 && a.ga2) a.ga2[(size_t)(m0 + r) * nm + n0 + c] = t;
+      if (ok2 && oga2) oga2[(size_t)(m0 + r) * nm + n0 + c] = t;
     }
     __syncthreads();
-    if (a.pb2 && tid < 32 && n0 + tid < nm) {
+    if (opb2 && tid < 32 && n0 + tid < nm) {
       T cs = T(0);
       for (int r = 0; r < rows; ++r) cs += gat[r * 33 + tid];
-      a.pb2[(size_t)rb * nm + n0 + tid] = cs;
+      opb2[(size_t)rb * nm + n0 + tid] = cs;
     }
-    if (a.pw3)
+    if (opw3)
       for (int e = tid; e < No * 32; e += MM_NT) {
         const int o = e >> 5, c = e & 31;
         if (n0 + c >= nm) continue;
         T acc = T(0);
         for (int r = 0; r < 32; ++r) acc += zt[r * 33 + o] * d3t[r * 33 + c];   // rows past M: gz = 0
-        a.pw3[(size_t)rb * No * nm + (size_t)o * nm + n0 + c] = acc;
+        opw3[(size_t)rb * No * nm + (size_t)o * nm + n0 + c] = acc;
       }
-    if (a.pb3 && first && tid < No) {
+    if (opb3 && first && tid < No) {
       T cs = T(0);
       for (int r = 0; r < rows; ++r) cs += zt[r * 33 + tid];
-      a.pb3[(size_t)rb * No + tid] = cs;
+      opb3[(size_t)rb * No + tid] = cs;
     }
     stamp(6);
   }
   if constexpr (EPI == MM_GA1) {
-    if (a.colpart) {
+    if (ocolpart) {
       __syncthreads();
       if (tid < 32 && n0 + tid < a.N) {
         T s = T(0);
         for (int r = 0; r < 32; ++r) s += red[0][r][tid];
-        a.colpart[(size_t)blockIdx.x * a.ldc + n0 + tid] = s;
+        ocolpart[(size_t)bk.x * a.ldc + n0 + tid] = s;
       }
     }
+  }
+}
+
+// amdgpu_waves_per_eu(4): two 8-wave workgroups per CU (≤ 128 registers): a batched fused launch
+// (MM_L23) needs all its problems' workgroups co-resident, and at 136 registers only one fit per CU.
+template <typename T, int EPI, int AOP, int BOP, int TA, int TB, int AV, int BV, int MK>
+__global__ __launch_bounds__(MM_NT) __attribute__((amdgpu_waves_per_eu(4))) void k_mm(MMArgs<T> a, MMProbs<T> pr) {
+  __shared__ T red[MM_NW][32][33];
+  __shared__ double rowl[32];
+  mm_body<T, EPI, AOP, BOP, TA, TB, AV, BV, MK>(
+      a, pr, Blk{(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z, (int)gridDim.x, (int)gridDim.y}, red, rowl);
+}
+
+// The batched fused forward at three workgroups per CU (≤ 80 registers, spilling the rest): all six
+// sub-steps' forwards then fit co-resident in one launch (HMCX_MLP_L23W=6; default 4 per launch).
+template <typename T, int EPI, int AOP, int BOP, int TA, int TB, int AV, int BV, int MK>
+__global__ __launch_bounds__(MM_NT) __attribute__((amdgpu_waves_per_eu(6))) void k_mm6(MMArgs<T> a, MMProbs<T> pr) {
+  __shared__ T red[MM_NW][32][33];
+  __shared__ double rowl[32];
+  mm_body<T, EPI, AOP, BOP, TA, TB, AV, BV, MK>(
+      a, pr, Blk{(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z, (int)gridDim.x, (int)gridDim.y}, red, rowl);
+}
+
+// Two independent launches as one: planes z < g1.z run grid 1 (g1.x × g1.y workgroups per plane, a
+// batched launch with its problems), the planes after it grid 2 (a plain launch, g2.x × g2.y).  The
+// launch grid is the larger of the two in x and y; workgroups outside their grid leave at once.
+template <typename T, int E1, int A1, int B1, int TA1, int TB1, int AV1, int BV1,
+          int E2, int A2, int B2, int TA2, int TB2, int AV2, int BV2, int MK>
+__global__ __launch_bounds__(MM_NT) __attribute__((amdgpu_waves_per_eu(4)))
+void k_mm2(MMArgs<T> a1, MMProbs<T> p1, MMArgs<T> a2, int3 g1, int2 g2) {
+  __shared__ T red[MM_NW][32][33];
+  __shared__ double rowl[32];
+  const int x = blockIdx.x, y = blockIdx.y, z = blockIdx.z;
+  if (z < g1.z) {
+    if (x < g1.x && y < g1.y) mm_body<T, E1, A1, B1, TA1, TB1, AV1, BV1, MK>(a1, p1, Blk{x, y, z, g1.x, g1.y}, red, rowl);
+  } else if (x < g2.x && y < g2.y) {
+    MMProbs<T> none;
+    none.n = 0;
+    mm_body<T, E2, A2, B2, TA2, TB2, AV2, BV2, MK>(a2, none, Blk{x, y, z - g1.z, g2.x, g2.y}, red, rowl);
   }
 }
 
@@ -777,7 +882,7 @@ __global__ __launch_bounds__(MM_NT) void k_l3_wide(MMArgs<T> a, const T* z) {
   T* scr = reinterpret_cast<T*>(dsm + 32 * sizeof(double));
   T* zt = scr + MM_NT;
   const int N = a.N, zs = N + 1, m0 = blockIdx.x * 32;
-  run_pending(a.pend);
+  run_pendset(a.pend, (int)blockIdx.x, (int)gridDim.x);
   for (int e = threadIdx.x; e < 32 * N; e += blockDim.x) {
     const int r = e / N, k = e - r * N;
     zt[r * zs + k] = (m0 + r < a.M) ? z[(size_t)(m0 + r) * N + k] + a.bias[k] : T(0);
@@ -795,6 +900,13 @@ __global__ void k_mlp_keep(uint8_t* keep, int n3, uint64_t seed, uint32_t chain,
   u32x4 c = {{(uint32_t)g, MASK_SLOT0 + (uint32_t)f, step, chain}};
   const u32x4 r = philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
   uint8_t* out = keep + (size_t)f * n3;
+  if ((n3 & 3) == 0) {                                         // the four flags in one 4-byte store
+    uint32_t w = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) w |= (keep_flag(r.v[q]) ? 1u : 0u) << (8 * q);
+    *reinterpret_cast<uint32_t*>(out + 4 * g) = w;
+    return;
+  }
 #pragma unroll
   for (int q = 0; q < 4; ++q)
     if (4 * g + q < n3) out[4 * g + q] = keep_flag(r.v[q]) ? 1 : 0;
@@ -838,6 +950,11 @@ __device__ inline void block_sum2(double a, double b, double* out_a, double* out
   if (t == 0) { *out_a = sa[0]; if (out_b) *out_b = sb[0]; }
 }
 
+// Blocks of grid.x that work on a variable of n elements (≈ 4 per thread): W1 (200,704 at config 3)
+// gets 196 blocks instead of a fixed 32, so no thread walks a long serial chain of loads and Philox
+// draws (k_mlp_init: 12.9 → 7.1 µs per step).  The other blocks only write zero partials.
+__device__ inline int var_blocks(int n) { return min((int)gridDim.x, max(1, (n + 1023) / 1024)); }
+
 // Momentum draw (hmc.py:82-87) + first drift q' = q + ε·p + partials of Σp², Σq² (part [2][6][NPART]).
 template <typename T>
 __global__ __launch_bounds__(256) void k_mlp_init(VarTab vt, T eps, int drift, int noise_mode, const double* noise,
@@ -846,8 +963,13 @@ __global__ __launch_bounds__(256) void k_mlp_init(VarTab vt, T eps, int drift, i
   const T* q = (const T*)vt.q[v];
   T* qn = (T*)vt.qn[v];
   T* p = (T*)vt.p[v];
+  const int nb = var_blocks(n);
+  if ((int)blockIdx.x >= nb) {                                 // block-uniform
+    if (threadIdx.x == 0) { part[v * NPART + blockIdx.x] = 0.0; part[(6 + v) * NPART + blockIdx.x] = 0.0; }
+    return;
+  }
   double sp = 0.0, sq = 0.0;
-  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += NPART * 256) {
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += nb * 256) {
     const uint32_t e = (uint32_t)(vt.e0[v] + i);
     const T z = noise_mode == HMCX_NOISE_BUFFER ? (T)noise[e] : philox_normal_t<T>(seed, chain, step, 0u, e);
     const T qv = q[i];
@@ -865,8 +987,13 @@ __global__ __launch_bounds__(256) void k_sumsq12(VarTab vt, double* part) {
   const int v = blockIdx.y, n = vt.n[v];
   const T* q = (const T*)vt.q[v];
   const T* p = (const T*)vt.p[v];
+  const int nb = var_blocks(n);
+  if ((int)blockIdx.x >= nb) {
+    if (threadIdx.x == 0) { part[v * NPART + blockIdx.x] = 0.0; part[(6 + v) * NPART + blockIdx.x] = 0.0; }
+    return;
+  }
   double sp = 0.0, sq = 0.0;
-  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += NPART * 256) {
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += nb * 256) {
     const double pv = (double)p[i], qv = (double)q[i];
     sp += pv * pv;
     sq += qv * qv;
@@ -885,13 +1012,15 @@ struct MlpAccept {
   int32_t* acc_flag;
 };
 // One workgroup of 26 × 32 threads: group g < 24 sums the NPART partials of (state g/12, kind, variable),
-// groups 24/25 the loss partials of the current / proposed state — each by a fixed-order tree.
+// groups 24/25 the loss partials of the current / proposed state — each lane a fixed-order strided
+// sum, then a fixed-order tree.
 __global__ __launch_bounds__(1024) void k_mlp_accept(MlpAccept a) {
   __shared__ double sh[26][32];
   const int t = threadIdx.x, g = t >> 5, j = t & 31;
   double x = 0.0;
   if (g < 24) {
-    x = (g < 12 ? a.part_cur : a.part_new)[(g % 12) * NPART + j];
+    const double* pp = (g < 12 ? a.part_cur : a.part_new) + (g % 12) * NPART;
+    for (int q = 0; q < NPART / 32; ++q) x += pp[q * 32 + j];
   } else if (g < 26) {
     const double* lp = g == 24 ? a.lp_cur : a.lp_new;
     for (int b = j; b < a.nlb; b += 32) x += lp[b];
@@ -957,10 +1086,13 @@ struct MlpNet {
   hipStream_t st;
   bool xw_valid = false;
   bool vec_masks = true;                 // masks may be read as 4-/2-element vectors
-  Pending<T> pend{};                     // consumed by the next launch
+  PendSet<T> pend{};                     // consumed by the next launch
   // fused layer 2 + layer 3 (MM_L23): granule arena and epoch counter of the context
   char* gx = nullptr; int gx_bytes = 0; hmcx_ctx* ctx = nullptr; int* abort_flag = nullptr; bool fuse = false;
+  double* lpart_scr = nullptr;           // batched sampler: the sub-step's loss partials (unused output)
   int force_abort = -1, l23_count = 0;   // HMCX_MLP_FORCE_ABORT: the fused launch (0-based, per call) that aborts
+  int l23_fit = 0;                       // fused grids that fit on the chip at once (occupancy × CUs / grid)
+  int l23_fit6 = 0;                      // the same for k_mm6 (HMCX_MLP_L23W=6)
   unsigned long long* prof = nullptr;    // HMCX_MLP_PROF: stamps of every fused launch of the call
   int prof_cap = 0;
   int nvar(int v) const {
@@ -981,23 +1113,40 @@ void net_init(MlpNet<T>& net, int B, int n_in, int n_mid, int n_out, hipStream_t
 // Launch k_mm for a call site with compile-time operand layouts (TA: A stored [K][M], TB: B stored
 // [N][K]); k-contiguous operands take the 16-byte vector path when aligned.  Takes the pending update.
 template <typename T, int EPI, int TA, int TB, int AOP = OP_PLAIN, int BOP = OP_PLAIN>
-hipError_t mm(MlpNet<T>& net, MMArgs<T>& a) {
+hipError_t mm(MlpNet<T>& net, MMArgs<T>& a, const MMProbs<T>* prp = nullptr, bool w6 = false) {
   if (a.ta != TA || a.tb != TB) return hipErrorInvalidValue;
   a.pend = net.pend;
-  net.pend.mode = UPD_NONE;
-  dim3 grid((a.M + 31) / 32, (a.N + 31) / 32), blk(MM_NT);
+  net.pend.n = 0;
+  MMProbs<T> pr{};
+  if (prp) pr = *prp;
+  // a batched launch: one plane per problem, plus one for the pending updates
+  dim3 grid((a.M + 31) / 32, (a.N + 31) / 32, pr.n > 0 ? pr.n + (a.pend.n > 0 ? 1 : 0) : 1), blk(MM_NT);
   if (EPI == MM_L3CE) grid.y = (unsigned)std::max(1, std::min(8, a.n_mid / 32));   // n_mid column slices
   const bool h1ok = AOP != OP_H1 || net.vec_masks;
   const bool kvec = a.K % (int)(16 / sizeof(T)) == 0;       // vectors never straddle the K end
-  const bool av = !TA && h1ok && kvec && vec_ok(a.A, a.lda, sizeof(T));
-  const bool bv = TB && kvec && vec_ok(a.B, a.ldb, sizeof(T));
+  bool aal = vec_ok(a.A, a.lda, sizeof(T)), bal = vec_ok(a.B, a.ldb, sizeof(T));
+  for (int p = 0; p < pr.n; ++p) {                            // every problem's operands
+    aal = aal && vec_ok(pr.p[p].A, a.lda, sizeof(T));
+    bal = bal && vec_ok(pr.p[p].B, a.ldb, sizeof(T));
+  }
+  const bool av = !TA && h1ok && kvec && aal;
+  const bool bv = TB && kvec && bal;
   hipStream_t st = net.st;
   auto go = [&](auto mkc) {
     constexpr int MK = decltype(mkc)::value;
-    if (av && bv) hipLaunchKernelGGL((k_mm<T, EPI, AOP, BOP, TA, TB, !TA, TB, MK>), grid, blk, 0, st, a);
-    else if (av) hipLaunchKernelGGL((k_mm<T, EPI, AOP, BOP, TA, TB, !TA, 0, MK>), grid, blk, 0, st, a);
-    else if (bv) hipLaunchKernelGGL((k_mm<T, EPI, AOP, BOP, TA, TB, 0, TB, MK>), grid, blk, 0, st, a);
-    else hipLaunchKernelGGL((k_mm<T, EPI, AOP, BOP, TA, TB, 0, 0, MK>), grid, blk, 0, st, a);
+    if constexpr (EPI == MM_L23) {
+      if (w6) {
+        if (av && bv) hipLaunchKernelGGL((k_mm6<T, EPI, AOP, BOP, TA, TB, !TA, TB, MK>), grid, blk, 0, st, a, pr);
+        else if (av) hipLaunchKernelGGL((k_mm6<T, EPI, AOP, BOP, TA, TB, !TA, 0, MK>), grid, blk, 0, st, a, pr);
+        else if (bv) hipLaunchKernelGGL((k_mm6<T, EPI, AOP, BOP, TA, TB, 0, TB, MK>), grid, blk, 0, st, a, pr);
+        else hipLaunchKernelGGL((k_mm6<T, EPI, AOP, BOP, TA, TB, 0, 0, MK>), grid, blk, 0, st, a, pr);
+        return;
+      }
+    }
+    if (av && bv) hipLaunchKernelGGL((k_mm<T, EPI, AOP, BOP, TA, TB, !TA, TB, MK>), grid, blk, 0, st, a, pr);
+    else if (av) hipLaunchKernelGGL((k_mm<T, EPI, AOP, BOP, TA, TB, !TA, 0, MK>), grid, blk, 0, st, a, pr);
+    else if (bv) hipLaunchKernelGGL((k_mm<T, EPI, AOP, BOP, TA, TB, 0, TB, MK>), grid, blk, 0, st, a, pr);
+    else hipLaunchKernelGGL((k_mm<T, EPI, AOP, BOP, TA, TB, 0, 0, MK>), grid, blk, 0, st, a, pr);
   };
   constexpr bool masked = AOP == OP_H1 || BOP == OP_H1 || EPI == MM_L2 || EPI == MM_L3CE || EPI == MM_GA1 ||
                           EPI == MM_L23;
@@ -1082,7 +1231,7 @@ hipError_t mlp_forward(MlpNet<T>& net, T* const* q, const MaskSrc<T>& ms, double
   }
   a.M = B; a.N = net.n_out; a.C = net.gz; a.ldc = net.n_out;
   a.pend = net.pend;
-  net.pend.mode = UPD_NONE;
+  net.pend.n = 0;
   const size_t lds = 32 * sizeof(double) + ((size_t)MM_NT + (size_t)32 * (net.n_out + 1)) * sizeof(T);
   if (a.ms.slot) hipLaunchKernelGGL((k_l3_wide<T, MK_PHILOX>), dim3(net.nlb), dim3(MM_NT), lds, net.st, a, (const T*)net.z);
   else if (a.ms.keep) hipLaunchKernelGGL((k_l3_wide<T, MK_KEEP>), dim3(net.nlb), dim3(MM_NT), lds, net.st, a, (const T*)net.z);
@@ -1120,24 +1269,166 @@ hipError_t mlp_wgrad(MlpNet<T>& net, T* const* q, const MaskSrc<T>& ms, int v, i
   return mm<T, MM_UPD, 1, 0>(net, a);
 }
 
+// xw = X·W1ᵀ into net.xw
 template <typename T>
-void set_pending(MlpNet<T>& net, int v, int mode, const Upd<T>& u) {
-  Pending<T>& p = net.pend;
+hipError_t mlp_layer1(MlpNet<T>& net, const T* W1) {
+  MMArgs<T> a{};
+  mm_set<T>(a, net.B, net.n_mid, net.n_in, net.X, net.n_in, 0, W1, net.n_in, 1, net.xw, net.n_mid);
+  net.xw_valid = true;
+  return mm<T, MM_STORE, 0, 1>(net, a);
+}
+
+// xw = X·W1ᵀ for np (W1, out) pairs in one launch
+template <typename T>
+hipError_t mlp_layer1_batch(MlpNet<T>& net, const T* const* W1, T* const* out, int np) {
+  MMArgs<T> a{};
+  MMProbs<T> pr{};
+  pr.n = np;
+  for (int p = 0; p < np; ++p) {
+    pr.p[p].A = net.X; pr.p[p].B = W1[p]; pr.p[p].C = out[p];
+  }
+  mm_set<T>(a, net.B, net.n_mid, net.n_in, net.X, net.n_in, 0, W1[0], net.n_in, 1, out[0], net.n_mid);
+  return mm<T, MM_STORE, 0, 1>(net, a, &pr);
+}
+
+// One sub-step's share of a batched launch: its positions, masks, scratch net (ga2, ga1, gz and the
+// gradient partials), loss partials and what its layer-3 backward must produce.
+template <typename T> struct SubStep {
+  const T* xw;                       // layer-1 output of its W1 (null: net's)
+  T* q[6];
+  MaskSrc<T> ms;
+  MlpNet<T>* scr;
+  double* lpart;
+  L3Want w;
+  int v;
+};
+
+// The fused forwards (MM_L23) of np sub-steps in one launch at net's xw (valid): problem p uses arena
+// region p and writes into its own scratch; net's pending updates run in it.
+template <typename T>
+hipError_t mlp_forward_batch(MlpNet<T>& net, const SubStep<T>* ss, int np, bool w6 = false) {
+  const int nm = net.n_mid;
+  MMArgs<T> a{};
+  MMProbs<T> pr{};
+  pr.n = np;
+  for (int p = 0; p < np; ++p) {
+    const SubStep<T>& s = ss[p];
+    const MlpNet<T>& sc = *s.scr;
+    MMProb<T>& q = pr.p[p];
+    q.A = s.xw ? s.xw : net.xw; q.B = s.q[2]; q.C = nullptr;
+    q.b1 = s.q[1]; q.bias = s.q[3]; q.W3 = s.q[4]; q.bias3 = s.q[5];
+    q.ms = s.ms;
+    q.ga2 = s.w.ga2 ? sc.ga2 : nullptr;
+    q.pb2 = s.w.pb2 ? sc.pb2 : nullptr;
+    q.pb3 = s.w.pb3 ? sc.pb3 : nullptr;
+    q.pw3 = s.w.pw3 ? sc.pw3 : nullptr;
+    q.gz = sc.gz; q.lpart = s.lpart; q.colpart = nullptr;
+    q.gx = net.gx + (size_t)p * net.gx_bytes;
+  }
+  const MMProb<T>& q0 = pr.p[0];
+  mm_set<T>(a, net.B, nm, nm, q0.A, nm, 0, q0.B, nm, 1, nullptr, nm);
+  a.bias = q0.bias; a.b1 = q0.b1; a.ms = q0.ms; a.C2 = nullptr;
+  a.N3 = net.n_out; a.bias3 = q0.bias3; a.gz = q0.gz; a.y = net.y; a.lpart = q0.lpart;
+  a.W3 = q0.W3; a.n_mid = nm;
+  a.ga2 = q0.ga2; a.pb2 = q0.pb2; a.pb3 = q0.pb3; a.pw3 = q0.pw3;
+  a.gx = q0.gx; a.gx_bytes = net.gx_bytes; a.ep = gx_next_epoch(net.ctx); a.abort_flag = net.abort_flag;
+  a.force_abort = net.l23_count == net.force_abort;
+  ++net.l23_count;
+  return mm<T, MM_L23, 0, 1, OP_H1>(net, a, &pr, w6);
+}
+
+// The layer-1 backwards (MM_GA1: ga1 = (ga2·W2)·gate, + b1 partials where wanted) of np sub-steps
+// in one launch, each from its own ga2 into its own ga1.
+template <typename T>
+hipError_t mlp_ga1_batch(MlpNet<T>& net, const SubStep<T>* const* ss, int np) {
+  const int nm = net.n_mid;
+  MMArgs<T> a{};
+  MMProbs<T> pr{};
+  pr.n = np;
+  for (int p = 0; p < np; ++p) {
+    const SubStep<T>& s = *ss[p];
+    MMProb<T>& q = pr.p[p];
+    q.A = s.scr->ga2; q.B = s.q[2]; q.C = s.scr->ga1;
+    q.b1 = s.q[1]; q.ms = s.ms;
+    q.colpart = s.v == 1 ? s.scr->pb1 : nullptr;
+  }
+  const MMProb<T>& q0 = pr.p[0];
+  mm_set<T>(a, net.B, nm, nm, q0.A, nm, 0, q0.B, nm, 0, q0.C, nm);
+  a.ms = q0.ms; a.H = net.xw; a.b1 = q0.b1; a.H1 = nullptr; a.colpart = q0.colpart;
+  return mm<T, MM_GA1, 0, 0>(net, a, &pr);
+}
+
+// The layer-1 backwards of np sub-steps (as mlp_ga1_batch) and the W2 gradient of sub-step net `w2n`
+// (ga2ᵀ·h1 with the SGHMC epilogue, as mlp_wgrad v = 2) in ONE launch (k_mm2): neither reads what the
+// other writes.  net's pending updates run in the first grid's extra plane.
+template <typename T>
+hipError_t mlp_ga1_w2(MlpNet<T>& net, const SubStep<T>* const* ss, int np, MlpNet<T>& w2n, const SubStep<T>& s2,
+                      const Upd<T>& u2) {
+  const int nm = net.n_mid;
+  MMArgs<T> a1{}, a2{};
+  MMProbs<T> pr{};
+  pr.n = np;
+  for (int p = 0; p < np; ++p) {
+    const SubStep<T>& s = *ss[p];
+    MMProb<T>& q = pr.p[p];
+    q.A = s.scr->ga2; q.B = s.q[2]; q.C = s.scr->ga1;
+    q.b1 = s.q[1]; q.ms = s.ms;
+    q.colpart = s.v == 1 ? s.scr->pb1 : nullptr;
+  }
+  const MMProb<T>& q0 = pr.p[0];
+  mm_set<T>(a1, net.B, nm, nm, q0.A, nm, 0, q0.B, nm, 0, q0.C, nm);
+  a1.ms = q0.ms; a1.H = net.xw; a1.b1 = q0.b1; a1.H1 = nullptr; a1.colpart = q0.colpart;
+  a1.pend = net.pend;
+  net.pend.n = 0;
+  mm_set<T>(a2, nm, nm, net.B, w2n.ga2, nm, 1, net.xw, nm, 0, nullptr, nm);   // ga2ᵀ·h1
+  a2.ms = s2.ms; a2.b1 = s2.q[1]; a2.upd_mode = UPD_SGHMC; a2.u = u2;
+  a2.pend = w2n.pend;
+  w2n.pend.n = 0;
+  if (((a1.ms.slot != 0) != (a2.ms.slot != 0)) || ((a1.ms.keep != nullptr) != (a2.ms.keep != nullptr)))
+    return hipErrorInvalidValue;                               // one mask kind per launch
+  const int3 g1 = make_int3((a1.M + 31) / 32, (a1.N + 31) / 32, np + (a1.pend.n > 0 ? 1 : 0));
+  const int2 g2 = make_int2((a2.M + 31) / 32, (a2.N + 31) / 32);
+  const dim3 grid((unsigned)std::max(g1.x, g2.x), (unsigned)std::max(g1.y, g2.y), (unsigned)(g1.z + 1));
+  bool aal = nm % (int)(16 / sizeof(T)) == 0;
+  for (int p = 0; p < np; ++p) aal = aal && vec_ok(pr.p[p].A, nm, sizeof(T));
+  hipStream_t st = net.st;
+  auto go = [&](auto mkc, auto avc) {
+    constexpr int MK = decltype(mkc)::value, AV = decltype(avc)::value;
+    hipLaunchKernelGGL((k_mm2<T, MM_GA1, OP_PLAIN, OP_PLAIN, 0, 0, AV, 0, MM_UPD, OP_PLAIN, OP_H1, 1, 0, 0, 0, MK>),
+                       grid, dim3(MM_NT), 0, st, a1, pr, a2, g1, g2);
+  };
+  auto go_mk = [&](auto mkc) {
+    if (aal) go(mkc, std::integral_constant<int, 1>{});
+    else go(mkc, std::integral_constant<int, 0>{});
+  };
+  if (a1.ms.slot) go_mk(std::integral_constant<int, MK_PHILOX>{});
+  else if (a1.ms.keep) go_mk(std::integral_constant<int, MK_KEEP>{});
+  else if (a1.ms.vals) go_mk(std::integral_constant<int, MK_VALS>{});
+  else go_mk(std::integral_constant<int, MK_NONE>{});
+  return hipGetLastError();
+}
+
+// Queue the update of variable v from the partials of `src` (default: net's own) on net's next launch.
+template <typename T>
+void set_pending(MlpNet<T>& net, int v, int mode, const Upd<T>& u, const MlpNet<T>* src = nullptr) {
+  if (!src) src = &net;
+  Pending<T>& p = net.pend.p[net.pend.n++];
   p.mode = mode; p.u = u; p.nparts = net.nlb;
   switch (v) {
-    case 1: p.part = net.pb1; p.n = net.n_mid; break;
-    case 3: p.part = net.pb2; p.n = net.n_mid; break;
-    case 4: p.part = net.pw3; p.n = net.n_out * net.n_mid; break;
-    default: p.part = net.pb3; p.n = net.n_out; break;
+    case 1: p.part = src->pb1; p.n = net.n_mid; break;
+    case 3: p.part = src->pb2; p.n = net.n_mid; break;
+    case 4: p.part = src->pw3; p.n = net.n_out * net.n_mid; break;
+    default: p.part = src->pb3; p.n = net.n_out; break;
   }
 }
 
 template <typename T>
 hipError_t flush_pending(MlpNet<T>& net) {
-  if (net.pend.mode == UPD_NONE) return hipSuccess;
-  const int n = net.pend.n;
+  if (net.pend.n == 0) return hipSuccess;
+  int n = 0;
+  for (int j = 0; j < net.pend.n; ++j) n = std::max(n, net.pend.p[j].n);
   hipLaunchKernelGGL(k_pending<T>, dim3((n + 255) / 256), dim3(256), 0, net.st, net.pend);
-  net.pend.mode = UPD_NONE;
+  net.pend.n = 0;
   return hipGetLastError();
 }
 
@@ -1145,8 +1436,9 @@ hipError_t flush_pending(MlpNet<T>& net) {
 // whole grid fits on the chip at once (its slice workgroups wait for each other); HMCX_MLP_FUSE=0 or
 // hmcx_set_mlp_fuse(ctx, 0) turns it off.  A timed-out exchange raises the MLP's own abort word
 // (ctx->mlp_abort_dev, never the persistent SGHMC kernels' word) and the call reports it (out_abort).
+// The arena holds `regions` equal parts: a batched fused launch gives problem p region p.
 template <typename T>
-int net_fuse(hmcx_ctx* ctx, MlpNet<T>& net) {
+int net_fuse(hmcx_ctx* ctx, MlpNet<T>& net, int regions = 1) {
   static const bool off = getenv("HMCX_MLP_FUSE") && getenv("HMCX_MLP_FUSE")[0] == '0';
   const int S = (net.n_mid + 31) / 32;
   if (off || ctx->mlp_nofuse || net.n_out > 32 || S > 16) return HMCX_OK;
@@ -1156,13 +1448,18 @@ int net_fuse(hmcx_ctx* ctx, MlpNet<T>& net) {
   if ((long)per_cu * ctx->num_cus < (long)net.nlb * S) return HMCX_OK;
   const size_t need = (size_t)net.nlb * S * 32 * net.n_out * 16;
   if (need > 0x7fffffff) return HMCX_OK;
-  if (int rc = gx_reserve(ctx, need)) return rc;
+  if (int rc = gx_reserve(ctx, need * regions)) return rc;
+  net.l23_fit = std::min(regions, (int)((long)per_cu * ctx->num_cus / ((long)net.nlb * S)));
+  const void* kfn6 = (const void*)k_mm6<T, MM_L23, OP_H1, OP_PLAIN, 0, 1, 1, 1, MK_KEEP>;
+  int per_cu6 = 0;
+  HMCX_HIP(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu6, kfn6, MM_NT, 0));
+  net.l23_fit6 = std::min(regions, (int)((long)per_cu6 * ctx->num_cus / ((long)net.nlb * S)));
   if (!ctx->mlp_abort_dev) {
     HMCX_HIP(ctx, hipMalloc((void**)&ctx->mlp_abort_dev, sizeof(int)));
     HMCX_HIP(ctx, hipMemsetAsync(ctx->mlp_abort_dev, 0, sizeof(int), ctx->stream));
   }
   net.gx = ctx->gx_arena;
-  net.gx_bytes = (int)ctx->gx_bytes;
+  net.gx_bytes = (int)need;
   net.ctx = ctx;
   net.abort_flag = ctx->mlp_abort_dev;
   net.fuse = true;
@@ -1260,7 +1557,7 @@ template <typename T>
 int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
   MlpNet<T> net{};
   net_init(net, s->B, s->n_in, s->n_mid, s->n_out, ctx->stream);
-  if (int rc0 = net_fuse<T>(ctx, net)) return rc0;
+  if (int rc0 = net_fuse<T>(ctx, net, MAXPROB)) return rc0;
   const int mn = s->B * s->n_mid, n3 = 3 * mn;
   int off_v[6], dim[6], P = 0;                                // element offset of each variable in `order`
   {
@@ -1290,6 +1587,20 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
   const bool keep_arr = philox_masks && !(mk_env && !strcmp(mk_env, "philox"));
   const char* h1_env = getenv("HMCX_MLP_H1");
   const bool store_h1 = philox_masks && h1_env && h1_env[0] == '1';    // m0 ∈ {0, scale} only for Philox masks
+  // Batched iterations.  Sub-step i of leapfrog iteration it (variable v = order[i]) evaluates the
+  // gradient at q_u(it) for the variables at order positions u ≤ i and q_u(it − 1) for the others
+  // (sghmc.py:29-34: each variable is drifted just before its own gradient call) and moves only v's
+  // momentum and v's NEXT position — so it needs iteration it − 1 complete and nothing of iteration it:
+  // the six sub-steps of one iteration are independent.  With W1 first (one xw per iteration), an
+  // iteration is: layer 1 (+ the previous iteration's bias / W3 updates in its prologue), the six fused
+  // forwards in one launch (or in chunks of what fits co-resident), the W1 / b1 layer-1 backwards in
+  // one launch, the W1 and W2 gradients with their SGHMC epilogues — 5 launches instead of 11.  Same
+  // kernels, operands, masks and noise as the one-at-a-time order: identical results.
+  // HMCX_MLP_BATCH=0 runs the sub-steps one at a time.
+  const char* batch_env = getenv("HMCX_MLP_BATCH");             // read per call (tests switch it)
+  const bool batch_off = batch_env && batch_env[0] == '0';
+  const bool batch = !batch_off && net.fuse && s->order[0] == 0 && !store_h1 && net.l23_fit >= 1;
+  MlpNet<T> pn[6]{};
   if (philox_masks) {
     if (n3 % 4) net.vec_masks = false;
   } else {
@@ -1298,7 +1609,7 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
       if ((s->mask_off[si] * sizeof(T)) % 16) net.vec_masks = false;
   }
   Workspace ws(ctx);
-  T *pv[6], *qa[6], *qb[6];
+  T *pv[6], *qa[6], *qb[6], *qc[6], *xw_par = nullptr;
   double *part_cur, *part_new, *lp_cur, *lp_new, *lp_scr;
   uint8_t* keep = nullptr;
   int32_t* accf;
@@ -1307,10 +1618,19 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
   do {
     ws.reset();
     mlp_workspace<T>(ws, net);
+    for (int i = 0; i < 6 && batch; ++i) {
+      net_init(pn[i], s->B, s->n_in, s->n_mid, s->n_out, ctx->stream);
+      mlp_workspace<T>(ws, pn[i]);
+      pn[i].lpart_scr = ws.take<double>(net.nlb);
+    }
     net.prof = prof_cap ? ws.take<unsigned long long>((size_t)prof_cap * net.nlb * ((net.n_mid + 31) / 32) * L23_NPH)
                         : nullptr;
     net.prof_cap = prof_cap;
-    for (int v = 0; v < 6; ++v) { pv[v] = ws.take<T>(dim[v]); qa[v] = ws.take<T>(dim[v]); qb[v] = ws.take<T>(dim[v]); }
+    for (int v = 0; v < 6; ++v) {
+      pv[v] = ws.take<T>(dim[v]); qa[v] = ws.take<T>(dim[v]); qb[v] = ws.take<T>(dim[v]);
+      qc[v] = batch ? ws.take<T>(dim[v]) : nullptr;
+    }
+    if (batch) xw_par = ws.take<T>((size_t)mn);
     part_cur = ws.take<double>(12 * NPART);
     part_new = ws.take<double>(12 * NPART);
     lp_cur = ws.take<double>(net.nlb);
@@ -1362,21 +1682,92 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
     T* cur[6];
     for (int v = 0; v < 6; ++v) cur[v] = par[v];
     int fwd = 0;
-    for (int it = 0; it < n; ++it) {
+    auto upd_for = [&](int it, int v, T* W, T* Qn) {
+      Upd<T> u{};
+      u.W = W; u.P = pv[v]; u.Qn = Qn;
+      u.half_alpha = (T)(0.5 * s->alpha); u.eps = (T)eps; u.one_minus_eps = (T)(1.0 - eps);
+      u.noise_scale = (T)(2.0 * eps);
+      u.noise_mode = s->noise_mode;
+      u.noise = nz ? nz + (size_t)P * (it + 1) + off_v[v] : nullptr;   // BUFFER: one block of P per iteration
+      u.seed = s->seed; u.chain = s->chain; u.step = step_id; u.slot = (uint32_t)(it + 1);
+      u.e0 = (uint32_t)off_v[v];
+      return u;
+    };
+    if (batch && n > 0) {
+      // positions of iteration it in q3[it % 3]: the sub-steps of iteration it read iterations it and
+      // it − 1 and write it + 1, so three sets never alias within an iteration (the pending updates of
+      // the bias / W3 sub-steps then run beside readers of it − 1)
+      T* const* q3[3] = {qa, qb, qc};
+      const char* w_env = getenv("HMCX_MLP_L23W");
+      const bool w6 = w_env && w_env[0] == '6' && net.l23_fit6 > net.l23_fit;
+      const int fit = std::min(MAXPROB, w6 ? net.l23_fit6 : net.l23_fit);
+      for (int i = 0; i < 6; ++i) {
+        pn[i].X = net.X; pn[i].y = net.y; pn[i].xw = net.xw; pn[i].vec_masks = net.vec_masks;
+      }
+      for (int it = 0; it < n; ++it) {
+        T* const* Xit = q3[it % 3];                              // positions of iteration it
+        T* const* Xpr = it == 0 ? par : q3[(it + 2) % 3];        // of iteration it − 1
+        T* const* Xnx = q3[(it + 1) % 3];                        // the next iteration's (written here)
+        if (it == 0) {                                           // xw(0) and the start state's xw (E_current)
+          const T* w1[2] = {qa[0], par[0]};
+          T* out[2] = {net.xw, xw_par};
+          HMCX_HIP(ctx, mlp_layer1_batch<T>(net, w1, out, 2));
+        } else {
+          HMCX_HIP(ctx, mlp_layer1<T>(net, Xit[0]));
+        }
+        SubStep<T> ss[6];
+        const SubStep<T>* ga[6];
+        int nga = 0;
+        for (int i = 0; i < 6; ++i) {
+          const int v = s->order[i];
+          SubStep<T>& x = ss[i];
+          x.xw = nullptr;
+          for (int j = 0; j < 6; ++j) x.q[s->order[j]] = j <= i ? Xit[s->order[j]] : Xpr[s->order[j]];
+          x.ms = masks_for(6 * it + i);
+          x.scr = &pn[i];
+          x.lpart = pn[i].lpart_scr;
+          x.w = L3Want{v <= 3, v == 3, v == 5, v == 4, false};
+          x.v = v;
+          if (v <= 1) ga[nga++] = &ss[i];
+        }
+        for (int i0 = 0; i0 < 6; i0 += fit) HMCX_HIP(ctx, mlp_forward_batch<T>(net, ss + i0, std::min(fit, 6 - i0), w6));
+        // bias / W3 updates from their partials: b2, W3, b3 (partials of the fused forwards) in the
+        // layer-1 backward launch, b1 (whose partials that launch makes) in the W1 gradient launch
+        for (int i = 0; i < 6; ++i) {
+          const int v = s->order[i];
+          if (v == 0 || v == 2) continue;
+          set_pending(v == 1 ? pn[0] : net, v, UPD_SGHMC, upd_for(it, v, Xit[v], it + 1 < n ? Xnx[v] : nullptr), &pn[i]);
+        }
+        int i2 = 0;                                              // the W2 sub-step rides in the
+        while (s->order[i2] != 2) ++i2;                          // layer-1 backward launch
+        HMCX_HIP(ctx, mlp_ga1_w2<T>(net, ga, nga, pn[i2], ss[i2], upd_for(it, 2, Xit[2], it + 1 < n ? Xnx[2] : nullptr)));
+        HMCX_HIP(ctx, mlp_wgrad<T>(pn[0], ss[0].q, ss[0].ms, 0, UPD_SGHMC,
+                                   upd_for(it, 0, Xit[0], it + 1 < n ? Xnx[0] : nullptr)));
+        fwd += 6;
+      }
+      for (int v = 0; v < 6; ++v) cur[v] = q3[(n - 1) % 3][v];
+      // energies (hmc.py:67-71: E_new with forward 6n's masks, E_current with forward 6n + 1's) in one launch
+      SubStep<T> es[2];
+      for (int e = 0; e < 2; ++e) {
+        SubStep<T>& x = es[e];
+        x.xw = e == 0 ? net.xw : xw_par;
+        for (int v = 0; v < 6; ++v) x.q[v] = e == 0 ? cur[v] : par[v];
+        x.ms = masks_for(fwd + e);
+        x.scr = &pn[e];
+        x.lpart = e == 0 ? lp_new : lp_cur;
+        x.w = L3Want{false, false, false, false, false};
+        x.v = -1;
+      }
+      for (int e0 = 0; e0 < 2; e0 += fit) HMCX_HIP(ctx, mlp_forward_batch<T>(net, es + e0, std::min(fit, 2 - e0), w6));
+      fwd += 2;
+    }
+    for (int it = 0; it < n && !batch; ++it) {
       for (int i = 0; i < 6; ++i) {
         const int v = s->order[i];
         cur[v] = (it & 1) ? qb[v] : qa[v];                    // drifted position of this iteration
         if (v == 0) net.xw_valid = false;
         const MaskSrc<T> ms = masks_for(fwd++);
-        Upd<T> u{};
-        u.W = cur[v]; u.P = pv[v];
-        u.Qn = it + 1 < n ? ((it & 1) ? qa[v] : qb[v]) : nullptr;
-        u.half_alpha = (T)(0.5 * s->alpha); u.eps = (T)eps; u.one_minus_eps = (T)(1.0 - eps);
-        u.noise_scale = (T)(2.0 * eps);
-        u.noise_mode = s->noise_mode;
-        u.noise = nz ? nz + (size_t)P * (it + 1) + off_v[v] : nullptr;   // BUFFER: one block of P per iteration
-        u.seed = s->seed; u.chain = s->chain; u.step = step_id; u.slot = (uint32_t)(it + 1);
-        u.e0 = (uint32_t)off_v[v];
+        const Upd<T> u = upd_for(it, v, cur[v], it + 1 < n ? ((it & 1) ? qa[v] : qb[v]) : nullptr);
         // h1 from the fused forward for the W1 / b1 / W2 sub-steps (HMCX_MLP_H1=0: recompute it)
         const L3Want w{v <= 3, v == 3, v == 5, v == 4, store_h1 && v <= 2};
         HMCX_HIP(ctx, mlp_forward<T>(net, cur, ms, lp_scr, w));
@@ -1386,9 +1777,11 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
       }
     }
     // energies (hmc.py:67-71: E_new first, then E_current), each with fresh masks
-    HMCX_HIP(ctx, mlp_forward<T>(net, cur, masks_for(fwd++), lp_new, L3Want{false, false, false, false}));
-    net.xw_valid = false;
-    HMCX_HIP(ctx, mlp_forward<T>(net, par, masks_for(fwd++), lp_cur, L3Want{false, false, false, false}));
+    if (!(batch && n > 0)) {
+      HMCX_HIP(ctx, mlp_forward<T>(net, cur, masks_for(fwd++), lp_new, L3Want{false, false, false, false}));
+      net.xw_valid = false;
+      HMCX_HIP(ctx, mlp_forward<T>(net, par, masks_for(fwd++), lp_cur, L3Want{false, false, false, false}));
+    }
     HMCX_HIP(ctx, flush_pending(net));
     VarTab ve{};
     for (int i = 0; i < 6; ++i) {

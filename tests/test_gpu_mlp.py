@@ -401,3 +401,37 @@ def test_sampler_philox_masks_equal_api_masks(variant, monkeypatch):
     assert L1 == L2 and a1 == a2 and max(L1) >= 2
     for k in p1:
         np.testing.assert_array_equal(p1[k], p2[k])
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+@pytest.mark.parametrize("order", ["natural", "w1-first-permuted"])
+def test_batched_iterations_equal_one_at_a_time(dtype, order, monkeypatch):
+    """The sampler's batched iterations (the six sub-steps of a leapfrog iteration as one fused-forward
+    launch, one layer-1-backward launch and the two weight-gradient launches: they only depend on the
+    previous iteration) give the one-sub-step-at-a-time trajectory bit for bit (HMCX_MLP_BATCH=0):
+    config-3 shape, Philox noise and masks, both dtypes, the natural variable order and a permuted
+    one with W1 first."""
+    mlp, sghmc = _mlp_cls()
+    n_in, n_mid, n_out, N, B = 784, 256, 10, 1000, 500
+    rs = np.random.RandomState(9)
+    X = rs.rand(N, n_in)
+    y = rs.randint(0, n_out, N)
+    m = mlp({"alpha": 0.01}, n_in, n_mid, n_out, dtype=dtype, device="cuda:0")
+    start = m.init_params(6)
+    if order != "natural":
+        keys = list(start)
+        start = {k: start[k] for k in [keys[0], keys[4], keys[2], keys[5], keys[1], keys[3]]}
+    kw = dict(path_length=4e-3, step_size=1e-3, verbose=False, noise='philox', seed=7, chain=1)
+    runs = []
+    for batch in ("1", "0"):
+        monkeypatch.setenv("HMCX_MLP_BATCH", batch)
+        s = sghmc(m, start, **kw)
+        s.trace, s.out = [], io.StringIO()
+        post, logp = s.sample(epochs=2, burnin=1, batch_size=B, X_train=X, y_train=y)
+        runs.append((post, logp, [t["L"] for t in s.trace], [t["accepted"] for t in s.trace]))
+    monkeypatch.delenv("HMCX_MLP_BATCH")
+    (p1, l1, L1, a1), (p2, l2, L2, a2) = runs
+    assert L1 == L2 and a1 == a2 and max(L1) >= 3
+    for k in p1:
+        np.testing.assert_array_equal(p1[k], p2[k])
+    np.testing.assert_array_equal(l1, l2)
