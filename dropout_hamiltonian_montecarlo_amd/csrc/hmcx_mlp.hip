@@ -23,11 +23,14 @@
 //  * Deferred updates: the gradient of a bias (or of W3) is a sum of per-row-block partials; its
 //    gradient / SGHMC update runs in the prologue of whatever kernel is launched next (none of them
 //    reads the momentum or the next-position buffer it writes) — no reduction launch.
-//  * k_mlp_keep: the keep flags of every dropout mask of one SGHMC step (Philox, one launch/step).
-//  * k_mlp_init / k_sumsq12 / k_mlp_accept / k_mlp_commit: momentum draw + first drift + energy
-//    partials, end-of-trajectory energy partials, MH accept (hmc.py:67-79), commit on accept.
-// Per leapfrog iteration at order (W1, b1, W2, b2, W3, b3): 17 launches, ≈1.0 GFLOP at
-// 784-256-256-10, B = 500 (layer 1 runs once, after W1 moved).
+//  * k_mlp_start (k_mlp_init + keep_flags) / k_sumsq12 / k_mlp_accept / k_mlp_commit: momentum draw,
+//    first drift and energy partials together with the keep flags of every dropout mask of the step
+//    (Philox), end-of-trajectory energy partials, MH accept (hmc.py:67-79), commit on accept.
+//  * Batched iterations (mlp_sghmc_t): the six sub-steps of a leapfrog iteration only depend on the
+//    previous iteration, so their kernels go out as multi-problem launches (k_mmb, blockIdx.z = sub-step)
+//    and one dual launch (k_mm2: layer-1 backwards + W2 gradient); ≈1.0 GFLOP per iteration at
+//    784-256-256-10, B = 500 (layer 1 runs once, after W1 moved), 5 launches per iteration (11 one
+//    sub-step at a time).
 #include "hmcx_common.h"
 #include "hmcx_internal.h"
 #include "hmcx_granule.h"
@@ -231,10 +234,12 @@ template <typename T> struct MMProb {
   T* ga2; T* pb2; T* pb3; T* pw3; T* gz; double* lpart; T* colpart;
   char* gx;                          // MM_L23: the problem's own region of the granule arena
 };
-template <typename T> struct MMProbs {
-  MMProb<T> p[MAXPROB];
+template <typename T, int NP> struct MMProbsN {
+  MMProb<T> p[NP];
   int n;                             // 0: a plain launch
 };
+template <typename T> using MMProbs = MMProbsN<T, MAXPROB>;
+template <typename T> using MMProbs3 = MMProbsN<T, 3>;   // the sub-grids of a dual launch
 
 template <typename T, int OP>
 __device__ inline T op_apply(T x, T mask, T bias) {
@@ -544,21 +549,17 @@ __device__ inline void mm_epilogue(const MMArgs<T>& a, int m, int n, T v) {
 // The workgroup's place in its (sub-)grid: a dual launch (k_mm2) runs two grids in one.
 struct Blk { int x, y, z, gx, gy; };
 
-template <typename T, int EPI, int AOP, int BOP, int TA, int TB, int AV, int BV, int MK>
-__device__ __forceinline__ void mm_body(const MMArgs<T>& a, const MMProbs<T>& pr, const Blk bk,
+template <typename T, int EPI, int AOP, int BOP, int TA, int TB, int AV, int BV, int MK, typename PR>
+__device__ __forceinline__ void mm_body(const MMArgs<T>& a, const PR& pr, const Blk bk,
                                         T (&red)[MM_NW][32][33], double* rowl) {
   using M = mfma16<T>;
   const int pbid0 = bk.y * bk.gx + bk.x, nb0 = bk.gx * bk.gy;
-  // MM_L23 runs the pending updates while its logit partials travel (below); nothing in this launch
-  // reads what they write (the momentum and the NEXT iteration's position buffer of other variables).
-  // A batched launch runs them in its extra plane (z = pr.n) and nowhere else.
-  if (pr.n > 0) {
-    if ((int)bk.z == pr.n) {
-      run_pendset(a.pend, pbid0, nb0);
-      return;
-    }
-  } else if constexpr (EPI != MM_L23) {
+  // The pending updates run in an extra plane of workgroups of their own (z = number of problems, 1
+  // for a plain launch), beside the GEMM: nothing in this launch reads what they write (the momentum
+  // and the NEXT iteration's position buffer of other variables), and no GEMM workgroup waits for them.
+  if ((int)bk.z == (pr.n > 0 ? pr.n : 1)) {
     run_pendset(a.pend, pbid0, nb0);
+    return;
   }
   // batched launch (pr.n > 0): the problem of this workgroup (bk.z) supplies the operands, masks
   // and outputs; the kernel argument block itself is never copied (a local MMArgs would live in scratch)
@@ -770,7 +771,6 @@ __device__ __forceinline__ void mm_body(const MMArgs<T>& a, const MMProbs<T>& pr
       gx_put(rs, base_rb + s * items + tid, (double)zp, a.ep);
     }
     stamp(2);
-    if (pr.n == 0) run_pendset(a.pend, pbid0, nb0);                          // while the partials travel
     stamp(3);
     if (tid < items) {
       const int r = tid / No, o = tid - r * No;
@@ -836,18 +836,19 @@ __device__ __forceinline__ void mm_body(const MMArgs<T>& a, const MMProbs<T>& pr
 
 // amdgpu_waves_per_eu(4): two 8-wave workgroups per CU (≤ 128 registers): a batched fused launch
 // (MM_L23) needs all its problems' workgroups co-resident, and at 136 registers only one fit per CU.
+// A plain launch (k_mm) and a batched one (k_mmb, blockIdx.z = problem): the plain kernel keeps the
+// small argument block (no problem table).
 template <typename T, int EPI, int AOP, int BOP, int TA, int TB, int AV, int BV, int MK>
-__global__ __launch_bounds__(MM_NT) __attribute__((amdgpu_waves_per_eu(4))) void k_mm(MMArgs<T> a, MMProbs<T> pr) {
+__global__ __launch_bounds__(MM_NT) __attribute__((amdgpu_waves_per_eu(4))) void k_mm(MMArgs<T> a) {
   __shared__ T red[MM_NW][32][33];
   __shared__ double rowl[32];
+  MMProbsN<T, 1> none;
+  none.n = 0;
   mm_body<T, EPI, AOP, BOP, TA, TB, AV, BV, MK>(
-      a, pr, Blk{(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z, (int)gridDim.x, (int)gridDim.y}, red, rowl);
+      a, none, Blk{(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z, (int)gridDim.x, (int)gridDim.y}, red, rowl);
 }
-
-// The batched fused forward at three workgroups per CU (≤ 80 registers, spilling the rest): all six
-// sub-steps' forwards then fit co-resident in one launch (HMCX_MLP_L23W=6; default 4 per launch).
 template <typename T, int EPI, int AOP, int BOP, int TA, int TB, int AV, int BV, int MK>
-__global__ __launch_bounds__(MM_NT) __attribute__((amdgpu_waves_per_eu(6))) void k_mm6(MMArgs<T> a, MMProbs<T> pr) {
+__global__ __launch_bounds__(MM_NT) __attribute__((amdgpu_waves_per_eu(4))) void k_mmb(MMArgs<T> a, MMProbs<T> pr) {
   __shared__ T red[MM_NW][32][33];
   __shared__ double rowl[32];
   mm_body<T, EPI, AOP, BOP, TA, TB, AV, BV, MK>(
@@ -860,16 +861,31 @@ __global__ __launch_bounds__(MM_NT) __attribute__((amdgpu_waves_per_eu(6))) void
 template <typename T, int E1, int A1, int B1, int TA1, int TB1, int AV1, int BV1,
           int E2, int A2, int B2, int TA2, int TB2, int AV2, int BV2, int MK>
 __global__ __launch_bounds__(MM_NT) __attribute__((amdgpu_waves_per_eu(4)))
-void k_mm2(MMArgs<T> a1, MMProbs<T> p1, MMArgs<T> a2, int3 g1, int2 g2) {
+void k_mm2(MMArgs<T> a1, MMProbs3<T> p1, MMArgs<T> a2, int3 g1, int2 g2) {
   __shared__ T red[MM_NW][32][33];
   __shared__ double rowl[32];
   const int x = blockIdx.x, y = blockIdx.y, z = blockIdx.z;
   if (z < g1.z) {
     if (x < g1.x && y < g1.y) mm_body<T, E1, A1, B1, TA1, TB1, AV1, BV1, MK>(a1, p1, Blk{x, y, z, g1.x, g1.y}, red, rowl);
   } else if (x < g2.x && y < g2.y) {
-    MMProbs<T> none;
+    MMProbsN<T, 1> none;
     none.n = 0;
     mm_body<T, E2, A2, B2, TA2, TB2, AV2, BV2, MK>(a2, none, Blk{x, y, z - g1.z, g2.x, g2.y}, red, rowl);
+  }
+}
+
+// Two batched launches as one: planes z < g1.z run batched grid 1, the next g2.z planes batched grid 2.
+template <typename T, int E1, int A1, int B1, int TA1, int TB1, int AV1, int BV1,
+          int E2, int A2, int B2, int TA2, int TB2, int AV2, int BV2, int MK>
+__global__ __launch_bounds__(MM_NT) __attribute__((amdgpu_waves_per_eu(4)))
+void k_mm2b(MMArgs<T> a1, MMProbs3<T> p1, MMArgs<T> a2, MMProbs3<T> p2, int3 g1, int3 g2) {
+  __shared__ T red[MM_NW][32][33];
+  __shared__ double rowl[32];
+  const int x = blockIdx.x, y = blockIdx.y, z = blockIdx.z;
+  if (z < g1.z) {
+    if (x < g1.x && y < g1.y) mm_body<T, E1, A1, B1, TA1, TB1, AV1, BV1, MK>(a1, p1, Blk{x, y, z, g1.x, g1.y}, red, rowl);
+  } else if (x < g2.x && y < g2.y) {
+    mm_body<T, E2, A2, B2, TA2, TB2, AV2, BV2, MK>(a2, p2, Blk{x, y, z - g1.z, g2.x, g2.y}, red, rowl);
   }
 }
 
@@ -893,9 +909,8 @@ __global__ __launch_bounds__(MM_NT) void k_l3_wide(MMArgs<T> a, const T* z) {
   l3_backward<T, MK>(a, zt, zs, m0, blockIdx.x, scr, MM_NT, 0, a.n_mid, true);
 }
 
-// Keep flags of F forwards (blockIdx.y = forward f, Philox slot MASK_SLOT0 + f), 3·mn per forward.
-__global__ void k_mlp_keep(uint8_t* keep, int n3, uint64_t seed, uint32_t chain, uint32_t step) {
-  const int g = blockIdx.x * blockDim.x + threadIdx.x, f = blockIdx.y;
+// Keep flags of forward f (Philox slot MASK_SLOT0 + f, 3·mn per forward), four per thread g.
+__device__ inline void keep_flags(uint8_t* keep, int n3, uint64_t seed, uint32_t chain, uint32_t step, int g, int f) {
   if (4 * g >= n3) return;
   u32x4 c = {{(uint32_t)g, MASK_SLOT0 + (uint32_t)f, step, chain}};
   const u32x4 r = philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
@@ -953,23 +968,23 @@ __device__ inline void block_sum2(double a, double b, double* out_a, double* out
 // Blocks of grid.x that work on a variable of n elements (≈ 4 per thread): W1 (200,704 at config 3)
 // gets 196 blocks instead of a fixed 32, so no thread walks a long serial chain of loads and Philox
 // draws (k_mlp_init: 12.9 → 7.1 µs per step).  The other blocks only write zero partials.
-__device__ inline int var_blocks(int n) { return min((int)gridDim.x, max(1, (n + 1023) / 1024)); }
+__device__ inline int var_blocks(int n) { return min(NPART, max(1, (n + 1023) / 1024)); }
 
 // Momentum draw (hmc.py:82-87) + first drift q' = q + ε·p + partials of Σp², Σq² (part [2][6][NPART]).
 template <typename T>
-__global__ __launch_bounds__(256) void k_mlp_init(VarTab vt, T eps, int drift, int noise_mode, const double* noise,
-                                                  uint64_t seed, uint32_t chain, uint32_t step, double* part) {
-  const int v = blockIdx.y, n = vt.n[v];
+__device__ inline void init_block(const VarTab& vt, T eps, int drift, int noise_mode, const double* noise,
+                                  uint64_t seed, uint32_t chain, uint32_t step, double* part, int v, int bx) {
+  const int n = vt.n[v];
   const T* q = (const T*)vt.q[v];
   T* qn = (T*)vt.qn[v];
   T* p = (T*)vt.p[v];
   const int nb = var_blocks(n);
-  if ((int)blockIdx.x >= nb) {                                 // block-uniform
-    if (threadIdx.x == 0) { part[v * NPART + blockIdx.x] = 0.0; part[(6 + v) * NPART + blockIdx.x] = 0.0; }
+  if (bx >= nb) {                                              // block-uniform
+    if (threadIdx.x == 0) { part[v * NPART + bx] = 0.0; part[(6 + v) * NPART + bx] = 0.0; }
     return;
   }
   double sp = 0.0, sq = 0.0;
-  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += nb * 256) {
+  for (int i = bx * 256 + threadIdx.x; i < n; i += nb * 256) {
     const uint32_t e = (uint32_t)(vt.e0[v] + i);
     const T z = noise_mode == HMCX_NOISE_BUFFER ? (T)noise[e] : philox_normal_t<T>(seed, chain, step, 0u, e);
     const T qv = q[i];
@@ -978,7 +993,25 @@ __global__ __launch_bounds__(256) void k_mlp_init(VarTab vt, T eps, int drift, i
     sp += (double)z * (double)z;
     sq += (double)qv * (double)qv;
   }
-  block_sum2(sp, sq, part + v * NPART + blockIdx.x, part + (6 + v) * NPART + blockIdx.x);
+  block_sum2(sp, sq, part + v * NPART + bx, part + (6 + v) * NPART + bx);
+}
+template <typename T>
+__global__ __launch_bounds__(256) void k_mlp_init(VarTab vt, T eps, int drift, int noise_mode, const double* noise,
+                                                  uint64_t seed, uint32_t chain, uint32_t step, double* part) {
+  init_block<T>(vt, eps, drift, noise_mode, noise, seed, chain, step, part, (int)blockIdx.y, (int)blockIdx.x);
+}
+// Step start in one launch: rows y < 6 draw the momentum of variable y and the first drift (k_mlp_init),
+// rows y ≥ 6 the keep flags of forward y − 6 (k_mlp_keep) — independent work, one launch less per step.
+template <typename T>
+__global__ __launch_bounds__(256) void k_mlp_start(VarTab vt, T eps, int drift, int noise_mode, const double* noise,
+                                                   uint64_t seed, uint32_t chain, uint32_t step, double* part,
+                                                   uint8_t* keep, int n3) {
+  if (blockIdx.y < 6) {
+    if (blockIdx.x < NPART)
+      init_block<T>(vt, eps, drift, noise_mode, noise, seed, chain, step, part, (int)blockIdx.y, (int)blockIdx.x);
+  } else {
+    keep_flags(keep, n3, seed, chain, step, (int)(blockIdx.x * blockDim.x + threadIdx.x), (int)blockIdx.y - 6);
+  }
 }
 
 // End-of-trajectory partials: part[0][i] = Σp², part[1][i] = Σq² per variable (same layout as init).
@@ -1092,7 +1125,6 @@ struct MlpNet {
   double* lpart_scr = nullptr;           // batched sampler: the sub-step's loss partials (unused output)
   int force_abort = -1, l23_count = 0;   // HMCX_MLP_FORCE_ABORT: the fused launch (0-based, per call) that aborts
   int l23_fit = 0;                       // fused grids that fit on the chip at once (occupancy × CUs / grid)
-  int l23_fit6 = 0;                      // the same for k_mm6 (HMCX_MLP_L23W=6)
   unsigned long long* prof = nullptr;    // HMCX_MLP_PROF: stamps of every fused launch of the call
   int prof_cap = 0;
   int nvar(int v) const {
@@ -1113,14 +1145,14 @@ void net_init(MlpNet<T>& net, int B, int n_in, int n_mid, int n_out, hipStream_t
 // Launch k_mm for a call site with compile-time operand layouts (TA: A stored [K][M], TB: B stored
 // [N][K]); k-contiguous operands take the 16-byte vector path when aligned.  Takes the pending update.
 template <typename T, int EPI, int TA, int TB, int AOP = OP_PLAIN, int BOP = OP_PLAIN>
-hipError_t mm(MlpNet<T>& net, MMArgs<T>& a, const MMProbs<T>* prp = nullptr, bool w6 = false) {
+hipError_t mm(MlpNet<T>& net, MMArgs<T>& a, const MMProbs<T>* prp = nullptr) {
   if (a.ta != TA || a.tb != TB) return hipErrorInvalidValue;
   a.pend = net.pend;
   net.pend.n = 0;
   MMProbs<T> pr{};
   if (prp) pr = *prp;
   // a batched launch: one plane per problem, plus one for the pending updates
-  dim3 grid((a.M + 31) / 32, (a.N + 31) / 32, pr.n > 0 ? pr.n + (a.pend.n > 0 ? 1 : 0) : 1), blk(MM_NT);
+  dim3 grid((a.M + 31) / 32, (a.N + 31) / 32, (pr.n > 0 ? pr.n : 1) + (a.pend.n > 0 ? 1 : 0)), blk(MM_NT);
   if (EPI == MM_L3CE) grid.y = (unsigned)std::max(1, std::min(8, a.n_mid / 32));   // n_mid column slices
   const bool h1ok = AOP != OP_H1 || net.vec_masks;
   const bool kvec = a.K % (int)(16 / sizeof(T)) == 0;       // vectors never straddle the K end
@@ -1134,19 +1166,17 @@ hipError_t mm(MlpNet<T>& net, MMArgs<T>& a, const MMProbs<T>* prp = nullptr, boo
   hipStream_t st = net.st;
   auto go = [&](auto mkc) {
     constexpr int MK = decltype(mkc)::value;
-    if constexpr (EPI == MM_L23) {
-      if (w6) {
-        if (av && bv) hipLaunchKernelGGL((k_mm6<T, EPI, AOP, BOP, TA, TB, !TA, TB, MK>), grid, blk, 0, st, a, pr);
-        else if (av) hipLaunchKernelGGL((k_mm6<T, EPI, AOP, BOP, TA, TB, !TA, 0, MK>), grid, blk, 0, st, a, pr);
-        else if (bv) hipLaunchKernelGGL((k_mm6<T, EPI, AOP, BOP, TA, TB, 0, TB, MK>), grid, blk, 0, st, a, pr);
-        else hipLaunchKernelGGL((k_mm6<T, EPI, AOP, BOP, TA, TB, 0, 0, MK>), grid, blk, 0, st, a, pr);
-        return;
-      }
+    if (pr.n > 0) {
+      if (av && bv) hipLaunchKernelGGL((k_mmb<T, EPI, AOP, BOP, TA, TB, !TA, TB, MK>), grid, blk, 0, st, a, pr);
+      else if (av) hipLaunchKernelGGL((k_mmb<T, EPI, AOP, BOP, TA, TB, !TA, 0, MK>), grid, blk, 0, st, a, pr);
+      else if (bv) hipLaunchKernelGGL((k_mmb<T, EPI, AOP, BOP, TA, TB, 0, TB, MK>), grid, blk, 0, st, a, pr);
+      else hipLaunchKernelGGL((k_mmb<T, EPI, AOP, BOP, TA, TB, 0, 0, MK>), grid, blk, 0, st, a, pr);
+      return;
     }
-    if (av && bv) hipLaunchKernelGGL((k_mm<T, EPI, AOP, BOP, TA, TB, !TA, TB, MK>), grid, blk, 0, st, a, pr);
-    else if (av) hipLaunchKernelGGL((k_mm<T, EPI, AOP, BOP, TA, TB, !TA, 0, MK>), grid, blk, 0, st, a, pr);
-    else if (bv) hipLaunchKernelGGL((k_mm<T, EPI, AOP, BOP, TA, TB, 0, TB, MK>), grid, blk, 0, st, a, pr);
-    else hipLaunchKernelGGL((k_mm<T, EPI, AOP, BOP, TA, TB, 0, 0, MK>), grid, blk, 0, st, a, pr);
+    if (av && bv) hipLaunchKernelGGL((k_mm<T, EPI, AOP, BOP, TA, TB, !TA, TB, MK>), grid, blk, 0, st, a);
+    else if (av) hipLaunchKernelGGL((k_mm<T, EPI, AOP, BOP, TA, TB, !TA, 0, MK>), grid, blk, 0, st, a);
+    else if (bv) hipLaunchKernelGGL((k_mm<T, EPI, AOP, BOP, TA, TB, 0, TB, MK>), grid, blk, 0, st, a);
+    else hipLaunchKernelGGL((k_mm<T, EPI, AOP, BOP, TA, TB, 0, 0, MK>), grid, blk, 0, st, a);
   };
   constexpr bool masked = AOP == OP_H1 || BOP == OP_H1 || EPI == MM_L2 || EPI == MM_L3CE || EPI == MM_GA1 ||
                           EPI == MM_L23;
@@ -1303,18 +1333,19 @@ template <typename T> struct SubStep {
   int v;
 };
 
-// The fused forwards (MM_L23) of np sub-steps in one launch at net's xw (valid): problem p uses arena
-// region p and writes into its own scratch; net's pending updates run in it.
-template <typename T>
-hipError_t mlp_forward_batch(MlpNet<T>& net, const SubStep<T>* ss, int np, bool w6 = false) {
+// Batched-launch argument builders: the shared MMArgs (problem 0's operands) and the problem table.
+// Fused forwards (MM_L23) at net's xw (or the sub-step's own): problem p uses arena region p0 + p and
+// writes into its own scratch.
+template <typename T, typename PR>
+void l23_build(MlpNet<T>& net, const SubStep<T>* const* ss, int np, int p0, MMArgs<T>& a, PR& pr) {
   const int nm = net.n_mid;
-  MMArgs<T> a{};
-  MMProbs<T> pr{};
+  a = MMArgs<T>{};
   pr.n = np;
   for (int p = 0; p < np; ++p) {
-    const SubStep<T>& s = ss[p];
+    const SubStep<T>& s = *ss[p];
     const MlpNet<T>& sc = *s.scr;
     MMProb<T>& q = pr.p[p];
+    q = MMProb<T>{};
     q.A = s.xw ? s.xw : net.xw; q.B = s.q[2]; q.C = nullptr;
     q.b1 = s.q[1]; q.bias = s.q[3]; q.W3 = s.q[4]; q.bias3 = s.q[5];
     q.ms = s.ms;
@@ -1323,7 +1354,7 @@ hipError_t mlp_forward_batch(MlpNet<T>& net, const SubStep<T>* ss, int np, bool 
     q.pb3 = s.w.pb3 ? sc.pb3 : nullptr;
     q.pw3 = s.w.pw3 ? sc.pw3 : nullptr;
     q.gz = sc.gz; q.lpart = s.lpart; q.colpart = nullptr;
-    q.gx = net.gx + (size_t)p * net.gx_bytes;
+    q.gx = net.gx + (size_t)(p0 + p) * net.gx_bytes;
   }
   const MMProb<T>& q0 = pr.p[0];
   mm_set<T>(a, net.B, nm, nm, q0.A, nm, 0, q0.B, nm, 1, nullptr, nm);
@@ -1334,20 +1365,19 @@ hipError_t mlp_forward_batch(MlpNet<T>& net, const SubStep<T>* ss, int np, bool 
   a.gx = q0.gx; a.gx_bytes = net.gx_bytes; a.ep = gx_next_epoch(net.ctx); a.abort_flag = net.abort_flag;
   a.force_abort = net.l23_count == net.force_abort;
   ++net.l23_count;
-  return mm<T, MM_L23, 0, 1, OP_H1>(net, a, &pr, w6);
 }
 
-// The layer-1 backwards (MM_GA1: ga1 = (ga2·W2)·gate, + b1 partials where wanted) of np sub-steps
-// in one launch, each from its own ga2 into its own ga1.
-template <typename T>
-hipError_t mlp_ga1_batch(MlpNet<T>& net, const SubStep<T>* const* ss, int np) {
+// Layer-1 backwards (MM_GA1: ga1 = (ga2·W2)·gate, + b1 partials for the b1 sub-step), each from its
+// own ga2 into its own ga1.
+template <typename T, typename PR>
+void ga1_build(MlpNet<T>& net, const SubStep<T>* const* ss, int np, MMArgs<T>& a, PR& pr) {
   const int nm = net.n_mid;
-  MMArgs<T> a{};
-  MMProbs<T> pr{};
+  a = MMArgs<T>{};
   pr.n = np;
   for (int p = 0; p < np; ++p) {
     const SubStep<T>& s = *ss[p];
     MMProb<T>& q = pr.p[p];
+    q = MMProb<T>{};
     q.A = s.scr->ga2; q.B = s.q[2]; q.C = s.scr->ga1;
     q.b1 = s.q[1]; q.ms = s.ms;
     q.colpart = s.v == 1 ? s.scr->pb1 : nullptr;
@@ -1355,37 +1385,54 @@ hipError_t mlp_ga1_batch(MlpNet<T>& net, const SubStep<T>* const* ss, int np) {
   const MMProb<T>& q0 = pr.p[0];
   mm_set<T>(a, net.B, nm, nm, q0.A, nm, 0, q0.B, nm, 0, q0.C, nm);
   a.ms = q0.ms; a.H = net.xw; a.b1 = q0.b1; a.H1 = nullptr; a.colpart = q0.colpart;
-  return mm<T, MM_GA1, 0, 0>(net, a, &pr);
 }
 
-// The layer-1 backwards of np sub-steps (as mlp_ga1_batch) and the W2 gradient of sub-step net `w2n`
-// (ga2ᵀ·h1 with the SGHMC epilogue, as mlp_wgrad v = 2) in ONE launch (k_mm2): neither reads what the
-// other writes.  net's pending updates run in the first grid's extra plane.
+// Weight gradient of W1 (v = 0: ga1ᵀ·X) or W2 (v = 2: ga2ᵀ·h1) of sub-step net `sn` with the SGHMC
+// epilogue, as mlp_wgrad.
+template <typename T>
+void wgrad_build(MlpNet<T>& sn, const SubStep<T>& s, int v, const Upd<T>& u, MMArgs<T>& a) {
+  const int B = sn.B, nm = sn.n_mid;
+  a = MMArgs<T>{};
+  a.upd_mode = UPD_SGHMC; a.u = u;
+  if (v == 2) {
+    mm_set<T>(a, nm, nm, B, sn.ga2, nm, 1, sn.xw, nm, 0, nullptr, nm);
+    a.ms = s.ms; a.b1 = s.q[1];
+  } else {
+    mm_set<T>(a, nm, sn.n_in, B, sn.ga1, nm, 1, sn.X, sn.n_in, 0, nullptr, sn.n_in);
+  }
+}
+
+template <typename T>
+hipError_t mlp_forward_batch(MlpNet<T>& net, const SubStep<T>* ss, int np) {
+  const SubStep<T>* sp[MAXPROB];
+  for (int p = 0; p < np; ++p) sp[p] = ss + p;
+  MMArgs<T> a;
+  MMProbs<T> pr{};
+  l23_build(net, sp, np, 0, a, pr);
+  return mm<T, MM_L23, 0, 1, OP_H1>(net, a, &pr);
+}
+
+// mask kind of a launch (one per launch: every sub-grid reads the same kind)
+template <typename T> inline int mask_kind(const MaskSrc<T>& ms) {
+  return ms.slot ? MK_PHILOX : ms.keep ? MK_KEEP : ms.vals ? MK_VALS : MK_NONE;
+}
+
+// The layer-1 backwards of np sub-steps and the W2 gradient of sub-step net `w2n` in ONE launch
+// (k_mm2): neither reads what the other writes.  net's pending updates run in the first grid's extra
+// plane.
 template <typename T>
 hipError_t mlp_ga1_w2(MlpNet<T>& net, const SubStep<T>* const* ss, int np, MlpNet<T>& w2n, const SubStep<T>& s2,
                       const Upd<T>& u2) {
   const int nm = net.n_mid;
-  MMArgs<T> a1{}, a2{};
-  MMProbs<T> pr{};
-  pr.n = np;
-  for (int p = 0; p < np; ++p) {
-    const SubStep<T>& s = *ss[p];
-    MMProb<T>& q = pr.p[p];
-    q.A = s.scr->ga2; q.B = s.q[2]; q.C = s.scr->ga1;
-    q.b1 = s.q[1]; q.ms = s.ms;
-    q.colpart = s.v == 1 ? s.scr->pb1 : nullptr;
-  }
-  const MMProb<T>& q0 = pr.p[0];
-  mm_set<T>(a1, net.B, nm, nm, q0.A, nm, 0, q0.B, nm, 0, q0.C, nm);
-  a1.ms = q0.ms; a1.H = net.xw; a1.b1 = q0.b1; a1.H1 = nullptr; a1.colpart = q0.colpart;
+  MMArgs<T> a1, a2;
+  MMProbs3<T> pr{};
+  ga1_build(net, ss, np, a1, pr);
   a1.pend = net.pend;
   net.pend.n = 0;
-  mm_set<T>(a2, nm, nm, net.B, w2n.ga2, nm, 1, net.xw, nm, 0, nullptr, nm);   // ga2ᵀ·h1
-  a2.ms = s2.ms; a2.b1 = s2.q[1]; a2.upd_mode = UPD_SGHMC; a2.u = u2;
+  wgrad_build(w2n, s2, 2, u2, a2);
   a2.pend = w2n.pend;
   w2n.pend.n = 0;
-  if (((a1.ms.slot != 0) != (a2.ms.slot != 0)) || ((a1.ms.keep != nullptr) != (a2.ms.keep != nullptr)))
-    return hipErrorInvalidValue;                               // one mask kind per launch
+  if (mask_kind(a1.ms) != mask_kind(a2.ms)) return hipErrorInvalidValue;
   const int3 g1 = make_int3((a1.M + 31) / 32, (a1.N + 31) / 32, np + (a1.pend.n > 0 ? 1 : 0));
   const int2 g2 = make_int2((a2.M + 31) / 32, (a2.N + 31) / 32);
   const dim3 grid((unsigned)std::max(g1.x, g2.x), (unsigned)std::max(g1.y, g2.y), (unsigned)(g1.z + 1));
@@ -1401,11 +1448,81 @@ hipError_t mlp_ga1_w2(MlpNet<T>& net, const SubStep<T>* const* ss, int np, MlpNe
     if (aal) go(mkc, std::integral_constant<int, 1>{});
     else go(mkc, std::integral_constant<int, 0>{});
   };
-  if (a1.ms.slot) go_mk(std::integral_constant<int, MK_PHILOX>{});
-  else if (a1.ms.keep) go_mk(std::integral_constant<int, MK_KEEP>{});
-  else if (a1.ms.vals) go_mk(std::integral_constant<int, MK_VALS>{});
-  else go_mk(std::integral_constant<int, MK_NONE>{});
+  switch (mask_kind(a1.ms)) {
+    case MK_PHILOX: go_mk(std::integral_constant<int, MK_PHILOX>{}); break;
+    case MK_KEEP: go_mk(std::integral_constant<int, MK_KEEP>{}); break;
+    case MK_VALS: go_mk(std::integral_constant<int, MK_VALS>{}); break;
+    default: go_mk(std::integral_constant<int, MK_NONE>{}); break;
+  }
   return hipGetLastError();
+}
+
+// Four launches per iteration (fit ≥ 4 fused grids co-resident, keep-flag or buffer masks, aligned
+// operands): the fused forwards of 4 sub-steps (those of W1, b1, W2 and one more), then ONE launch of
+// the other 2 fused forwards beside the layer-1 backwards of W1 / b1 (k_mm2b), then ONE launch of the
+// W1 and W2 gradients (k_mm2, the pending bias / W3 updates in its extra plane), then layer 1.
+template <typename T>
+bool quad_ok(const MlpNet<T>& net, const SubStep<T>* ss) {
+  if (sizeof(T) != 4) return false;                            // float64: two fused grids fit, not four
+  const int mk = mask_kind(ss[0].ms);
+  if (mk != MK_KEEP && mk != MK_VALS) return false;
+  if (net.l23_fit < 4 || net.n_mid % (int)(16 / sizeof(T)) || net.n_in % (int)(16 / sizeof(T))) return false;
+  if (!net.vec_masks || !vec_ok(net.xw, net.n_mid, sizeof(T))) return false;
+  for (int i = 0; i < 6; ++i)
+    if (!vec_ok(ss[i].q[2], net.n_mid, sizeof(T)) || !vec_ok(ss[i].scr->ga2, net.n_mid, sizeof(T))) return false;
+  return true;
+}
+
+template <typename T>
+hipError_t mlp_l23_ga1(MlpNet<T>& net, const SubStep<T>* const* fw, int nf, const SubStep<T>* const* ga, int nga) {
+  MMArgs<T> a1, a2;
+  MMProbs3<T> p1{}, p2{};
+  l23_build(net, fw, nf, 0, a1, p1);
+  ga1_build(net, ga, nga, a2, p2);
+  a1.pend.n = 0;
+  a2.pend.n = 0;
+  const int3 g1 = make_int3((a1.M + 31) / 32, (a1.N + 31) / 32, nf);
+  const int3 g2 = make_int3((a2.M + 31) / 32, (a2.N + 31) / 32, nga);
+  const dim3 grid((unsigned)std::max(g1.x, g2.x), (unsigned)std::max(g1.y, g2.y), (unsigned)(g1.z + g2.z));
+  hipStream_t st = net.st;
+  if constexpr (sizeof(T) == 4) {                              // float32 only (quad_ok)
+    auto go = [&](auto mkc) {
+      constexpr int MK = decltype(mkc)::value;
+      hipLaunchKernelGGL((k_mm2b<T, MM_L23, OP_H1, OP_PLAIN, 0, 1, 1, 1, MM_GA1, OP_PLAIN, OP_PLAIN, 0, 0, 1, 0, MK>),
+                         grid, dim3(MM_NT), 0, st, a1, p1, a2, p2, g1, g2);
+    };
+    if (mask_kind(a1.ms) == MK_KEEP) go(std::integral_constant<int, MK_KEEP>{});
+    else go(std::integral_constant<int, MK_VALS>{});
+    return hipGetLastError();
+  }
+  return hipErrorInvalidValue;
+}
+
+template <typename T>
+hipError_t mlp_w1_w2(MlpNet<T>& net, MlpNet<T>& w1n, const SubStep<T>& s1, const Upd<T>& u1, MlpNet<T>& w2n,
+                     const SubStep<T>& s2, const Upd<T>& u2) {
+  MMArgs<T> a1, a2;
+  MMProbs3<T> p1{};
+  wgrad_build(w1n, s1, 0, u1, a1);
+  wgrad_build(w2n, s2, 2, u2, a2);
+  a1.pend = net.pend;
+  net.pend.n = 0;
+  a2.pend.n = 0;
+  const int3 g1 = make_int3((a1.M + 31) / 32, (a1.N + 31) / 32, 1 + (a1.pend.n > 0 ? 1 : 0));
+  const int2 g2 = make_int2((a2.M + 31) / 32, (a2.N + 31) / 32);
+  const dim3 grid((unsigned)std::max(g1.x, g2.x), (unsigned)std::max(g1.y, g2.y), (unsigned)(g1.z + 1));
+  hipStream_t st = net.st;
+  if constexpr (sizeof(T) == 4) {                              // float32 only (quad_ok)
+    auto go = [&](auto mkc) {
+      constexpr int MK = decltype(mkc)::value;   // the W1 gradient reads no masks: any kind is its plain code
+      hipLaunchKernelGGL((k_mm2<T, MM_UPD, OP_PLAIN, OP_PLAIN, 1, 0, 0, 0, MM_UPD, OP_PLAIN, OP_H1, 1, 0, 0, 0, MK>),
+                         grid, dim3(MM_NT), 0, st, a1, p1, a2, g1, g2);
+    };
+    if (mask_kind(a2.ms) == MK_KEEP) go(std::integral_constant<int, MK_KEEP>{});
+    else go(std::integral_constant<int, MK_VALS>{});
+    return hipGetLastError();
+  }
+  return hipErrorInvalidValue;
 }
 
 // Queue the update of variable v from the partials of `src` (default: net's own) on net's next launch.
@@ -1449,11 +1566,19 @@ int net_fuse(hmcx_ctx* ctx, MlpNet<T>& net, int regions = 1) {
   const size_t need = (size_t)net.nlb * S * 32 * net.n_out * 16;
   if (need > 0x7fffffff) return HMCX_OK;
   if (int rc = gx_reserve(ctx, need * regions)) return rc;
-  net.l23_fit = std::min(regions, (int)((long)per_cu * ctx->num_cus / ((long)net.nlb * S)));
-  const void* kfn6 = (const void*)k_mm6<T, MM_L23, OP_H1, OP_PLAIN, 0, 1, 1, 1, MK_KEEP>;
-  int per_cu6 = 0;
-  HMCX_HIP(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu6, kfn6, MM_NT, 0));
-  net.l23_fit6 = std::min(regions, (int)((long)per_cu6 * ctx->num_cus / ((long)net.nlb * S)));
+  // batched fused launches: the fewest workgroups per CU of the batched variants that can run
+  int per_b = per_cu;
+  for (const void* f : {(const void*)k_mmb<T, MM_L23, OP_H1, OP_PLAIN, 0, 1, 1, 1, MK_KEEP>,
+                        (const void*)k_mmb<T, MM_L23, OP_H1, OP_PLAIN, 0, 1, 0, 0, MK_KEEP>,
+                        (const void*)k_mmb<T, MM_L23, OP_H1, OP_PLAIN, 0, 1, 1, 1, MK_VALS>,
+                        (const void*)k_mmb<T, MM_L23, OP_H1, OP_PLAIN, 0, 1, 0, 0, MK_VALS>,
+                        (const void*)k_mmb<T, MM_L23, OP_H1, OP_PLAIN, 0, 1, 1, 1, MK_PHILOX>,
+                        (const void*)k_mmb<T, MM_L23, OP_H1, OP_PLAIN, 0, 1, 0, 0, MK_PHILOX>}) {
+    int pc = 0;
+    if (int rc = kernel_occupancy(ctx, f, MM_NT, 0, &pc)) return rc;
+    per_b = std::min(per_b, pc);
+  }
+  net.l23_fit = std::min(regions, (int)((long)per_b * ctx->num_cus / ((long)net.nlb * S)));
   if (!ctx->mlp_abort_dev) {
     HMCX_HIP(ctx, hipMalloc((void**)&ctx->mlp_abort_dev, sizeof(int)));
     HMCX_HIP(ctx, hipMemsetAsync(ctx->mlp_abort_dev, 0, sizeof(int), ctx->stream));
@@ -1659,10 +1784,7 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
     const int n = s->n_iter[si], F = 6 * n + 2;
     const uint32_t step_id = s->step_base + (uint32_t)si;
     const double* nz = s->noise_mode == HMCX_NOISE_BUFFER ? s->noise + s->noise_off[si] : nullptr;
-    if (philox_masks && keep_arr) {
-      hipLaunchKernelGGL(k_mlp_keep, dim3((unsigned)(((n3 + 3) / 4 + 255) / 256), (unsigned)F), dim3(256), 0, st, keep,
-                         n3, s->seed, s->chain, step_id);
-    }
+    const bool fused_start = philox_masks && keep_arr;       // keep flags in the momentum launch
     auto masks_for = [&](int f) -> MaskSrc<T> {
       // PHILOX: the kernels draw the flags they read (MK_PHILOX, slot MASK_SLOT0 + f); with
       // HMCX_MLP_MASKS=keep, k_mlp_keep stores the same flags once per step and the kernels load them
@@ -1677,8 +1799,14 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
       const int v = s->order[i];
       vt.q[i] = par[v]; vt.qn[i] = qa[v]; vt.p[i] = pv[v]; vt.n[i] = dim[v]; vt.e0[i] = off_v[v];
     }
-    hipLaunchKernelGGL(k_mlp_init<T>, dim3(NPART, 6), dim3(256), 0, st, vt, (T)eps, n > 0 ? 1 : 0, s->noise_mode,
-                       nz, s->seed, s->chain, step_id, part_cur);
+    if (fused_start) {
+      const unsigned kb = (unsigned)(((n3 + 3) / 4 + 255) / 256);
+      hipLaunchKernelGGL(k_mlp_start<T>, dim3(std::max(kb, (unsigned)NPART), (unsigned)(6 + F)), dim3(256), 0, st, vt, (T)eps,
+                         n > 0 ? 1 : 0, s->noise_mode, nz, s->seed, s->chain, step_id, part_cur, keep, n3);
+    } else {
+      hipLaunchKernelGGL(k_mlp_init<T>, dim3(NPART, 6), dim3(256), 0, st, vt, (T)eps, n > 0 ? 1 : 0, s->noise_mode,
+                         nz, s->seed, s->chain, step_id, part_cur);
+    }
     T* cur[6];
     for (int v = 0; v < 6; ++v) cur[v] = par[v];
     int fwd = 0;
@@ -1698,9 +1826,10 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
       // it − 1 and write it + 1, so three sets never alias within an iteration (the pending updates of
       // the bias / W3 sub-steps then run beside readers of it − 1)
       T* const* q3[3] = {qa, qb, qc};
-      const char* w_env = getenv("HMCX_MLP_L23W");
-      const bool w6 = w_env && w_env[0] == '6' && net.l23_fit6 > net.l23_fit;
-      const int fit = std::min(MAXPROB, w6 ? net.l23_fit6 : net.l23_fit);
+      // as many fused forwards per launch as fit co-resident (f32 at config 3: 4 at two workgroups per
+      // CU; three per CU with the registers spilled measured slower: one 6-problem launch 47.8 µs vs
+      // 23.8 + 17.4 for 4 + 2)
+      const int fit = std::min(MAXPROB, net.l23_fit);
       for (int i = 0; i < 6; ++i) {
         pn[i].X = net.X; pn[i].y = net.y; pn[i].xw = net.xw; pn[i].vec_masks = net.vec_masks;
       }
@@ -1730,7 +1859,36 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
           x.v = v;
           if (v <= 1) ga[nga++] = &ss[i];
         }
-        for (int i0 = 0; i0 < 6; i0 += fit) HMCX_HIP(ctx, mlp_forward_batch<T>(net, ss + i0, std::min(fit, 6 - i0), w6));
+        int i2 = 0;                                              // position of the W2 sub-step
+        while (s->order[i2] != 2) ++i2;
+        if (quad_ok(net, ss)) {
+          // 4 launches: forwards of W1, b1, W2 (+ one more) | the other two forwards + the W1 / b1
+          // layer-1 backwards | the W1 and W2 gradients + every pending update | layer 1
+          const SubStep<T>* fa[6];
+          const SubStep<T>* fb[6];
+          int na = 0, nb = 0;
+          for (int i = 0; i < 6; ++i)
+            if (s->order[i] <= 2) fa[na++] = &ss[i];
+          for (int i = 0; i < 6; ++i)
+            if (s->order[i] > 2) {
+              if (na < 4) fa[na++] = &ss[i];
+              else fb[nb++] = &ss[i];
+            }
+          MMArgs<T> a;
+          MMProbs<T> pr{};
+          l23_build(net, fa, na, 0, a, pr);
+          HMCX_HIP(ctx, (mm<T, MM_L23, 0, 1, OP_H1>(net, a, &pr)));
+          HMCX_HIP(ctx, mlp_l23_ga1<T>(net, fb, nb, ga, nga));
+          for (int i = 0; i < 6; ++i) {
+            const int v = s->order[i];
+            if (v != 0 && v != 2) set_pending(net, v, UPD_SGHMC, upd_for(it, v, Xit[v], it + 1 < n ? Xnx[v] : nullptr), &pn[i]);
+          }
+          HMCX_HIP(ctx, mlp_w1_w2<T>(net, pn[0], ss[0], upd_for(it, 0, Xit[0], it + 1 < n ? Xnx[0] : nullptr), pn[i2],
+                                     ss[i2], upd_for(it, 2, Xit[2], it + 1 < n ? Xnx[2] : nullptr)));
+          fwd += 6;
+          continue;
+        }
+        for (int i0 = 0; i0 < 6; i0 += fit) HMCX_HIP(ctx, mlp_forward_batch<T>(net, ss + i0, std::min(fit, 6 - i0)));
         // bias / W3 updates from their partials: b2, W3, b3 (partials of the fused forwards) in the
         // layer-1 backward launch, b1 (whose partials that launch makes) in the W1 gradient launch
         for (int i = 0; i < 6; ++i) {
@@ -1738,8 +1896,6 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
           if (v == 0 || v == 2) continue;
           set_pending(v == 1 ? pn[0] : net, v, UPD_SGHMC, upd_for(it, v, Xit[v], it + 1 < n ? Xnx[v] : nullptr), &pn[i]);
         }
-        int i2 = 0;                                              // the W2 sub-step rides in the
-        while (s->order[i2] != 2) ++i2;                          // layer-1 backward launch
         HMCX_HIP(ctx, mlp_ga1_w2<T>(net, ga, nga, pn[i2], ss[i2], upd_for(it, 2, Xit[2], it + 1 < n ? Xnx[2] : nullptr)));
         HMCX_HIP(ctx, mlp_wgrad<T>(pn[0], ss[0].q, ss[0].ms, 0, UPD_SGHMC,
                                    upd_for(it, 0, Xit[0], it + 1 < n ? Xnx[0] : nullptr)));
@@ -1758,7 +1914,7 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
         x.w = L3Want{false, false, false, false, false};
         x.v = -1;
       }
-      for (int e0 = 0; e0 < 2; e0 += fit) HMCX_HIP(ctx, mlp_forward_batch<T>(net, es + e0, std::min(fit, 2 - e0), w6));
+      for (int e0 = 0; e0 < 2; e0 += fit) HMCX_HIP(ctx, mlp_forward_batch<T>(net, es + e0, std::min(fit, 2 - e0)));
       fwd += 2;
     }
     for (int it = 0; it < n && !batch; ++it) {

@@ -14,11 +14,10 @@ for rep in $(seq $N); do
   for dt in f32 f64; do
     echo "[$A $dt] $(HMCX_LIB=$A timeout -k 10 120 python tools/probe_mlp.py $dt 40 2>&1 | tail -1)"
     echo "[new $dt] $(timeout -k 10 120 python tools/probe_mlp.py $dt 40 2>&1 | tail -1)"
-    echo "[new w6 $dt] $(HMCX_MLP_L23W=6 timeout -k 10 120 python tools/probe_mlp.py $dt 40 2>&1 | tail -1)"
   done
 done
 cd /tmp && export TMPDIR=/tmp
-for v in 4 6; do
+for v in 4; do
   HMCX_MLP_L23W=$v timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_mlpb_$v -o run --output-format csv -- python3 $R/tools/probe_mlp.py 40 > $R/gpurun_out/probe_mlpb_prof.txt 2>&1 || { tail -5 $R/gpurun_out/probe_mlpb_prof.txt; exit 1; }
   echo "== L23W=$v"
   python3 -c "
