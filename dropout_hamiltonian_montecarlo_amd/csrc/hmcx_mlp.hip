@@ -50,7 +50,8 @@ constexpr int MM_NT = MM_NW * 64;
 // Dropout masks of one forward: m0, m1, m2 at offsets 0, mn, 2·mn.
 template <typename T> struct MaskSrc {
   const T* vals;          // explicit mask values (API / BUFFER mode), or
-  const uint8_t* keep;    // keep flags (k_mlp_keep): value = keep ? scale : 0;  neither: no dropout or MK_PHILOX
+  const uint32_t* keep;   // keep flags, one bit per element (bit e % 32 of word e / 32): value = keep ? scale : 0;
+                          // neither vals nor keep: no dropout or MK_PHILOX
   T scale;
   int mn;
   // MK_PHILOX: the keep flags are drawn where they are used — element e = which·mn + i is word e % 4
@@ -75,7 +76,7 @@ template <typename T> struct MRaw { T v; uint32_t k; };
 template <typename T, int MK> __device__ inline MRaw<T> mraw(const MaskSrc<T>& s, int which, size_t i) {
   MRaw<T> r{T(1), 1u};
   const size_t e = (size_t)which * s.mn + i;
-  if constexpr (MK == MK_KEEP) r.k = s.keep[e];
+  if constexpr (MK == MK_KEEP) r.k = (s.keep[e >> 5] >> (e & 31)) & 1u;
   if constexpr (MK == MK_VALS) r.v = s.vals[e];
   if constexpr (MK == MK_PHILOX) r.k = keep_flag(mask_words(s, e).v[e & 3]) ? 1u : 0u;
   return r;
@@ -106,12 +107,11 @@ template <typename T, int V, int MK> __device__ inline void mvals(const MaskSrc<
 #pragma unroll
     for (int q = 0; q < V; ++q) m[q] = v[q];
   } else if constexpr (MK == MK_KEEP) {
-    uint32_t k;
-    if constexpr (V == 4) k = *reinterpret_cast<const uint32_t*>(s.keep + e);
-    else k = *reinterpret_cast<const uint16_t*>(s.keep + e);
+    uint32_t k = s.keep[e >> 5];                                 // e % V == 0: V bits of one word
     asm volatile("" : "+v"(k));
+    k >>= (e & 31);
 #pragma unroll
-    for (int q = 0; q < V; ++q) m[q] = ((k >> (8 * q)) & 0xFF) ? s.scale : T(0);
+    for (int q = 0; q < V; ++q) m[q] = ((k >> q) & 1u) ? s.scale : T(0);
   } else if constexpr (MK == MK_PHILOX) {                        // e % V == 0: one Philox block
     const u32x4 w = mask_words(s, e);
 #pragma unroll
@@ -180,11 +180,24 @@ template <typename T> struct PendSet {
   Pending<T> p[MAXPEND];
   int n;
 };
+// With at least one workgroup per update, update j gets its own share of the workgroups (they run side
+// by side: each is a short chain of partial loads, a Philox draw and stores); otherwise every
+// workgroup runs them in turn.
 template <typename T>
 __device__ inline void run_pendset(const PendSet<T>& ps, int bid, int nb) {
+  if (ps.n == 0) return;
+  const bool split = nb >= ps.n;
+  const int per = split ? nb / ps.n : nb;
 #pragma unroll
   for (int j = 0; j < MAXPEND; ++j)
-    if (j < ps.n) run_pending(ps.p[j], bid, nb);
+    if (j < ps.n) {
+      if (!split) {
+        run_pending(ps.p[j], bid, nb);
+      } else {
+        const int lo = j * per, hi = j == ps.n - 1 ? nb : lo + per;
+        if (bid >= lo && bid < hi) run_pending(ps.p[j], bid - lo, hi - lo);
+      }
+    }
 }
 template <typename T>
 __global__ __launch_bounds__(256) void k_pending(PendSet<T> ps) {
@@ -909,22 +922,22 @@ __global__ __launch_bounds__(MM_NT) void k_l3_wide(MMArgs<T> a, const T* z) {
   l3_backward<T, MK>(a, zt, zs, m0, blockIdx.x, scr, MM_NT, 0, a.n_mid, true);
 }
 
-// Keep flags of forward f (Philox slot MASK_SLOT0 + f, 3·mn per forward), four per thread g.
-__device__ inline void keep_flags(uint8_t* keep, int n3, uint64_t seed, uint32_t chain, uint32_t step, int g, int f) {
-  if (4 * g >= n3) return;
+// Keep flags of forward f, one bit per element (bit e % 32 of word e / 32; forward f's words start at
+// f·⌈n3/32⌉).  Thread g draws Philox block g (flags 4g … 4g + 3, flag e = keep_flag(word e % 4)); eight
+// neighbouring lanes OR their nibbles into one word, which the first of them stores.
+__device__ inline void keep_flags(uint32_t* keep, int n3, uint64_t seed, uint32_t chain, uint32_t step, int g, int f) {
+  const int W = (n3 + 31) / 32;
   u32x4 c = {{(uint32_t)g, MASK_SLOT0 + (uint32_t)f, step, chain}};
   const u32x4 r = philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
-  uint8_t* out = keep + (size_t)f * n3;
-  if ((n3 & 3) == 0) {                                         // the four flags in one 4-byte store
-    uint32_t w = 0;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) w |= (keep_flag(r.v[q]) ? 1u : 0u) << (8 * q);
-    *reinterpret_cast<uint32_t*>(out + 4 * g) = w;
-    return;
-  }
+  uint32_t w = 0;
 #pragma unroll
   for (int q = 0; q < 4; ++q)
-    if (4 * g + q < n3) out[4 * g + q] = keep_flag(r.v[q]) ? 1 : 0;
+    if (4 * g + q < n3 && keep_flag(r.v[q])) w |= 1u << q;
+  w <<= 4 * (g & 7);
+  w |= __shfl_xor(w, 1, 8);                                   // every lane of the group takes part
+  w |= __shfl_xor(w, 2, 8);
+  w |= __shfl_xor(w, 4, 8);
+  if ((g & 7) == 0 && (g >> 3) < W) keep[(size_t)f * W + (g >> 3)] = w;
 }
 
 // Mask values of one forward (the API twin of k_mlp_keep: same counters, value = keep·(1/0.9)).
@@ -949,6 +962,7 @@ __global__ void k_bias_into_z(T* z, const T* b, int n, int N) {
 // Six variables in the caller's order (position i of `order`).
 struct VarTab {
   void* q[6]; void* qn[6]; void* p[6];
+  void* qc[6];                 // step start: the previous step's proposal, committed here if accepted
   int n[6], e0[6];
 };
 
@@ -971,11 +985,16 @@ __device__ inline void block_sum2(double a, double b, double* out_a, double* out
 __device__ inline int var_blocks(int n) { return min(NPART, max(1, (n + 1023) / 1024)); }
 
 // Momentum draw (hmc.py:82-87) + first drift q' = q + ε·p + partials of Σp², Σq² (part [2][6][NPART]).
+// With prev_acc set, the previous step's commit happens here first (state ← proposal where it was
+// accepted, hmc.py:75-79): one launch less per step.
 template <typename T>
 __device__ inline void init_block(const VarTab& vt, T eps, int drift, int noise_mode, const double* noise,
-                                  uint64_t seed, uint32_t chain, uint32_t step, double* part, int v, int bx) {
+                                  uint64_t seed, uint32_t chain, uint32_t step, double* part, int v, int bx,
+                                  const int32_t* prev_acc) {
   const int n = vt.n[v];
-  const T* q = (const T*)vt.q[v];
+  T* const qw = (T*)vt.q[v];
+  const bool take = prev_acc != nullptr && vt.qc[v] != nullptr && *prev_acc != 0;   // uniform
+  const T* q = take ? (const T*)vt.qc[v] : qw;
   T* qn = (T*)vt.qn[v];
   T* p = (T*)vt.p[v];
   const int nb = var_blocks(n);
@@ -988,6 +1007,7 @@ __device__ inline void init_block(const VarTab& vt, T eps, int drift, int noise_
     const uint32_t e = (uint32_t)(vt.e0[v] + i);
     const T z = noise_mode == HMCX_NOISE_BUFFER ? (T)noise[e] : philox_normal_t<T>(seed, chain, step, 0u, e);
     const T qv = q[i];
+    if (take) qw[i] = qv;
     p[i] = z;
     if (drift) qn[i] = qv + eps * z;
     sp += (double)z * (double)z;
@@ -997,18 +1017,20 @@ __device__ inline void init_block(const VarTab& vt, T eps, int drift, int noise_
 }
 template <typename T>
 __global__ __launch_bounds__(256) void k_mlp_init(VarTab vt, T eps, int drift, int noise_mode, const double* noise,
-                                                  uint64_t seed, uint32_t chain, uint32_t step, double* part) {
-  init_block<T>(vt, eps, drift, noise_mode, noise, seed, chain, step, part, (int)blockIdx.y, (int)blockIdx.x);
+                                                  uint64_t seed, uint32_t chain, uint32_t step, double* part,
+                                                  const int32_t* prev_acc) {
+  init_block<T>(vt, eps, drift, noise_mode, noise, seed, chain, step, part, (int)blockIdx.y, (int)blockIdx.x, prev_acc);
 }
 // Step start in one launch: rows y < 6 draw the momentum of variable y and the first drift (k_mlp_init),
 // rows y ≥ 6 the keep flags of forward y − 6 (k_mlp_keep) — independent work, one launch less per step.
 template <typename T>
 __global__ __launch_bounds__(256) void k_mlp_start(VarTab vt, T eps, int drift, int noise_mode, const double* noise,
                                                    uint64_t seed, uint32_t chain, uint32_t step, double* part,
-                                                   uint8_t* keep, int n3) {
+                                                   const int32_t* prev_acc, uint32_t* keep, int n3) {
   if (blockIdx.y < 6) {
     if (blockIdx.x < NPART)
-      init_block<T>(vt, eps, drift, noise_mode, noise, seed, chain, step, part, (int)blockIdx.y, (int)blockIdx.x);
+      init_block<T>(vt, eps, drift, noise_mode, noise, seed, chain, step, part, (int)blockIdx.y, (int)blockIdx.x,
+                    prev_acc);
   } else {
     keep_flags(keep, n3, seed, chain, step, (int)(blockIdx.x * blockDim.x + threadIdx.x), (int)blockIdx.y - 6);
   }
@@ -1726,6 +1748,7 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
   const bool batch_off = batch_env && batch_env[0] == '0';
   const bool batch = !batch_off && net.fuse && s->order[0] == 0 && !store_h1 && net.l23_fit >= 1;
   MlpNet<T> pn[6]{};
+  MlpNet<T> en[2]{};                                           // scratch (gz) of the E_new / E_current forwards
   if (philox_masks) {
     if (n3 % 4) net.vec_masks = false;
   } else {
@@ -1736,7 +1759,8 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
   Workspace ws(ctx);
   T *pv[6], *qa[6], *qb[6], *qc[6], *xw_par = nullptr;
   double *part_cur, *part_new, *lp_cur, *lp_new, *lp_scr;
-  uint8_t* keep = nullptr;
+  uint32_t* keep = nullptr;                                  // keep flags of the step: one bit per element
+  const int kw = (n3 + 31) / 32;                              // words per forward
   int32_t* accf;
   static const char* prof_path = getenv("HMCX_MLP_PROF");
   const int prof_cap = prof_path && net.fuse ? 8192 : 0;
@@ -1755,13 +1779,16 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
       pv[v] = ws.take<T>(dim[v]); qa[v] = ws.take<T>(dim[v]); qb[v] = ws.take<T>(dim[v]);
       qc[v] = batch ? ws.take<T>(dim[v]) : nullptr;
     }
-    if (batch) xw_par = ws.take<T>((size_t)mn);
+    if (batch) {
+      xw_par = ws.take<T>((size_t)mn);
+      for (auto& e : en) e.gz = ws.take<T>((size_t)s->B * s->n_out);
+    }
     part_cur = ws.take<double>(12 * NPART);
     part_new = ws.take<double>(12 * NPART);
     lp_cur = ws.take<double>(net.nlb);
     lp_new = ws.take<double>(net.nlb);
     lp_scr = ws.take<double>(net.nlb);
-    if (keep_arr) keep = ws.take<uint8_t>((size_t)maxF * n3);
+    if (keep_arr) keep = ws.take<uint32_t>((size_t)maxF * kw);
     accf = ws.take<int32_t>(1);
   } while (ws.retry());
   if (ws.failed) return HMCX_ENOMEM;
@@ -1775,6 +1802,8 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
   for (int v = 0; v < 6; ++v) par[v] = (T*)s->par.p[v];
   const T* Xall = (const T*)s->X;
   const T scale = (T)(1.0 / 0.9);
+  bool commit_pending = false;                                // the previous step's proposal awaits its commit
+  T* prev_prop[6] = {};
 
   for (int si = 0; si < s->n_steps; ++si) {
     net.X = Xall + (size_t)s->row0[si] * s->n_in;
@@ -1790,7 +1819,7 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
       // HMCX_MLP_MASKS=keep, k_mlp_keep stores the same flags once per step and the kernels load them
       if (philox_masks && !keep_arr)
         return MaskSrc<T>{nullptr, nullptr, scale, mn, s->seed, s->chain, step_id, MASK_SLOT0 + (uint32_t)f};
-      if (philox_masks) return MaskSrc<T>{nullptr, keep + (size_t)f * n3, scale, mn, 0, 0, 0, 0};
+      if (philox_masks) return MaskSrc<T>{nullptr, keep + (size_t)f * kw, scale, mn, 0, 0, 0, 0};
       return MaskSrc<T>{(const T*)s->masks + s->mask_off[si] + (size_t)f * n3, nullptr, scale, mn, 0, 0, 0, 0};
     };
     // momentum (hmc.py:82-87), first drift into qa, Σp², Σθ² of the current state
@@ -1798,14 +1827,17 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
     for (int i = 0; i < 6; ++i) {
       const int v = s->order[i];
       vt.q[i] = par[v]; vt.qn[i] = qa[v]; vt.p[i] = pv[v]; vt.n[i] = dim[v]; vt.e0[i] = off_v[v];
+      vt.qc[i] = commit_pending ? prev_prop[v] : nullptr;
     }
+    const int32_t* prev_acc = commit_pending ? accf : nullptr;   // the previous step's commit, folded in
+    commit_pending = false;
     if (fused_start) {
-      const unsigned kb = (unsigned)(((n3 + 3) / 4 + 255) / 256);
+      const unsigned kb = (unsigned)((8 * kw + 255) / 256);
       hipLaunchKernelGGL(k_mlp_start<T>, dim3(std::max(kb, (unsigned)NPART), (unsigned)(6 + F)), dim3(256), 0, st, vt, (T)eps,
-                         n > 0 ? 1 : 0, s->noise_mode, nz, s->seed, s->chain, step_id, part_cur, keep, n3);
+                         n > 0 ? 1 : 0, s->noise_mode, nz, s->seed, s->chain, step_id, part_cur, prev_acc, keep, n3);
     } else {
       hipLaunchKernelGGL(k_mlp_init<T>, dim3(NPART, 6), dim3(256), 0, st, vt, (T)eps, n > 0 ? 1 : 0, s->noise_mode,
-                         nz, s->seed, s->chain, step_id, part_cur);
+                         nz, s->seed, s->chain, step_id, part_cur, prev_acc);
     }
     T* cur[6];
     for (int v = 0; v < 6; ++v) cur[v] = par[v];
@@ -1832,6 +1864,22 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
       const int fit = std::min(MAXPROB, net.l23_fit);
       for (int i = 0; i < 6; ++i) {
         pn[i].X = net.X; pn[i].y = net.y; pn[i].xw = net.xw; pn[i].vec_masks = net.vec_masks;
+      }
+      // energies (hmc.py:67-71): E_new at the last iteration's positions with forward 6n's masks,
+      // E_current at the start state with forward 6n + 1's.  Both only need what is known when the
+      // last (first) iteration starts, so they ride in its second launch when there is room
+      SubStep<T> es[2];
+      bool e_done[2] = {false, false};
+      T* const* Xlast = q3[(n - 1) % 3];
+      for (int e = 0; e < 2; ++e) {
+        SubStep<T>& x = es[e];
+        x.xw = e == 0 ? net.xw : xw_par;
+        for (int v = 0; v < 6; ++v) x.q[v] = e == 0 ? Xlast[v] : par[v];
+        x.ms = masks_for(6 * n + e);
+        x.scr = &en[e];
+        x.lpart = e == 0 ? lp_new : lp_cur;
+        x.w = L3Want{false, false, false, false, false};
+        x.v = -1;
       }
       for (int it = 0; it < n; ++it) {
         T* const* Xit = q3[it % 3];                              // positions of iteration it
@@ -1874,6 +1922,8 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
               if (na < 4) fa[na++] = &ss[i];
               else fb[nb++] = &ss[i];
             }
+          if (it == n - 1) { fb[nb++] = &es[0]; e_done[0] = true; }
+          if (it == 0 && n > 1) { fb[nb++] = &es[1]; e_done[1] = true; }
           MMArgs<T> a;
           MMProbs<T> pr{};
           l23_build(net, fa, na, 0, a, pr);
@@ -1902,19 +1952,12 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
         fwd += 6;
       }
       for (int v = 0; v < 6; ++v) cur[v] = q3[(n - 1) % 3][v];
-      // energies (hmc.py:67-71: E_new with forward 6n's masks, E_current with forward 6n + 1's) in one launch
-      SubStep<T> es[2];
-      for (int e = 0; e < 2; ++e) {
-        SubStep<T>& x = es[e];
-        x.xw = e == 0 ? net.xw : xw_par;
-        for (int v = 0; v < 6; ++v) x.q[v] = e == 0 ? cur[v] : par[v];
-        x.ms = masks_for(fwd + e);
-        x.scr = &pn[e];
-        x.lpart = e == 0 ? lp_new : lp_cur;
-        x.w = L3Want{false, false, false, false, false};
-        x.v = -1;
-      }
-      for (int e0 = 0; e0 < 2; e0 += fit) HMCX_HIP(ctx, mlp_forward_batch<T>(net, es + e0, std::min(fit, 2 - e0)));
+      // the energies that did not ride along, in one launch (xw holds the last iteration's xw)
+      SubStep<T> rest[2];
+      int nr = 0;
+      for (int e = 0; e < 2; ++e)
+        if (!e_done[e]) rest[nr++] = es[e];
+      for (int e0 = 0; e0 < nr; e0 += fit) HMCX_HIP(ctx, mlp_forward_batch<T>(net, rest + e0, std::min(fit, nr - e0)));
       fwd += 2;
     }
     for (int it = 0; it < n && !batch; ++it) {
@@ -1955,7 +1998,14 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
     ac.out_E = s->out_E ? s->out_E + 2 * si : nullptr;
     ac.acc_flag = accf;
     hipLaunchKernelGGL(k_mlp_accept, dim3(1), dim3(26 * 32), 0, st, ac);
-    if (n > 0) hipLaunchKernelGGL(k_mlp_commit<T>, dim3(NPART, 6), dim3(256), 0, st, ve, accf);
+    if (n > 0) {                       // commit: in the next step's start launch, or here after the last step
+      if (si + 1 < s->n_steps) {
+        commit_pending = true;
+        for (int v = 0; v < 6; ++v) prev_prop[v] = cur[v];
+      } else {
+        hipLaunchKernelGGL(k_mlp_commit<T>, dim3(NPART, 6), dim3(256), 0, st, ve, accf);
+      }
+    }
     HMCX_HIP(ctx, hipGetLastError());
   }
   if ((rc = gs.finish())) return rc;
