@@ -1520,6 +1520,41 @@ hipError_t mlp_l23_ga1(MlpNet<T>& net, const SubStep<T>* const* fw, int nf, cons
   return hipErrorInvalidValue;
 }
 
+// Layer 1 of the next iteration (xw = X·W1ᵀ into `out`, net's X) and the W2 gradient of sub-step net
+// `w2n` in one launch (k_mm2): the W2 gradient reads the CURRENT iteration's xw (another buffer) and
+// writes only W2's momentum and next position; layer 1 reads only X and W1.  False: the operands are
+// not all 16-byte aligned (the caller launches them one by one).
+template <typename T>
+hipError_t mlp_l1_w2(MlpNet<T>& net, const T* W1, T* out, MlpNet<T>& w2n, const SubStep<T>& s2, const Upd<T>& u2,
+                     bool* done) {
+  *done = false;
+  MMArgs<T> a1{}, a2;
+  MMProbs3<T> p1{};
+  mm_set<T>(a1, net.B, net.n_mid, net.n_in, net.X, net.n_in, 0, W1, net.n_in, 1, out, net.n_mid);
+  wgrad_build(w2n, s2, 2, u2, a2);
+  a1.pend.n = 0;
+  a2.pend.n = 0;
+  const int mk = mask_kind(a2.ms);
+  if (sizeof(T) != 4 || (mk != MK_KEEP && mk != MK_VALS) || net.n_in % 4 || !vec_ok(net.X, net.n_in, sizeof(T)) ||
+      !vec_ok(W1, net.n_in, sizeof(T)))
+    return hipSuccess;
+  const int3 g1 = make_int3((a1.M + 31) / 32, (a1.N + 31) / 32, 1);
+  const int2 g2 = make_int2((a2.M + 31) / 32, (a2.N + 31) / 32);
+  const dim3 grid((unsigned)std::max(g1.x, g2.x), (unsigned)std::max(g1.y, g2.y), 2u);
+  hipStream_t st = net.st;
+  if constexpr (sizeof(T) == 4) {
+    auto go = [&](auto mkc) {
+      constexpr int MK = decltype(mkc)::value;   // layer 1 reads no masks: any kind is its plain code
+      hipLaunchKernelGGL((k_mm2<T, MM_STORE, OP_PLAIN, OP_PLAIN, 0, 1, 1, 1, MM_UPD, OP_PLAIN, OP_H1, 1, 0, 0, 0, MK>),
+                         grid, dim3(MM_NT), 0, st, a1, p1, a2, g1, g2);
+    };
+    if (mk == MK_KEEP) go(std::integral_constant<int, MK_KEEP>{});
+    else go(std::integral_constant<int, MK_VALS>{});
+    *done = true;
+  }
+  return hipGetLastError();
+}
+
 template <typename T>
 hipError_t mlp_w1_w2(MlpNet<T>& net, MlpNet<T>& w1n, const SubStep<T>& s1, const Upd<T>& u1, MlpNet<T>& w2n,
                      const SubStep<T>& s2, const Upd<T>& u2) {
@@ -1757,7 +1792,7 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
       if ((s->mask_off[si] * sizeof(T)) % 16) net.vec_masks = false;
   }
   Workspace ws(ctx);
-  T *pv[6], *qa[6], *qb[6], *qc[6], *xw_par = nullptr;
+  T *pv[6], *qa[6], *qb[6], *qc[6], *xw_par = nullptr, *xw_b1 = nullptr;
   double *part_cur, *part_new, *lp_cur, *lp_new, *lp_scr;
   uint32_t* keep = nullptr;                                  // keep flags of the step: one bit per element
   const int kw = (n3 + 31) / 32;                              // words per forward
@@ -1781,6 +1816,7 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
     }
     if (batch) {
       xw_par = ws.take<T>((size_t)mn);
+      xw_b1 = ws.take<T>((size_t)mn);
       for (auto& e : en) e.gz = ws.take<T>((size_t)s->B * s->n_out);
     }
     part_cur = ws.take<double>(12 * NPART);
@@ -1868,12 +1904,16 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
       // energies (hmc.py:67-71): E_new at the last iteration's positions with forward 6n's masks,
       // E_current at the start state with forward 6n + 1's.  Both only need what is known when the
       // last (first) iteration starts, so they ride in its second launch when there is room
+      // xw of iteration it in xwb[it & 1]: the next iteration's layer 1 may run beside this
+      // iteration's W2 gradient, which reads this iteration's xw
+      T* const xwb[2] = {net.xw, xw_b1};
       SubStep<T> es[2];
       bool e_done[2] = {false, false};
+      bool l1_done = false;
       T* const* Xlast = q3[(n - 1) % 3];
       for (int e = 0; e < 2; ++e) {
         SubStep<T>& x = es[e];
-        x.xw = e == 0 ? net.xw : xw_par;
+        x.xw = e == 0 ? xwb[(n - 1) & 1] : xw_par;
         for (int v = 0; v < 6; ++v) x.q[v] = e == 0 ? Xlast[v] : par[v];
         x.ms = masks_for(6 * n + e);
         x.scr = &en[e];
@@ -1885,13 +1925,16 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
         T* const* Xit = q3[it % 3];                              // positions of iteration it
         T* const* Xpr = it == 0 ? par : q3[(it + 2) % 3];        // of iteration it − 1
         T* const* Xnx = q3[(it + 1) % 3];                        // the next iteration's (written here)
+        net.xw = xwb[it & 1];
+        for (int i = 0; i < 6; ++i) pn[i].xw = net.xw;
         if (it == 0) {                                           // xw(0) and the start state's xw (E_current)
           const T* w1[2] = {qa[0], par[0]};
           T* out[2] = {net.xw, xw_par};
           HMCX_HIP(ctx, mlp_layer1_batch<T>(net, w1, out, 2));
-        } else {
+        } else if (!l1_done) {
           HMCX_HIP(ctx, mlp_layer1<T>(net, Xit[0]));
         }
+        l1_done = false;
         SubStep<T> ss[6];
         const SubStep<T>* ga[6];
         int nga = 0;
@@ -1929,12 +1972,17 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
           l23_build(net, fa, na, 0, a, pr);
           HMCX_HIP(ctx, (mm<T, MM_L23, 0, 1, OP_H1>(net, a, &pr)));
           HMCX_HIP(ctx, mlp_l23_ga1<T>(net, fb, nb, ga, nga));
+          // the W1 gradient with every pending bias / W3 update in its extra plane; then the next
+          // iteration's layer 1 beside this iteration's W2 gradient (which needs neither)
           for (int i = 0; i < 6; ++i) {
             const int v = s->order[i];
-            if (v != 0 && v != 2) set_pending(net, v, UPD_SGHMC, upd_for(it, v, Xit[v], it + 1 < n ? Xnx[v] : nullptr), &pn[i]);
+            if (v != 0 && v != 2) set_pending(pn[0], v, UPD_SGHMC, upd_for(it, v, Xit[v], it + 1 < n ? Xnx[v] : nullptr), &pn[i]);
           }
-          HMCX_HIP(ctx, mlp_w1_w2<T>(net, pn[0], ss[0], upd_for(it, 0, Xit[0], it + 1 < n ? Xnx[0] : nullptr), pn[i2],
-                                     ss[i2], upd_for(it, 2, Xit[2], it + 1 < n ? Xnx[2] : nullptr)));
+          HMCX_HIP(ctx, mlp_wgrad<T>(pn[0], ss[0].q, ss[0].ms, 0, UPD_SGHMC,
+                                     upd_for(it, 0, Xit[0], it + 1 < n ? Xnx[0] : nullptr)));
+          const Upd<T> u2 = upd_for(it, 2, Xit[2], it + 1 < n ? Xnx[2] : nullptr);
+          if (it + 1 < n) HMCX_HIP(ctx, mlp_l1_w2<T>(net, Xnx[0], xwb[(it + 1) & 1], pn[i2], ss[i2], u2, &l1_done));
+          if (!l1_done) HMCX_HIP(ctx, mlp_wgrad<T>(pn[i2], ss[i2].q, ss[i2].ms, 2, UPD_SGHMC, u2));
           fwd += 6;
           continue;
         }
@@ -1952,13 +2000,14 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
         fwd += 6;
       }
       for (int v = 0; v < 6; ++v) cur[v] = q3[(n - 1) % 3][v];
-      // the energies that did not ride along, in one launch (xw holds the last iteration's xw)
+      // the energies that did not ride along (each names its xw), in one launch (xw holds the last iteration's xw)
       SubStep<T> rest[2];
       int nr = 0;
       for (int e = 0; e < 2; ++e)
         if (!e_done[e]) rest[nr++] = es[e];
       for (int e0 = 0; e0 < nr; e0 += fit) HMCX_HIP(ctx, mlp_forward_batch<T>(net, rest + e0, std::min(fit, nr - e0)));
       fwd += 2;
+      net.xw = xwb[0];                                         // the net's own buffer again
     }
     for (int it = 0; it < n && !batch; ++it) {
       for (int i = 0; i < 6; ++i) {
