@@ -84,21 +84,41 @@ def launch_ranks(n, argv):
                    GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HMCX_BENCH_CHILD="1")
         procs.append(subprocess.Popen([sys.executable, me] + list(argv), env=env, cwd=REPO,
                                       stdout=out0 if r == 0 else subprocess.DEVNULL))
+    def _term(signum, frame):
+        raise SystemExit(128 + signum)
+    signal.signal(signal.SIGTERM, _term)        # so the finally below runs on a SIGTERM to this parent
     rc = 0
     live = list(procs)
-    while live:
-        time.sleep(0.2)
-        for p in list(live):
-            c = p.poll()
-            if c is None:
-                continue
-            live.remove(p)
-            if c != 0 and rc == 0:
-                rc = c if c > 0 else 128 - c
-                print("bench: rank %d exited with %d; stopping the other ranks" % (procs.index(p), c),
-                      file=sys.stderr)
-                for q in live:
-                    q.send_signal(signal.SIGTERM)
+    deadline = time.monotonic() + float(os.environ.get("HMCX_BENCH_DEADLINE_S", "1800"))
+    try:
+        while live:
+            time.sleep(0.2)
+            if time.monotonic() > deadline:
+                print("bench: ranks still running after the deadline; stopping them", file=sys.stderr)
+                rc = rc or 124
+                break
+            for p in list(live):
+                c = p.poll()
+                if c is None:
+                    continue
+                live.remove(p)
+                if c != 0 and rc == 0:
+                    rc = c if c > 0 else 128 - c
+                    print("bench: rank %d exited with %d; stopping the other ranks" % (procs.index(p), c),
+                          file=sys.stderr)
+                    for q in live:
+                        q.send_signal(signal.SIGTERM)
+    finally:
+        # a hung rank, a failed one or a signal to this parent: no child outlives it (exact PIDs)
+        for q in procs:
+            if q.poll() is None:
+                q.send_signal(signal.SIGTERM)
+        for q in procs:
+            try:
+                q.wait(timeout=20)
+            except subprocess.TimeoutExpired:
+                q.kill()
+                q.wait()
     out0.seek(0)
     text = out0.read()
     lines = [ln for ln in text.splitlines() if ln.strip().startswith("{")]
@@ -188,9 +208,33 @@ def _cpu_baseline(X, Y, budget_s):
             "kind": "port",
             "sample": "oracle/samplers.py SGHMC (NumPy f64, bit-exact to the reference) incl. its per-10-minibatch "
                       "log-likelihood logging: %d steps / %.0f leapfrogs on minibatches of B=500 (D=784, K=10), "
-                      "eps=1e-3, lambda=1e-2, %.1f s, %d BLAS threads, host %s (%d CPUs in affinity mask)" % (
-                          steps, lf, t_total, threads, cpu_model(), len(os.sched_getaffinity(0))),
+                      "eps=1e-3, lambda=1e-2, %.1f s, %d BLAS threads, host %s (%d CPUs in affinity mask; "
+                      "OMP_NUM_THREADS=%s is this job's CPU share, so 'all cores' = that share, not the mask)" % (
+                          steps, lf, t_total, threads, cpu_model(), len(os.sched_getaffinity(0)),
+                          os.environ.get("OMP_NUM_THREADS", "unset")),
             "lf_per_s": lf / t_total}
+
+
+def calibrated(line):
+    """Attach the committed port/reference throughput ratio (profiles/cpu_calibration.json, made by
+    tools/cpu_calibration.py in the build container, where the reference exists: the oracle's SGHMC
+    against the reference's own sghmc.py + softmax.py on the same loop) for the nearest BLAS thread
+    count; ratio > 1 means the port is faster than the reference (the reference also evaluates the dead
+    gradient of sghmc.py:26 every step)."""
+    f = os.path.join(REPO, "profiles", "cpu_calibration.json")
+    try:
+        with open(f) as fh:
+            cal = json.load(fh)["by_threads"]
+    except (OSError, ValueError, KeyError):
+        line["calibration_ratio"] = None
+        return line
+    thr = min(cal, key=lambda t: abs(int(t) - int(line["cores"])))
+    line["calibration_ratio"] = cal[thr]["ratio_port_over_reference"]
+    line["calibration"] = ("port/reference lf/s = %.3f at %s BLAS thread(s) in the build container "
+                           "(profiles/cpu_calibration.json); reference-equivalent value = value / ratio"
+                           % (cal[thr]["ratio_port_over_reference"], thr))
+    line["reference_equivalent_value"] = line["value"] / cal[thr]["ratio_port_over_reference"]
+    return line
 
 
 def pmc_file(dtype, path):
@@ -538,8 +582,18 @@ def bench(args, parallel):
         v_out = plantvillage_measure(args.sgld_steps, rank)
         parallel.barrier()
     parallel.barrier()
-    if rank != 0:
-        return                        # main() tears the process group down on every rank
+    if rank == 0:
+        report(args, world, value, t_max, lf_total, lf_local, n_calls, kern_ms, kern_n, diag_par, diag,
+               batched, mlp_out, v_out, X, Y)
+    # closing barrier: every rank waits here until rank 0 has run its CPU baselines and printed, so the
+    # RCCL communicator and the process group are torn down by all ranks together (main()'s finally)
+    parallel.barrier()
+
+
+def report(args, world, value, t_max, lf_total, lf_local, n_calls, kern_ms, kern_n, diag_par, diag,
+           batched, mlp_out, v_out, X, Y):
+    """Rank 0: the JSON line (and the CPU baselines, after every rank's GPU work)."""
+    from dropout_hamiltonian_montecarlo_amd import parallel
     path = "persistent" if (args.path != "kernels") else "kernels"
     assert kern_n == n_calls, (kern_n, n_calls)
     launch_ms = kern_ms / kern_n
@@ -586,8 +640,8 @@ def bench(args, parallel):
     }
     if args.cpu_seconds > 0:
         # rank 0, after every rank's GPU work (the barrier above): the oracle on host cores
-        out["cpu_baseline"] = cpu_baseline(X, Y, args.cpu_seconds)
-        out["cpu_baseline_1thread"] = cpu_baseline(X, Y, args.cpu_seconds, threads=1)
+        out["cpu_baseline"] = calibrated(cpu_baseline(X, Y, args.cpu_seconds))
+        out["cpu_baseline_1thread"] = calibrated(cpu_baseline(X, Y, args.cpu_seconds, threads=1))
         if mlp_out is not None:
             mlp_out["cpu_baseline"] = mlp_cpu_baseline(X, np.argmax(Y, axis=1), args.cpu_seconds)
         if v_out is not None:

@@ -1757,6 +1757,10 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
   int maxF = 2;
   for (int si = 0; si < s->n_steps; ++si) {
     if (s->n_iter[si] < 0) return set_error(ctx, HMCX_EINVAL, "mlp sghmc: n_iter < 0");
+    // the step-start launch has one grid row per forward of the step (gridDim.y = 6 + 6·n_iter + 2,
+    // capped at 65535 by the hardware)
+    if (s->n_iter[si] > (65535 - 8) / 6)
+      return set_error(ctx, HMCX_EINVAL, "mlp sghmc: n_iter above 10921 leapfrog iterations per step");
     maxF = std::max(maxF, 6 * s->n_iter[si] + 2);
   }
   const bool philox_masks = s->mask_mode == HMCX_NOISE_PHILOX;

@@ -286,6 +286,40 @@ __device__ inline bool gather(__amdgpu_buffer_rsrc_t rs, int base0, int pstride,
   return gather_u<4>(rs, base0, pstride, np, nitems, ioff, want, ep, abort_flag, stage);
 }
 
+// ---------------------------------------------------------------- commit decision
+// One 64-bit word per launch decides whether the launch commits: (epoch << 2) | d, d = 1 commit,
+// d = 2 abort, set ONCE by a compare-and-swap (vector global atomic; words of earlier launches carry
+// older epochs).  Whoever swaps first decides; every other proposer, and every waiter, adopts that
+// value — so all workgroups that read a decision read the same one, whatever their timeouts.
+constexpr int P2_COMMIT = 1, P2_ABORT = 2;
+__device__ inline int p2_decide(unsigned long long* w, unsigned ep, int d) {
+  const unsigned long long mine = ((unsigned long long)ep << 2) | (unsigned)d;
+  unsigned long long cur = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  while ((cur >> 2) != (unsigned long long)ep) {
+    if (__hip_atomic_compare_exchange_strong(w, &cur, mine, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT))
+      return d;
+  }
+  return (int)(cur & 3ull);
+}
+// Waits (bounded) for the launch's decision; on timeout or a raised abort word it proposes abort —
+// and adopts whatever was decided first.  A decided abort raises the context's sticky abort word.
+__device__ inline int p2_wait_decision(unsigned long long* w, unsigned ep, int* abort_flag) {
+  unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  for (int spins = 0;; ++spins) {
+    const unsigned long long cur = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((cur >> 2) == (unsigned long long)ep) return (int)(cur & 3ull);
+    if ((spins & 63) == 63 &&
+        (__builtin_amdgcn_s_memrealtime() - t0 > QTIMEOUT ||
+         __hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+      const int d = p2_decide(w, ep, P2_ABORT);
+      if (d == P2_ABORT) __hip_atomic_store(abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return d;
+    }
+    if (HMCX_P2_SLEEP) __builtin_amdgcn_s_sleep(1);
+  }
+}
+
 // Workgroup-uniform verdict after a gather (also the barrier that publishes dst).
 __device__ inline bool all_ok(bool ok, int* sh_fail) {
   if (!ok) *sh_fail = 1;

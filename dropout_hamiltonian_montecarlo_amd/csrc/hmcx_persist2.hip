@@ -94,14 +94,15 @@ __device__ inline V sched_at(bool inl, int s, V kv, const V* g) {
   return inl ? kv : gv;
 }
 
-// Writes the launch's abort verdict when the workgroup leaves the kernel, whichever return it takes:
-// workgroup 0 reaching the end means every member passed the last accept round (0); any early return
-// is a timed-out hand-off or a sticky abort word (1).
+// Writes the launch's abort verdict when a workgroup leaves the kernel without committing (a timed-out
+// hand-off, a sticky abort word, or a decided abort): 1.  The host zeroes the verdict before the launch
+// and nothing stores 0, so the verdict is sticky — an abort is never overwritten (the commit decision
+// makes "no workgroup stored 1" and "every workgroup committed" the same event).
 struct P2Verdict {
   int* out;
-  bool first, done;
+  bool done;
   __device__ ~P2Verdict() {
-    if (out && (!done || first)) out[0] = done ? 0 : 1;
+    if (out && !done) out[0] = 1;
   }
 };
 constexpr int P2TR_IT = 16;                 // traced leapfrog iterations
@@ -314,7 +315,7 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
   const int wl = (fo0 + od) * 16 + okc;               // index in Wf
   T pw = T(0), wv = T(0), w0 = T(0), zn = T(0);
 
-  P2Verdict verdict{threadIdx.x == 0 ? a.verdict : nullptr, bid == 0, false};
+  P2Verdict verdict{threadIdx.x == 0 ? a.verdict : nullptr, false};
   const bool inl = a.ninl > 0;
   // a launch behind a timed-out one (sticky abort word) leaves everything untouched
   if (__hip_atomic_load(a.abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
@@ -857,19 +858,28 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
   }
   prof.stamp(0);
   prof.flush();
-  // ---- commit round: every workgroup publishes a 'done' granule and waits for all G before it
-  //      writes its slice.  A member that timed out anywhere never publishes, so every other member
-  //      times out here too: either every workgroup writes its slice of W/b or none does (checking
-  //      the abort word right before the stores alone left a window — members can see a late
-  //      granule at different times, e.g. under a misplaced team, HMCX_P2_XMAP=2)
+  // ---- commit round: every workgroup publishes a 'done' granule; workgroup 0 gathers all G and
+  //      proposes commit (or abort, when its gather times out or sees the abort word) on the launch's
+  //      decision word; the others wait for the decision (bounded: on timeout they propose abort).
+  //      The first compare-and-swap decides and everyone follows it, so either every workgroup
+  //      writes its slice of W/b or none does — independent timeouts (each measured from its own
+  //      publish) cannot split the launch, and a decided abort leaves W/b untouched for the re-run.
+  //      A member that timed out anywhere earlier never publishes, so workgroup 0 cannot commit.
   ++ep;
   if (tid == 0) put(rs, a.oXC + bid, 1.0, ep);
   {
-    const bool ok = gather_st(rs, a.oXC, 1, G, 1, [](int) { return 0; }, ep, a.abort_flag, [](int, double) {});
-    if (!all_ok(ok, ish)) return;
+    unsigned long long* dword = reinterpret_cast<unsigned long long*>(a.arena + (size_t)(a.oXC + G) * 16);
+    if (bid == 0) {
+      const bool ok = gather_st(rs, a.oXC, 1, G, 1, [](int) { return 0; }, ep, a.abort_flag, [](int, double) {});
+      const bool all = all_ok(ok, ish);
+      if (tid == 0) ish[1] = p2_decide(dword, ep, all ? P2_COMMIT : P2_ABORT);
+    } else if (tid == 0) {
+      ish[1] = p2_wait_decision(dword, ep, a.abort_flag);
+    }
+    __syncthreads();
+    if (ish[1] != P2_COMMIT) return;
   }
   // ---- committed state: owners write their weights, workgroup 0 the bias
-  if (__hip_atomic_load(a.abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
   verdict.done = true;
   if (own) reinterpret_cast<T*>(a.W)[e_own] = wv;
   if (bid == 0 && tid < K) reinterpret_cast<T*>(a.b)[tid] = bsh[tid];
@@ -942,7 +952,7 @@ int sghmc_p2_t(hmcx_ctx* ctx, const hmcx_sampler_args* s, const PersistPlan2& pl
   const long nXA = 2L * G * pl.Br * KC, nXD = 2L * G * p2_pad(KC + 1 + pl.Ro * KC, pad),
              nXB = 2L * G * p2_pad(KC + 1 + pl.Bf * KC, pad), nXW = 2L * G * p2_pad(pl.Fo * KC, pad),
              nXS = 2L * G * (pad ? 8 : 4);
-  const long nXC = G;
+  const long nXC = G + 1;                        // 'done' granules + the launch's decision word
   const long ngran = nXA + nXD + nXB + nXW + nXS + nXC + 1;
   if (ngran * 16 > 0x7fffffffL) return set_error(ctx, HMCX_EUNSUPPORTED, "persistent SGHMC: arena too large");
   int rc = abort_precheck(ctx);                  // an earlier launch's timeout, before enqueueing more
@@ -1091,6 +1101,12 @@ int sghmc_p2_t(hmcx_ctx* ctx, const hmcx_sampler_args* s, const PersistPlan2& pl
   if ((rc = kernel_occupancy(ctx, kfn, QTH, (int)pl.lds, &per_cu))) return rc;
   if ((long)per_cu * ctx->num_cus < G)
     return set_error(ctx, HMCX_EUNSUPPORTED, "persistent SGHMC: workgroups cannot be co-resident");
+  // the verdict is sticky (P2Verdict): zeroed here, only a workgroup that leaves without committing
+  // stores 1.  The call's output slot is idle at enqueue time (the caller collected its previous use).
+  if (direct_host)
+    *reinterpret_cast<volatile int*>(a.verdict) = 0;
+  else if (a.verdict)
+    HMCX_HIP(ctx, hipMemsetAsync(a.verdict, 0, sizeof(int), ctx->stream));
   if ((rc = timing_begin(ctx, ctx->stream))) return rc;
   HMCX_HIP(ctx, hipLaunchKernel(kfn, dim3(G), dim3(QTH), kargs, (unsigned)pl.lds, ctx->stream));
   if ((rc = timing_end(ctx, ctx->stream))) return rc;

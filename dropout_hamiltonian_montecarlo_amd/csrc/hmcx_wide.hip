@@ -26,6 +26,7 @@
 #include "hmcx_common.h"
 #include "hmcx_internal.h"
 #include "hmcx_p2x.h"
+#include "hmcx_granule.h"
 #include <algorithm>
 #include <cstdio>
 #include <vector>
@@ -50,6 +51,10 @@ template <typename T> struct WideArgs {
   uint64_t seed; uint32_t chain, step;   // PHILOX: keyed by chain + c
   unsigned long long* prof;              // HMCX_WIDE_PROF: per-workgroup s_memrealtime stamps (WPH each)
   int wt;                                // slab / diff stored write-through (sc1; HMCX_WIDE_WT=0: plain)
+  // fused forward + softmax (k_wfwd_sm): the row team's partial logits travel as tagged granules
+  char* gx; int gx_bytes; unsigned ep;   // the context's granule arena and this launch's epoch
+  int* abort_flag;                       // the context's sticky abort word (raised on a timed-out poll)
+  int force_abort;                       // test knob (HMCX_WIDE_FORCE_ABORT): workgroup 0 raises the word
 };
 
 // a store that leaves the XCD's L2 (sc1: written through, the line dropped) or a plain one: the
@@ -204,6 +209,173 @@ __global__ __launch_bounds__(WTH) void k_wsoft(WideArgs<T> a) {
     if (tid == 0) a.llp[(size_t)ch * a.nSB + blockIdx.x] = ((ll[0] + ll[1]) + ll[2]) + ll[3];
   }
   WSTAMP(3);
+}
+
+// One softmax row (lane = class): Σ_z of the row's partials in slice order (the caller's sum), + b,
+// clip, softmax by wave reductions; the diff row (gradient pass) or the row's log-likelihood term.
+template <typename T>
+__device__ inline double wide_softmax_row(const WideArgs<T>& a, int ch, int row, int k, T xw) {
+  const int K = a.K;
+  const bool kv = k < K;
+  const int kc = min(k, K - 1);
+  const T bk = a.b[ch * K + kc], yk = a.Y[(size_t)row * K + kc];                          // unconditional loads
+  const T zz = kv ? clipz(xw + bk, a.clip_hi, a.clip_lo) : (T)-__builtin_inf();            // softmax.py:39-41
+  const T m = wave_max(zz);
+  const T e = kv ? exp(zz - m) : T(0);                                                    // softmax.py:34
+  const T s = wave_sum(e);
+  const T y = kv ? yk : T(0);
+  if (a.want_diff) {
+    const T d = kv ? y - e / s : T(0);                                                    // softmax.py:52
+    if (k < a.KP) wstore(a.diff + ((size_t)ch * a.B + row) * a.KP + k, d, a.wt);
+    return 0.0;
+  }
+  const T lse = log(s) + m;                                                               // softmax.py:18-20
+  return wave_sum(kv ? (double)(y * (zz - lse)) : 0.0);
+}
+
+// ---------------------------------------------------------------- fused forward + softmax
+// k_wfwd's partial logits, then ONE team round instead of a kernel boundary and k_wsoft: the S
+// workgroups of a row block (its D slices) publish their 32 × K partials as tagged granules
+// (hmcx_granule.h), workgroup z owns rows [z·R, z·R + R) (R = ⌈32/S⌉), gathers their S partials
+// (pairs dealt over all threads, landing in LDS), sums them in slice order — the order k_wsoft sums
+// the slab in, so the logits are bit-identical — and runs the softmax rows.  The grid must be
+// co-resident (checked on the host); polls are bounded (2 s) and raise the context's abort word.
+constexpr int WSM_STAGE = 8 * WTH;       // gathered (slice, row, class) partials per workgroup (LDS)
+template <typename T, int KB>
+__global__ __launch_bounds__(WTH) void k_wfwd_sm(WideArgs<T> a) {
+  using M = mfma16<T>;
+  constexpr int KP = 16 * KB;
+  __shared__ __align__(16) T red[4 * WRB * KP];
+  __shared__ double stage[WSM_STAGE];
+  __shared__ double llw[4];
+  __shared__ int fail;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lg = lane >> 4;
+  const int m0 = blockIdx.x * WRB, z = blockIdx.y, ch = blockIdx.z;
+  const int dlo = min(a.D, z * a.Dz), dhi = min(a.D, dlo + a.Dz);
+  const int nrow = min(WRB, a.B - m0), K = a.K, NW = a.C * K, S = a.S;
+  const T* Wc = a.W + (size_t)ch * K;
+  WSTAMP(0);
+  if (tid == 0) fail = 0;
+  const int f0 = dlo + 32 * wave + 8 * lg;
+  const int fsafe = dlo < a.D ? dlo : 0;
+  T xa[2][8], wb[8][KB];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt) {
+    const int i = mt * 16 + lr;
+    const T* xr = a.X + (size_t)m0 * a.D + (size_t)(i < nrow ? i : 0) * a.D;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) xa[mt][j] = xr[f0 + j < dhi ? f0 + j : fsafe];
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int nb = 0; nb < KB; ++nb) {
+      const int c = nb * 16 + lr;
+      wb[j][nb] = Wc[(f0 + j < dhi && c < K) ? (size_t)(f0 + j) * NW + c : 0];
+    }
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (!(mt * 16 + lr < nrow && f0 + j < dhi)) xa[mt][j] = T(0);
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int nb = 0; nb < KB; ++nb)
+      if (!(f0 + j < dhi && nb * 16 + lr < K)) wb[j][nb] = T(0);
+  WSTAMP(1);
+  typename M::acc_t acc[2][KB];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int nb = 0; nb < KB; ++nb) acc[mt][nb] = M::zero();
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int nb = 0; nb < KB; ++nb) {
+      acc[0][nb] = M::fma(xa[0][j], wb[j][nb], acc[0][nb]);
+      acc[1][nb] = M::fma(xa[1][j], wb[j][nb], acc[1][nb]);
+    }
+  WSTAMP(2);
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int nb = 0; nb < KB; ++nb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        red[(wave * WRB + mt * 16 + M::row(lane, q)) * KP + nb * 16 + lr] = acc[mt][nb][q];
+  __syncthreads();
+  // publish the workgroup's partial (the 4 waves summed in wave order, as k_wfwd's slab entry)
+  const __amdgpu_buffer_rsrc_t rs = gx_rsrc(a.gx, a.gx_bytes);
+  const int blk = WRB * K;                                       // granules per producer
+  const int team = (ch * gridDim.x + blockIdx.x) * S;            // first producer block of my team
+  for (int e = tid; e < nrow * K; e += WTH) {
+    const int i = e / K, k = e - (e / K) * K, x = i * KP + k;
+    const T v = ((red[x] + red[WRB * KP + x]) + red[2 * WRB * KP + x]) + red[3 * WRB * KP + x];
+    gx_put(rs, (team + z) * blk + e, (double)v, a.ep);
+  }
+  if (a.force_abort && blockIdx.x == 0 && z == 0 && ch == 0 && tid == 0)
+    __hip_atomic_store(a.abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  WSTAMP(3);
+  // gather my rows' partials from the S producers: pair q = p·nit + it, it = row-in-slice·K + class
+  const int R = (WRB + S - 1) / S;
+  const int r0 = min(nrow, z * R), r1 = min(nrow, r0 + R);
+  const int nit = (r1 - r0) * K, npair = S * nit;
+  {
+    typedef unsigned int g4 __attribute__((ext_vector_type(4)));
+    constexpr int U = WSM_STAGE / WTH;
+    unsigned pend = 0;
+    int o[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int q = tid + u * WTH;
+      const int p = q / max(nit, 1), it = q - p * max(nit, 1);
+      const bool w = q < npair;
+      pend |= w ? 1u << u : 0u;
+      o[u] = w ? ((team + p) * blk + r0 * K + it) * 16 : 0;
+    }
+    unsigned long long t0 = 0;
+    bool ok = true;
+    for (int spins = 0; pend; ++spins) {
+      g4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, o[u], 0, 16 /* sc1 */);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (((pend >> u) & 1u) && v[u].y == a.ep && v[u].w == a.ep) {
+          stage[tid + u * WTH] = __builtin_bit_cast(double, (unsigned long long)v[u].x | ((unsigned long long)v[u].z << 32));
+          pend &= ~(1u << u);
+        }
+      if (!pend) break;
+      if (spins == 0) t0 = __builtin_amdgcn_s_memrealtime();
+      if ((spins & 63) == 63 && (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull ||
+                                 __hip_atomic_load(a.abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+        __hip_atomic_store(a.abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = false;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (!ok) fail = 1;
+  }
+  __syncthreads();
+  WSTAMP(4);
+  if (fail) return;                    // the host sees the abort word and re-runs the call unfused
+  double t = 0.0;
+  for (int row = r0 + wave; row < r1; row += 4) {
+    const int kc = min(lane, K - 1);
+    const int ri = (row - r0) * K + kc;
+    T xw = (T)stage[ri];
+    for (int p = 1; p < S; ++p) xw = xw + (T)stage[p * nit + ri];          // k_wsoft's slab order
+    t += wide_softmax_row(a, ch, m0 + row, lane, xw);
+  }
+  WSTAMP(5);
+  if (!a.want_diff) {                  // the logging pass: ll partial of my rows (waves in order)
+    if (lane == 0) llw[wave] = t;
+    __syncthreads();
+    if (tid == 0) a.llp[((size_t)ch * gridDim.x + blockIdx.x) * S + z] = ((llw[0] + llw[1]) + llw[2]) + llw[3];
+  }
+  WSTAMP(6);
 }
 
 template <typename T>
@@ -383,11 +555,53 @@ static void launch_fwd(const WideArgs<T>& a, hipStream_t st) {
   }
 }
 
+template <typename T, int KB>
+static void launch_fwd_sm_kb(const WideArgs<T>& a, hipStream_t st) {
+  hipLaunchKernelGGL((k_wfwd_sm<T, KB>), dim3((a.B + WRB - 1) / WRB, a.S, a.C), dim3(WTH), 0, st, a);
+}
+template <typename T>
+static void launch_fwd_sm(const WideArgs<T>& a, hipStream_t st) {
+  switch (a.KP / 16) {
+    case 1: launch_fwd_sm_kb<T, 1>(a, st); break;
+    case 2: launch_fwd_sm_kb<T, 2>(a, st); break;
+    case 3: launch_fwd_sm_kb<T, 3>(a, st); break;
+    default: launch_fwd_sm_kb<T, 4>(a, st); break;
+  }
+}
+template <typename T>
+static const void* fwd_sm_fn(int KP) {
+  switch (KP / 16) {
+    case 1: return (const void*)k_wfwd_sm<T, 1>;
+    case 2: return (const void*)k_wfwd_sm<T, 2>;
+    case 3: return (const void*)k_wfwd_sm<T, 3>;
+    default: return (const void*)k_wfwd_sm<T, 4>;
+  }
+}
+
+template <typename T>
+static int sgld_wide_impl(hmcx_ctx* ctx, const hmcx_sampler_args* s, bool allow_fuse);
+
 template <typename T>
 int sgld_wide_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
+  return sgld_wide_impl<T>(ctx, s, true);
+}
+
+template <typename T>
+static int sgld_wide_impl(hmcx_ctx* ctx, const hmcx_sampler_args* s, bool allow_fuse) {
   const int B = s->B, D = s->D, K = s->K, C = s->C, KP = (K + 15) / 16 * 16;
   const int S = (D + WDZ - 1) / WDZ, Dz = ((D + S - 1) / S + 3) / 4 * 4;
   const int nSB = (B + WSR - 1) / WSR;
+  const int nRB = (B + WRB - 1) / WRB;
+  // fused forward + softmax (k_wfwd_sm: one team round instead of k_wsoft and a kernel boundary) when
+  // the whole forward grid is co-resident and a workgroup's gathered partials fit its LDS stage;
+  // HMCX_WIDE_FUSE=0 keeps the three launches
+  const int fuse_env = getenv("HMCX_WIDE_FUSE") ? atoi(getenv("HMCX_WIDE_FUSE")) : 1;     // read per call (tests)
+  bool fuse = allow_fuse && fuse_env != 0 && S * ((WRB + S - 1) / S) * K <= WSM_STAGE;
+  if (fuse) {
+    int per_cu = 0, rc0 = kernel_occupancy(ctx, fwd_sm_fn<T>(KP), WTH, 0, &per_cu);
+    if (rc0) return rc0;
+    fuse = (long)per_cu * ctx->num_cus >= (long)nRB * S * C;
+  }
   const int ntile = (D + 15) / 16;
   const size_t nsc = (size_t)s->n_steps * C;
   // HMCX_WIDE_PROF=<file> (one chain): stamps of the first 64 steps' three launches, appended to
@@ -403,19 +617,45 @@ int sgld_wide_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
   double* llp;
   int64_t* d_noff = nullptr;
   unsigned long long* prof = nullptr;
+  T *snapW = nullptr, *snapb = nullptr, *snappW = nullptr, *snappb = nullptr;
+  const size_t nW = (size_t)D * C * K, nb = (size_t)C * K;
   do {
     ws.reset();
-    slab = ws.take<T>((size_t)S * C * B * KP);
+    slab = fuse ? nullptr : ws.take<T>((size_t)S * C * B * KP);
     diff = ws.take<T>((size_t)C * B * KP);
-    llp = ws.take<double>((size_t)C * nSB);
+    llp = ws.take<double>((size_t)C * std::max(nSB, nRB * S));
+    if (fuse) {                        // the call's start state, for the unfused re-run after a timeout
+      snapW = ws.take<T>(nW);
+      snapb = ws.take<T>(nb);
+      if (s->pW) { snappW = ws.take<T>(nW); snappb = ws.take<T>(nb); }
+    }
     if (buf) d_noff = ws.take<int64_t>(nsc);
     if (nprof) prof = ws.take<unsigned long long>((size_t)nprof * GALL * WPH);
   } while (ws.retry());
   if (ws.failed) return HMCX_ENOMEM;
   int rc;
+  unsigned ep0 = 0;
+  if (fuse) {
+    if ((rc = abort_precheck(ctx))) return rc;
+    unsigned nfwd = 0;
+    for (int i = 0; i < s->n_steps; ++i) nfwd += 1u + ((s->want_ll && s->want_ll[i] && s->out_ll) ? 1u : 0u);
+    if ((rc = gx_reserve(ctx, (size_t)nRB * S * C * WRB * K * 16))) return rc;
+    if ((rc = gx_epochs(ctx, nfwd, &ep0))) return rc;
+  }
   begin_call(ctx);
   if (buf && (rc = upload(ctx, d_noff, s->noise_off, nsc * sizeof(int64_t)))) return rc;
+  if (fuse) {
+    HMCX_HIP(ctx, hipMemcpyAsync(snapW, s->W, nW * sizeof(T), hipMemcpyDeviceToDevice, ctx->stream));
+    HMCX_HIP(ctx, hipMemcpyAsync(snapb, s->b, nb * sizeof(T), hipMemcpyDeviceToDevice, ctx->stream));
+    if (snappW) {
+      HMCX_HIP(ctx, hipMemcpyAsync(snappW, s->pW, nW * sizeof(T), hipMemcpyDeviceToDevice, ctx->stream));
+      HMCX_HIP(ctx, hipMemcpyAsync(snappb, s->pb, nb * sizeof(T), hipMemcpyDeviceToDevice, ctx->stream));
+    }
+  }
+  const int force_abort = getenv("HMCX_WIDE_FORCE_ABORT") ? atoi(getenv("HMCX_WIDE_FORCE_ABORT")) : -1;
   WideArgs<T> a{};
+  a.gx = ctx->gx_arena; a.gx_bytes = (int)std::min<size_t>(ctx->gx_bytes, 0x7fffffff);
+  a.abort_flag = ctx->abort_dev;
   a.W = (T*)s->W; a.b = (T*)s->b; a.pW = (T*)s->pW; a.pb = (T*)s->pb;
   a.B = B; a.D = D; a.K = K; a.KP = KP; a.S = S; a.Dz = Dz; a.nSB = nSB; a.C = C;
   a.slab = slab; a.diff = diff; a.llp = llp;
@@ -440,9 +680,16 @@ int sgld_wide_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
     a.want_diff = 1;
     unsigned long long* pr = i < nprof ? prof + (size_t)i * GALL * WPH : nullptr;
     a.prof = pr;
-    launch_fwd<T>(a, st);
-    a.prof = pr ? pr + (size_t)GF * WPH : nullptr;
-    hipLaunchKernelGGL(k_wsoft<T>, sgrid, dim3(WTH), 0, st, a);
+    if (fuse) {
+      a.ep = ep0++;
+      a.force_abort = i == force_abort;
+      launch_fwd_sm<T>(a, st);
+      a.force_abort = 0;
+    } else {
+      launch_fwd<T>(a, st);
+      a.prof = pr ? pr + (size_t)GF * WPH : nullptr;
+      hipLaunchKernelGGL(k_wsoft<T>, sgrid, dim3(WTH), 0, st, a);
+    }
     a.prof = pr ? pr + (size_t)(GF + GS) * WPH : nullptr;
     // one chain: 16 k-steps of loads per batch (one batch at B = 500, one workgroup per CU);
     // several chains: 8 per batch, so that two workgroups fit on a CU (C = 8 at config 5: 92.7 → see
@@ -458,14 +705,41 @@ int sgld_wide_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
     HMCX_HIP(ctx, hipGetLastError());
     if (s->want_ll && s->want_ll[i] && s->out_ll) {                   // sgmcmc.py:61 logging
       a.want_diff = 0;
-      launch_fwd<T>(a, st);
-      hipLaunchKernelGGL(k_wsoft<T>, sgrid, dim3(WTH), 0, st, a);
-      hipLaunchKernelGGL(k_wreduce_ll, dim3(C), dim3(256), 0, st, (const double*)llp, nSB, s->out_ll + (size_t)i * C);
+      if (fuse) {
+        a.ep = ep0++;
+        launch_fwd_sm<T>(a, st);
+        hipLaunchKernelGGL(k_wreduce_ll, dim3(C), dim3(256), 0, st, (const double*)llp, nRB * S,
+                           s->out_ll + (size_t)i * C);
+      } else {
+        launch_fwd<T>(a, st);
+        hipLaunchKernelGGL(k_wsoft<T>, sgrid, dim3(WTH), 0, st, a);
+        hipLaunchKernelGGL(k_wreduce_ll, dim3(C), dim3(256), 0, st, (const double*)llp, nSB, s->out_ll + (size_t)i * C);
+      }
       HMCX_HIP(ctx, hipGetLastError());
     }
   }
   if ((rc = gs.finish())) return rc;
   if ((rc = timing_end(ctx, ctx->stream))) return rc;
+  if (fuse) {
+    // a timed-out team round raised the abort word (the launch's workgroups then stopped early): put the
+    // call's start state back, lower the word and run the call again on the three-launch path — same
+    // operands, same noise, so the result is the one the fused call would have given
+    int flag = 0;
+    HMCX_HIP(ctx, hipMemcpyAsync(&flag, ctx->abort_dev, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    HMCX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (flag) {
+      HMCX_HIP(ctx, hipMemsetAsync(ctx->abort_dev, 0, sizeof(int), ctx->stream));
+      HMCX_HIP(ctx, hipMemcpyAsync(s->W, snapW, nW * sizeof(T), hipMemcpyDeviceToDevice, ctx->stream));
+      HMCX_HIP(ctx, hipMemcpyAsync(s->b, snapb, nb * sizeof(T), hipMemcpyDeviceToDevice, ctx->stream));
+      if (snappW) {
+        HMCX_HIP(ctx, hipMemcpyAsync(s->pW, snappW, nW * sizeof(T), hipMemcpyDeviceToDevice, ctx->stream));
+        HMCX_HIP(ctx, hipMemcpyAsync(s->pb, snappb, nb * sizeof(T), hipMemcpyDeviceToDevice, ctx->stream));
+      }
+      HMCX_HIP(ctx, hipStreamSynchronize(ctx->stream));     // the snapshot lives in the workspace
+      fprintf(stderr, "[hmcx] wide SGLD: a team round timed out; call re-run on the three-launch path\n");
+      return sgld_wide_impl<T>(ctx, s, false);
+    }
+  }
   if (nprof) {
     std::vector<unsigned long long> h((size_t)nprof * GALL * WPH);
     HMCX_HIP(ctx, hipStreamSynchronize(ctx->stream));

@@ -124,7 +124,7 @@ class sghmc(sgmcmc):
     def _call_template(self, Xd, Yd, W, b, batch_size, D, K, C):
         """hmcx_sampler_args fields that stay fixed from call to call (cached per data/state)."""
         key = (Xd.data_ptr(), Yd.data_ptr(), W.data_ptr(), b.data_ptr(), batch_size, C, self.path_length,
-               self.seed, self.chain)
+               self.seed, self.chain, self.model.alpha)
         tpl = self.__dict__.get('_tpl')
         if tpl is None or tpl[0] != key:
             a = nat.SamplerArgs()
@@ -146,18 +146,21 @@ class sghmc(sgmcmc):
         q = self.__dict__.get('_quick')
         if q is not None and not _HOST_PROF and self.noise == 'philox' and not self.record_steps \
                 and not self.__dict__.get('_want_mom'):
-            h = self._enqueue_quick(q, state, data, rows, eps)
+            h = self._enqueue_quick(q, state, data, rows, eps, batch_size)
             if h is not None:
                 return h
         return self._enqueue_full(state, data, rows, eps, rng, batch_size)
 
-    def _enqueue_quick(self, q, state, data, rows, eps):
+    def _enqueue_quick(self, q, state, data, rows, eps, batch_size):
         """The cached fast path of _enqueue_full (same struct, same host arrays, same slot rotation):
-        only valid when the data / state tensors and the step count are those the cache was made for."""
+        only valid when the data / state tensors, the step count and every sampler setting baked into
+        the cached argument struct (batch size, chains, path length, seed, chain id, alpha) are those the
+        cache was made for — anything else takes the full path, which rebuilds the struct."""
         n_steps = len(rows)
         W, b = state['weights'], state['bias']
         if (data[0] is not q['X'] or data[1] is not q['Y'] or W is not q['W'] or b is not q['b']
-                or self.trace is not None):
+                or self.trace is not None or q['tkey'][4:] != (batch_size, self.chains, self.path_length,
+                                                               self.seed, self.chain, self.model.alpha)):
             return None
         ring = self._io_ring
         i = self._io_next
@@ -229,7 +232,7 @@ class sghmc(sgmcmc):
             # offsets.  A miss rebuilds the caches of ALL slots at once, so the first call on each slot
             # (and a call with a new step count) costs no more than the others.
             tkey = (Xd.data_ptr(), Yd.data_ptr(), W.data_ptr(), b.data_ptr(), batch_size, C, self.path_length,
-                    self.seed, self.chain)
+                    self.seed, self.chain, self.model.alpha)
             ac = slot.get('acache')
             if ac is None or ac[0] != tkey or ac[1] is not slot['dev'] or n_steps > ac[6]:
                 cap = max(128, 1 << (n_steps - 1).bit_length())
@@ -310,8 +313,7 @@ class sghmc(sgmcmc):
         self.__dict__.setdefault('_inflight', []).append(h)
         if fast and C == 1 and out_steps is None and out_mom is None:
             self._quick = dict(X=Xd, Y=Yd, W=W, b=b, ctx=ctx,
-                               tkey=(Xd.data_ptr(), Yd.data_ptr(), W.data_ptr(), b.data_ptr(), batch_size, C,
-                                     self.path_length, self.seed, self.chain))
+                               tkey=tkey)
         return h
 
     def _collect(self, h):

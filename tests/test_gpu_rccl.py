@@ -83,3 +83,26 @@ def test_bench_self_launch_two_ranks_shared_gpu():
     line = json.loads(lines[0])
     assert line["n_gpus"] == 2 and line["config"]["chains"] == 2 and line["value"] > 0
     assert line["diagnostics"]["per_parameter"]["chains"] == 2
+
+
+def test_bench_four_ranks_shared_gpu_default_legs():
+    """the N > 1 path at the driver's settings — every secondary leg at its
+    default and rank 0 running CPU baselines while the other ranks wait in the closing barrier
+    (bench.py: all ranks tear the communicator / process group down together).  Four ranks share
+    cuda:0 over gloo; --path kernels, since four persistent single-chain kernels of 128 workgroups
+    each would oversubscribe one GPU's 256 CUs."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(HMCX_BENCH_SHARED_GPU="1", HMCX_DIST_BACKEND="gloo")
+    cmd = [sys.executable, "bench.py", "--gpus", "4", "--path", "kernels", "--steps", "20", "--warmup", "5",
+           "--cpu-seconds", "1"]
+    r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=420)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 4 and line["config"]["chains"] == 4 and line["value"] > 0
+    assert line["diagnostics"]["per_parameter"]["chains"] == 4
+    assert line["diagnostics"]["per_parameter"]["params"] == 7850
+    assert line["cpu_baseline"]["value"] > 0 and line["cpu_baseline"]["calibration_ratio"] > 0
+    for leg in ("chain_batched", "mlp", "plantvillage_sgld"):
+        assert line[leg] is not None and line[leg]["value"] > 0, leg

@@ -216,14 +216,17 @@ def test_sgld_wide_features_split_forward_vs_oracle(monkeypatch):
     np.testing.assert_allclose(logp_g, logp_r, rtol=1e-10)
 
 
+@pytest.mark.parametrize("fuse", ["1", "0"])
 @pytest.mark.parametrize("K,D,B", [(38, 2048, 500), (10, 131, 77), (64, 300, 40), (17, 8, 5), (38, 2000, 130)])
-def test_sgld_wide_path_vs_oracle(K, D, B, monkeypatch):
-    """The wide SGLD path (hmcx_wide.hip, three launches per step), forced here for every shape:
-    float64 trajectory within rel 1e-9 of the oracle, printed loss lines identical.  Covers BASELINE
-    config 5's shape (D=2048, K=38, B=500), a ragged shape (D not a multiple of the vector width,
-    partial row block), the largest class count, a D smaller than one MFMA k-step group, and ragged
-    row and feature blocks at config-5 width."""
+def test_sgld_wide_path_vs_oracle(K, D, B, fuse, monkeypatch):
+    """The wide SGLD path (hmcx_wide.hip), forced here for every shape, both as two launches per step
+    (fuse=1: forward + softmax fused by a team round, k_wfwd_sm) and as three (fuse=0: k_wfwd,
+    k_wsoft, k_wgrad): float64 trajectory within rel 1e-9 of the oracle, printed loss lines identical.
+    Covers BASELINE config 5's shape (D=2048, K=38, B=500), a ragged shape (D not a multiple of the
+    vector width, partial row block), the largest class count, a D smaller than one MFMA k-step group,
+    and ragged row and feature blocks at config-5 width."""
     monkeypatch.setenv("HMCX_SGLD_WIDE", "1")
+    monkeypatch.setenv("HMCX_WIDE_FUSE", fuse)
     c = dict(kind="sgld", N=2 * B, B=B, D=D, K=K, alpha=0.01, step_size=1e-4, path_length=1.0,
              burnin=1, epochs=2, data_seed=41, np_seed=2, rng_seed=3)
     post_r, logp_r, _, log_r = _run_oracle(c)
@@ -232,6 +235,23 @@ def test_sgld_wide_path_vs_oracle(K, D, B, monkeypatch):
         np.testing.assert_allclose(post_g[v], post_r[v], rtol=1e-9, atol=1e-12)
     np.testing.assert_allclose(logp_g, logp_r, rtol=1e-10)
     assert [l for l in log_g.splitlines() if "loss" in l] == [l for l in log_r.splitlines() if "loss" in l]
+
+
+def test_sgld_wide_fused_timeout_reruns_unfused(monkeypatch, capfd):
+    """A timed-out team round of the fused forward (forced: HMCX_WIDE_FORCE_ABORT=<step> raises the
+    abort word in that step's launch) makes the call put its start state back and run again on the
+    three-launch path: the trajectory is still the oracle's, and the re-run is reported on stderr."""
+    monkeypatch.setenv("HMCX_SGLD_WIDE", "1")
+    monkeypatch.setenv("HMCX_WIDE_FUSE", "1")
+    monkeypatch.setenv("HMCX_WIDE_FORCE_ABORT", "1")
+    c = dict(kind="sgld", N=1000, B=500, D=2048, K=38, alpha=0.01, step_size=1e-4, path_length=1.0,
+             burnin=1, epochs=2, data_seed=41, np_seed=2, rng_seed=3)
+    post_r, logp_r, _, _ = _run_oracle(c)
+    post_g, logp_g, _, _ = _run_gpu(c)
+    for v in ("weights", "bias"):
+        np.testing.assert_allclose(post_g[v], post_r[v], rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(logp_g, logp_r, rtol=1e-10)
+    assert "re-run on the three-launch path" in capfd.readouterr().err
 
 
 @pytest.mark.parametrize("dtype", ["f64", "f32"])
