@@ -594,6 +594,7 @@ def report(args, world, value, t_max, lf_total, lf_local, n_calls, kern_ms, kern
            batched, mlp_out, v_out, X, Y):
     """Rank 0: the JSON line (and the CPU baselines, after every rank's GPU work)."""
     from dropout_hamiltonian_montecarlo_amd import parallel
+    CHUNK = N_DATA // B                              # steps per call (one epoch), as in bench()
     path = "persistent" if (args.path != "kernels") else "kernels"
     assert kern_n == n_calls, (kern_n, n_calls)
     launch_ms = kern_ms / kern_n
