@@ -53,7 +53,6 @@ template <typename T> struct WideArgs {
   int wt;                                // slab / diff stored write-through (sc1; HMCX_WIDE_WT=0: plain)
   // fused forward + softmax (k_wfwd_sm): the row team's partial logits travel as tagged granules
   char* gx; int gx_bytes; unsigned ep;   // the context's granule arena and this launch's epoch
-  int gx_off;                            // k_wgrad_team: its region of the arena (after the forward's)
   int* abort_flag;                       // the context's sticky abort word (raised on a timed-out poll)
   int force_abort;                       // test knob (HMCX_WIDE_FORCE_ABORT): workgroup 0 raises the word
 };
@@ -215,11 +214,9 @@ __global__ __launch_bounds__(WTH) void k_wsoft(WideArgs<T> a) {
 // One softmax row (lane = class): Σ_z of the row's partials in slice order (the caller's sum), + b,
 // clip, softmax by wave reductions; the diff row (gradient pass) or the row's log-likelihood term.
 template <typename T>
-__device__ inline double wide_softmax_row(const WideArgs<T>& a, int ch, int row, int k, T xw) {
+__device__ inline double wide_softmax_row(const WideArgs<T>& a, int ch, int row, int k, T xw, T bk, T yk) {
   const int K = a.K;
   const bool kv = k < K;
-  const int kc = min(k, K - 1);
-  const T bk = a.b[ch * K + kc], yk = a.Y[(size_t)row * K + kc];                          // unconditional loads
   const T zz = kv ? clipz(xw + bk, a.clip_hi, a.clip_lo) : (T)-__builtin_inf();            // softmax.py:39-41
   const T m = wave_max(zz);
   const T e = kv ? exp(zz - m) : T(0);                                                    // softmax.py:34
@@ -232,6 +229,13 @@ __device__ inline double wide_softmax_row(const WideArgs<T>& a, int ch, int row,
   }
   const T lse = log(s) + m;                                                               // softmax.py:18-20
   return wave_sum(kv ? (double)(y * (zz - lse)) : 0.0);
+}
+
+template <typename T> __device__ inline T wide_ld(__amdgpu_buffer_rsrc_t rs, int off) {
+  if constexpr (sizeof(T) == 8)
+    return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0));
+  else
+    return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
 }
 
 // ---------------------------------------------------------------- fused forward + softmax
@@ -254,36 +258,40 @@ __global__ __launch_bounds__(WTH) void k_wfwd_sm(WideArgs<T> a) {
   const int m0 = blockIdx.x * WRB, z = blockIdx.y, ch = blockIdx.z;
   const int dlo = min(a.D, z * a.Dz), dhi = min(a.D, dlo + a.Dz);
   const int nrow = min(WRB, a.B - m0), K = a.K, NW = a.C * K, S = a.S;
-  const T* Wc = a.W + (size_t)ch * K;
   WSTAMP(0);
   if (tid == 0) fail = 0;
   const int f0 = dlo + 32 * wave + 8 * lg;
-  const int fsafe = dlo < a.D ? dlo : 0;
+  // operands by buffer loads issued k-step by k-step: an element outside the tile (row past the
+  // minibatch, feature past the slice, class past K) gets an out-of-range offset and reads 0 with no
+  // memory request, so nothing is masked after the batch and the MFMAs of step j wait only for the
+  // loads of steps ≤ j (the loads of the later steps are still landing)
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<T*>(a.X) + (size_t)m0 * a.D, 0, nrow * a.D * (int)sizeof(T), 0x00020000);
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+      a.W + (size_t)ch * K, 0, (a.D * NW - ch * K) * (int)sizeof(T), 0x00020000);
+  constexpr int OOB = 0x7fffffff;
   T xa[2][8], wb[8][KB];
 #pragma unroll
-  for (int mt = 0; mt < 2; ++mt) {
-    const int i = mt * 16 + lr;
-    const T* xr = a.X + (size_t)m0 * a.D + (size_t)(i < nrow ? i : 0) * a.D;
+  for (int j = 0; j < 8; ++j) {
+    const bool fok = f0 + j < dhi;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) xa[mt][j] = xr[f0 + j < dhi ? f0 + j : fsafe];
-  }
-#pragma unroll
-  for (int j = 0; j < 8; ++j)
+    for (int mt = 0; mt < 2; ++mt) {
+      const int off = fok ? ((mt * 16 + lr) * a.D + f0 + j) * (int)sizeof(T) : OOB;
+      xa[mt][j] = wide_ld<T>(xrs, off);
+    }
 #pragma unroll
     for (int nb = 0; nb < KB; ++nb) {
       const int c = nb * 16 + lr;
-      wb[j][nb] = Wc[(f0 + j < dhi && c < K) ? (size_t)(f0 + j) * NW + c : 0];
+      const int off = (fok && c < K) ? ((f0 + j) * NW + c) * (int)sizeof(T) : OOB;
+      wb[j][nb] = wide_ld<T>(wrs, off);
     }
-#pragma unroll
-  for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      if (!(mt * 16 + lr < nrow && f0 + j < dhi)) xa[mt][j] = T(0);
-#pragma unroll
-  for (int j = 0; j < 8; ++j)
-#pragma unroll
-    for (int nb = 0; nb < KB; ++nb)
-      if (!(f0 + j < dhi && nb * 16 + lr < K)) wb[j][nb] = T(0);
+  }
+  // softmax operands of this wave's first owned row (b and the labels), loaded while the partials travel
+  const int R = (WRB + S - 1) / S;
+  const int r0 = min(nrow, z * R), r1 = min(nrow, r0 + R);
+  const int kc = min(lane, K - 1);
+  const T bk = a.b[ch * K + kc];
+  const T yk0 = a.Y[(size_t)(m0 + min(r0 + wave, nrow - 1)) * K + kc];
   WSTAMP(1);
   typename M::acc_t acc[2][KB];
 #pragma unroll
@@ -319,8 +327,6 @@ __global__ __launch_bounds__(WTH) void k_wfwd_sm(WideArgs<T> a) {
     __hip_atomic_store(a.abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   WSTAMP(3);
   // gather my rows' partials from the S producers: pair q = p·nit + it, it = row-in-slice·K + class
-  const int R = (WRB + S - 1) / S;
-  const int r0 = min(nrow, z * R), r1 = min(nrow, r0 + R);
   const int nit = (r1 - r0) * K, npair = S * nit;
   {
     typedef unsigned int g4 __attribute__((ext_vector_type(4)));
@@ -364,11 +370,20 @@ __global__ __launch_bounds__(WTH) void k_wfwd_sm(WideArgs<T> a) {
   if (fail) return;                    // the host sees the abort word and re-runs the call unfused
   double t = 0.0;
   for (int row = r0 + wave; row < r1; row += 4) {
-    const int kc = min(lane, K - 1);
     const int ri = (row - r0) * K + kc;
     T xw = (T)stage[ri];
-    for (int p = 1; p < S; ++p) xw = xw + (T)stage[p * nit + ri];          // k_wsoft's slab order
-    t += wide_softmax_row(a, ch, m0 + row, lane, xw);
+    // Σ over the S slices in slice order (k_wsoft's slab order), the LDS reads of 16 slices at a time
+    // issued together (a runtime-length loop waited for each read before the next add)
+    for (int p0 = 1; p0 < S; p0 += 16) {
+      double v[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) v[q] = stage[min(p0 + q, S - 1) * nit + ri];
+#pragma unroll
+      for (int q = 0; q < 16; ++q)
+        if (p0 + q < S) xw = xw + (T)v[q];
+    }
+    const T yk = row == r0 + wave ? yk0 : a.Y[(size_t)(m0 + row) * K + kc];
+    t += wide_softmax_row(a, ch, m0 + row, lane, xw, bk, yk);
   }
   WSTAMP(5);
   if (!a.want_diff) {                  // the logging pass: ll partial of my rows (waves in order)
@@ -516,204 +531,6 @@ __global__ __launch_bounds__(GTH) void k_wgrad(WideArgs<T> a) {
   WSTAMP(5);
 }
 
-// ---------------------------------------------------------------- Xᵀ·diff by row-slice teams
-// k_wgrad reads, per workgroup, its 16 features' X columns AND all 500 diff rows of its class group
-// (≈140 KB per CU at config 5: the launch waits on its loads).  Here a workgroup takes a 32-feature
-// tile × ALL classes over one quarter of the minibatch rows (≈70 KB per CU at config 5: 64 tiles × 4
-// row slices = 256 workgroups); the four row-slice workgroups of a tile (a team, placed on one XCD)
-// publish their partial Xᵀ·diff and diff column sums as tagged granules, and member r owns features
-// [8r, 8r + 8) of the tile: it sums the four partials in slice order and applies the SGLD update;
-// member 0 of tile 0 also owns the biases.  The grid must be co-resident (checked on the host).
-constexpr int WTF = 32;                  // features per tile
-constexpr int WTR = 4;                   // row slices per tile (team size)
-template <typename T, int NT>
-__global__ __launch_bounds__(WTH) void k_wgrad_team(WideArgs<T> a) {
-  using M = mfma16<T>;
-  constexpr int NC = NT * 16;
-  __shared__ T red[4][WTF][NC + 1];
-  __shared__ T cs[4][NC];
-  __shared__ double stage[8 * WTH];
-  __shared__ int fail;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lg = lane >> 4;
-  const int ch = blockIdx.y;
-  // XCD-grouped team placement: blocks b, b + 8, b + 16, b + 24 (one XCD) are the team of tile t
-  const int bx = blockIdx.x, x8 = bx & 7, sx = bx >> 3, r = sx % WTR, t = (sx / WTR) * 8 + x8;
-  const int nft = (a.D + WTF - 1) / WTF;
-  if (t >= nft) return;                                        // padding of the XCD grouping
-  WSTAMP(0);
-  if (tid == 0) fail = 0;
-  const int K = a.K, B = a.B, KP = a.KP, NW = a.C * K, d0 = t * WTF;
-  const int nks = (B + 3) / 4, kps = (nks + WTR - 1) / WTR;      // k-steps (4 rows) per row slice
-  const int ks0 = r * kps, ks1 = min(nks, ks0 + kps);
-  const int kpw = (kps + 3) / 4;                                  // k-steps per wave
-  const int kw0 = ks0 + wave * kpw, kw1 = min(ks1, kw0 + kpw);
-  const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(
-      a.diff + (size_t)ch * B * KP, 0, B * KP * (int)sizeof(T), 0x00020000);
-  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<T*>(a.X), 0, B * a.D * (int)sizeof(T), 0x00020000);
-  // owned elements (feature 8r + e / K of the tile, class e % K) and, for member 0 of tile 0, the biases
-  const int nown = max(0, min(8, a.D - (d0 + 8 * r))) * K;
-  const bool bown = t == 0 && r == 0;
-  const int nall = nown + (bown ? K : 0);
-  const bool gpu_var = a.pW != nullptr;
-  const T* psrc = gpu_var ? a.pW : a.W;
-  // epilogue operands and the noise of my (at most 2) owned elements, drawn while the loads fly
-  T wv[2], pv[2], zv[2];
-  size_t wi[2];
-  int bi[2];
-  typename M::acc_t acc[2][NT];
-  T csum[NT];
-#pragma unroll
-  for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-    for (int j = 0; j < NT; ++j) acc[mt][j] = M::zero();
-#pragma unroll
-  for (int j = 0; j < NT; ++j) csum[j] = T(0);
-  constexpr int U = 8;                                           // k-steps of loads in flight per batch
-  bool first = true;
-  for (int ks = kw0; ks < kw1 || first; ks += U) {
-    T av[U][2], bv[U][NT];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int row = (ks + u) * 4 + lg;
-      const bool ok = ks + u < kw1 && row < B;
-#pragma unroll
-      for (int mt = 0; mt < 2; ++mt) {
-        const int f = d0 + mt * 16 + lr;
-        const int off = (ok && f < a.D) ? (row * a.D + f) * (int)sizeof(T) : 0x7fffffff;
-        if constexpr (sizeof(T) == 8)
-          av[u][mt] = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(xrs, off, 0, 0));
-        else
-          av[u][mt] = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(xrs, off, 0, 0));
-      }
-#pragma unroll
-      for (int j = 0; j < NT; ++j) {
-        const int off = (ok && j * 16 + lr < K) ? (row * KP + j * 16 + lr) * (int)sizeof(T) : 0x7fffffff;
-        if constexpr (sizeof(T) == 8)
-          bv[u][j] = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(drs, off, 0, 0));
-        else
-          bv[u][j] = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(drs, off, 0, 0));
-      }
-    }
-    if (first) {
-      first = false;
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const int e = tid + q * WTH;
-        const bool isw = e < nown, isb = !isw && e < nall;
-        const int fi = d0 + 8 * r + (isw ? e / K : 0), k = isw ? e - (e / K) * K : (isb ? e - nown : 0);
-        wi[q] = isw ? (size_t)fi * NW + (size_t)ch * K + k : 0;
-        bi[q] = ch * K + k;
-        wv[q] = isb ? a.b[bi[q]] : a.W[wi[q]];
-        pv[q] = gpu_var ? (isb ? a.pb[bi[q]] : psrc[wi[q]]) : T(0);
-        zv[q] = (isw || isb) ? (T)wide_noise(a, ch, isw ? (uint32_t)(fi * K + k) : (uint32_t)(a.D * K + k)) : T(0);
-      }
-      WSTAMP(1);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-      for (int j = 0; j < NT; ++j) {
-        acc[0][j] = M::fma(av[u][0], bv[u][j], acc[0][j]);
-        acc[1][j] = M::fma(av[u][1], bv[u][j], acc[1][j]);
-        csum[j] += bv[u][j];
-      }
-  }
-  WSTAMP(2);
-#pragma unroll
-  for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-    for (int j = 0; j < NT; ++j)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) red[wave][mt * 16 + M::row(lane, q)][j * 16 + lr] = acc[mt][j][q];
-#pragma unroll
-  for (int j = 0; j < NT; ++j) {
-    T v = csum[j];
-    v += __shfl_xor(v, 16, 64);
-    v += __shfl_xor(v, 32, 64);
-    if (lg == 0) cs[wave][j * 16 + lr] = v;
-  }
-  __syncthreads();
-  // publish this slice's partial: [32 features][K] then the K column sums (waves summed in order)
-  const __amdgpu_buffer_rsrc_t rs = gx_rsrc(a.gx + a.gx_off, a.gx_bytes - a.gx_off);
-  const int blk = WTF * K + K;
-  const int team = (ch * ((nft + 7) / 8 * 8) + t) * WTR;           // first producer block of my team
-  for (int e = tid; e < blk; e += WTH) {
-    T v;
-    if (e < WTF * K) {
-      const int fi = e / K, k = e - (e / K) * K;
-      v = ((red[0][fi][k] + red[1][fi][k]) + red[2][fi][k]) + red[3][fi][k];
-    } else {
-      const int k = e - WTF * K;
-      v = ((cs[0][k] + cs[1][k]) + cs[2][k]) + cs[3][k];
-    }
-    gx_put(rs, (team + r) * blk + e, (double)v, a.ep);
-  }
-  WSTAMP(3);
-  // gather my owned elements' four partials: pair q = p·nall + e
-  {
-    typedef unsigned int g4 __attribute__((ext_vector_type(4)));
-    constexpr int UG = 8;
-    const int npair = WTR * nall;
-    unsigned pend = 0;
-    int o[UG];
-#pragma unroll
-    for (int u = 0; u < UG; ++u) {
-      const int q = tid + u * WTH;
-      const int p = q / max(nall, 1), e = q - p * max(nall, 1);
-      const bool w = q < npair;
-      const int src = e < nown ? (8 * r + e / K) * K + (e - (e / K) * K) : WTF * K + (e - nown);
-      pend |= w ? 1u << u : 0u;
-      o[u] = w ? ((team + p) * blk + src) * 16 : 0;
-    }
-    unsigned long long t0 = 0;
-    bool ok = true;
-    for (int spins = 0; pend; ++spins) {
-      g4 v[UG];
-#pragma unroll
-      for (int u = 0; u < UG; ++u) v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, o[u], 0, 16 /* sc1 */);
-#pragma unroll
-      for (int u = 0; u < UG; ++u)
-        if (((pend >> u) & 1u) && v[u].y == a.ep && v[u].w == a.ep) {
-          stage[tid + u * WTH] = __builtin_bit_cast(double, (unsigned long long)v[u].x | ((unsigned long long)v[u].z << 32));
-          pend &= ~(1u << u);
-        }
-      if (!pend) break;
-      if (spins == 0) t0 = __builtin_amdgcn_s_memrealtime();
-      if ((spins & 63) == 63 && (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull ||
-                                 __hip_atomic_load(a.abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
-        __hip_atomic_store(a.abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ok = false;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-    if (!ok) fail = 1;
-  }
-  __syncthreads();
-  WSTAMP(4);
-  if (fail) return;
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int e = tid + q * WTH;
-    if (e >= nall) continue;
-    T dot = (T)stage[e];
-#pragma unroll
-    for (int p = 1; p < WTR; ++p) dot += (T)stage[p * nall + e];                 // row-slice order
-    T pn = a.noise_scale * zv[q];                                                 // sgld.py:43-46
-    if (gpu_var) pn = pn * pv[q];                                                 // gpu/sgld.py:18
-    pn = pn + a.m_half_eps * (-(dot - a.alpha * wv[q]));                          // softmax.py:55-60, sgld.py:37
-    if (e < nown) {
-      if (gpu_var) a.pW[wi[q]] = pn;
-      a.W[wi[q]] = wv[q] + pn;                                                    // sgld.py:38
-    } else {
-      if (gpu_var) a.pb[bi[q]] = pn;
-      a.b[bi[q]] = wv[q] + pn;
-    }
-  }
-  WSTAMP(5);
-}
-
 __global__ void k_wreduce_ll(const double* llp, int n, double* out) {   // block = chain
   __shared__ double sh[256];
   const double* p = llp + (size_t)blockIdx.x * n;
@@ -778,26 +595,6 @@ static const void* fwd_sm_fn(int KP) {
 }
 
 template <typename T>
-static const void* gteam_fn(int KP) {
-  switch (KP / 16) {
-    case 1: return (const void*)k_wgrad_team<T, 1>;
-    case 2: return (const void*)k_wgrad_team<T, 2>;
-    case 3: return (const void*)k_wgrad_team<T, 3>;
-    default: return (const void*)k_wgrad_team<T, 4>;
-  }
-}
-template <typename T>
-static void launch_gteam(const WideArgs<T>& a, int nftp, hipStream_t st) {
-  const dim3 grid((unsigned)(nftp * WTR), (unsigned)a.C);
-  switch (a.KP / 16) {
-    case 1: hipLaunchKernelGGL((k_wgrad_team<T, 1>), grid, dim3(WTH), 0, st, a); break;
-    case 2: hipLaunchKernelGGL((k_wgrad_team<T, 2>), grid, dim3(WTH), 0, st, a); break;
-    case 3: hipLaunchKernelGGL((k_wgrad_team<T, 3>), grid, dim3(WTH), 0, st, a); break;
-    default: hipLaunchKernelGGL((k_wgrad_team<T, 4>), grid, dim3(WTH), 0, st, a); break;
-  }
-}
-
-template <typename T>
 static int sgld_wide_impl(hmcx_ctx* ctx, const hmcx_sampler_args* s, bool allow_fuse);
 
 template <typename T>
@@ -811,6 +608,8 @@ static int sgld_wide_impl(hmcx_ctx* ctx, const hmcx_sampler_args* s, bool allow_
   const int S = (D + WDZ - 1) / WDZ, Dz = ((D + S - 1) / S + 3) / 4 * 4;
   const int nSB = (B + WSR - 1) / WSR;
   const int nRB = (B + WRB - 1) / WRB;
+  const int ntile = (D + 15) / 16;
+  const size_t nsc = (size_t)s->n_steps * C;
   // fused forward + softmax (k_wfwd_sm: one team round instead of k_wsoft and a kernel boundary) when
   // the whole forward grid is co-resident and a workgroup's gathered partials fit its LDS stage;
   // HMCX_WIDE_FUSE=0 keeps the three launches
@@ -821,24 +620,11 @@ static int sgld_wide_impl(hmcx_ctx* ctx, const hmcx_sampler_args* s, bool allow_
     if (rc0) return rc0;
     fuse = (long)per_cu * ctx->num_cus >= (long)nRB * S * C;
   }
-  // the gradient by row-slice teams (k_wgrad_team) rides on the same co-residency and recovery;
-  // HMCX_WIDE_GTEAM=0 keeps k_wgrad
-  const int nft = (D + WTF - 1) / WTF, nftp = (nft + 7) / 8 * 8;
-  const int gteam_env = getenv("HMCX_WIDE_GTEAM") ? atoi(getenv("HMCX_WIDE_GTEAM")) : 1;
-  bool gteam = fuse && gteam_env != 0 && K <= 56;
-  if (gteam) {
-    int per_cu = 0, rc0 = kernel_occupancy(ctx, gteam_fn<T>(KP), WTH, 0, &per_cu);
-    if (rc0) return rc0;
-    gteam = (long)per_cu * ctx->num_cus >= (long)nftp * WTR * C;
-  }
-  const int ntile = (D + 15) / 16;
-  const size_t nsc = (size_t)s->n_steps * C;
-  // HMCX_WIDE_PROF=<file> (one chain): stamps of the first 64 steps' three launches, appended to
-  // <file> after the call (header: steps, workgroups of k_wfwd, k_wsoft, k_wgrad, WPH;
-  // tools/wide_prof_summary.py)
+  // HMCX_WIDE_PROF=<file> (one chain): stamps of the first 64 steps' launches, appended to <file> after
+  // the call (header: steps, workgroups of k_wfwd(_sm), k_wsoft, k_wgrad, WPH; tools/wide_prof_summary.py)
   static const char* prof_path = getenv("HMCX_WIDE_PROF");
   const WGroups wg = wide_groups(K);
-  const int GF = ((B + WRB - 1) / WRB) * S, GS = nSB, GG = std::max(wg.G * ntile, gteam ? nftp * WTR : 0), GALL = GF + GS + GG;
+  const int GF = nRB * S, GS = nSB, GG = wg.G * ntile, GALL = GF + GS + GG;
   const int nprof = (prof_path && C == 1) ? std::min(s->n_steps, 64) : 0;
   const bool buf = s->noise_mode == HMCX_NOISE_BUFFER;
   Workspace ws(ctx);
@@ -864,15 +650,11 @@ static int sgld_wide_impl(hmcx_ctx* ctx, const hmcx_sampler_args* s, bool allow_
   if (ws.failed) return HMCX_ENOMEM;
   int rc;
   unsigned ep0 = 0;
-  size_t gx_fwd = 0;
   if (fuse) {
     if ((rc = abort_precheck(ctx))) return rc;
     unsigned nfwd = 0;
     for (int i = 0; i < s->n_steps; ++i) nfwd += 1u + ((s->want_ll && s->want_ll[i] && s->out_ll) ? 1u : 0u);
-    if (gteam) nfwd += (unsigned)s->n_steps;
-    gx_fwd = (size_t)nRB * S * C * WRB * K * 16;
-    const size_t gx_grad = gteam ? (size_t)C * nftp * WTR * (WTF * K + K) * 16 : 0;
-    if ((rc = gx_reserve(ctx, gx_fwd + gx_grad))) return rc;
+    if ((rc = gx_reserve(ctx, (size_t)nRB * S * C * WRB * K * 16))) return rc;
     if ((rc = gx_epochs(ctx, nfwd, &ep0))) return rc;
   }
   begin_call(ctx);
@@ -888,7 +670,6 @@ static int sgld_wide_impl(hmcx_ctx* ctx, const hmcx_sampler_args* s, bool allow_
   const int force_abort = getenv("HMCX_WIDE_FORCE_ABORT") ? atoi(getenv("HMCX_WIDE_FORCE_ABORT")) : -1;
   WideArgs<T> a{};
   a.gx = ctx->gx_arena; a.gx_bytes = (int)std::min<size_t>(ctx->gx_bytes, 0x7fffffff);
-  a.gx_off = (int)gx_fwd;
   a.abort_flag = ctx->abort_dev;
   a.W = (T*)s->W; a.b = (T*)s->b; a.pW = (T*)s->pW; a.pb = (T*)s->pb;
   a.B = B; a.D = D; a.K = K; a.KP = KP; a.S = S; a.Dz = Dz; a.nSB = nSB; a.C = C;
@@ -928,10 +709,7 @@ static int sgld_wide_impl(hmcx_ctx* ctx, const hmcx_sampler_args* s, bool allow_
     // one chain: 16 k-steps of loads per batch (one batch at B = 500, one workgroup per CU);
     // several chains: 8 per batch, so that two workgroups fit on a CU (C = 8 at config 5: 92.7 → see
     // DESIGN §5.4)
-    if (gteam) {
-      a.ep = ep0++;
-      launch_gteam<T>(a, nftp, st);
-    } else if (wg.NT == 1) {
+    if (wg.NT == 1) {
       if (C == 1) hipLaunchKernelGGL((k_wgrad<T, 1, 16>), ggrid, dim3(GTH), 0, st, a);
       else hipLaunchKernelGGL((k_wgrad<T, 1, 8>), ggrid, dim3(GTH), 0, st, a);
     } else {

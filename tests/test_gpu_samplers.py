@@ -216,19 +216,17 @@ def test_sgld_wide_features_split_forward_vs_oracle(monkeypatch):
     np.testing.assert_allclose(logp_g, logp_r, rtol=1e-10)
 
 
-@pytest.mark.parametrize("fuse,gteam", [("1", "1"), ("1", "0"), ("0", "0")])
+@pytest.mark.parametrize("fuse", ["1", "0"])
 @pytest.mark.parametrize("K,D,B", [(38, 2048, 500), (10, 131, 77), (64, 300, 40), (17, 8, 5), (38, 2000, 130)])
-def test_sgld_wide_path_vs_oracle(K, D, B, fuse, gteam, monkeypatch):
+def test_sgld_wide_path_vs_oracle(K, D, B, fuse, monkeypatch):
     """The wide SGLD path (hmcx_wide.hip), forced here for every shape, as two launches per step
-    (fuse=1: forward + softmax fused by a team round, k_wfwd_sm; gteam=1: the gradient by row-slice
-    teams, k_wgrad_team, where K ≤ 56) or three (fuse=0: k_wfwd, k_wsoft, k_wgrad): float64
-    trajectory within rel 1e-9 of the oracle, printed loss lines identical.
+    (fuse=1: forward + softmax fused by a team round, k_wfwd_sm) or three (fuse=0: k_wfwd, k_wsoft,
+    k_wgrad): float64 trajectory within rel 1e-9 of the oracle, printed loss lines identical.
     Covers BASELINE config 5's shape (D=2048, K=38, B=500), a ragged shape (D not a multiple of the
     vector width, partial row block), the largest class count, a D smaller than one MFMA k-step group,
     and ragged row and feature blocks at config-5 width."""
     monkeypatch.setenv("HMCX_SGLD_WIDE", "1")
     monkeypatch.setenv("HMCX_WIDE_FUSE", fuse)
-    monkeypatch.setenv("HMCX_WIDE_GTEAM", gteam)
     c = dict(kind="sgld", N=2 * B, B=B, D=D, K=K, alpha=0.01, step_size=1e-4, path_length=1.0,
              burnin=1, epochs=2, data_seed=41, np_seed=2, rng_seed=3)
     post_r, logp_r, _, log_r = _run_oracle(c)
