@@ -3,6 +3,7 @@
 #include "hmcx_common.h"
 #include "hmcx_internal.h"
 #include <new>
+#include <cstdio>
 #include <cstring>
 #include <cmath>
 
@@ -473,7 +474,9 @@ int hmcx_create(int device, hmcx_ctx** out) {
     return HMCX_EHIP;
   }
   c->stream = c->own_stream;
-  if (hipMalloc((void**)&c->abort_dev, sizeof(int)) != hipSuccess || hipMemset(c->abort_dev, 0, sizeof(int)) != hipSuccess) {
+  // the abort word and, after it, where the first timeout happened (hmcx_p2x.h p2_timeout)
+  if (hipMalloc((void**)&c->abort_dev, ABORT_WORDS * sizeof(int)) != hipSuccess ||
+      hipMemset(c->abort_dev, 0, ABORT_WORDS * sizeof(int)) != hipSuccess) {
     delete c;
     return HMCX_EHIP;
   }
@@ -544,7 +547,15 @@ int hmcx_clear_abort(hmcx_ctx* ctx) {
   HMCX_GUARD_CTX(ctx);
   for (auto& pr : ctx->abort_pend) ctx->ev_pool.push_back(pr.first);
   ctx->abort_pend.clear();
-  HMCX_HIP(ctx, hipMemsetAsync(ctx->abort_dev, 0, sizeof(int), ctx->stream));
+  static const bool dbg = getenv("HMCX_P2_DEBUG") && getenv("HMCX_P2_DEBUG")[0] == '1';
+  if (dbg) {                                        // where the first timeout happened
+    int w[ABORT_WORDS];
+    HMCX_HIP(ctx, hipMemcpyAsync(w, ctx->abort_dev, sizeof(w), hipMemcpyDeviceToHost, ctx->stream));
+    HMCX_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    fprintf(stderr, "[hmcx] abort word %d; first timeout: workgroup %d, granule base %d, epoch %d\n", w[0], w[1] - 1,
+            w[2], w[3]);
+  }
+  HMCX_HIP(ctx, hipMemsetAsync(ctx->abort_dev, 0, ABORT_WORDS * sizeof(int), ctx->stream));
   return HMCX_OK;
 }
 

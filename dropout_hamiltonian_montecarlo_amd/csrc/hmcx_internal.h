@@ -64,6 +64,7 @@ struct hmcx_ctx {
   int mlp_nofuse = 0;                  // hmcx_set_mlp_fuse(ctx, 0): the sampler runs unfused
 };
 constexpr int ABORT_SLOTS = 64;
+constexpr int ABORT_WORDS = 4;       // abort_dev: the word, then workgroup / granule base / epoch of the first timeout
 
 namespace hmcx {
 

@@ -54,6 +54,28 @@ __device__ inline double decode(gran_t w) {
   return __builtin_bit_cast(double, (unsigned long long)w.x | ((unsigned long long)w.z << 32));
 }
 
+// A timed-out poll raises the sticky abort word; the first timeout also records where it happened
+// (abort_flag[1] = workgroup + 1, [2] = the round's granule base, [3] = its epoch) for diagnosis
+// (hmcx_clear_abort prints them under HMCX_P2_DEBUG=1).  A poll that sees the word already raised
+// only leaves.
+__device__ inline void p2_timeout(int* abort_flag, int where, unsigned ep) {
+  int z = 0;
+  if (__hip_atomic_compare_exchange_strong(abort_flag + 1, &z, (int)blockIdx.x + 1, __ATOMIC_RELAXED,
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+    __hip_atomic_store(abort_flag + 2, where, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(abort_flag + 3, (int)ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __hip_atomic_store(abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline bool p2_spin_over(unsigned long long t0, int* abort_flag, int where, unsigned ep) {
+  if (__builtin_amdgcn_s_memrealtime() - t0 > QTIMEOUT) {
+    p2_timeout(abort_flag, where, ep);
+    return true;
+  }
+  if (__hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return true;
+  return false;
+}
+
 // Polls one granule per producer p < np (p != pskip) at base0 + p·pstride + off until both epoch
 // words match.  Loads go out unpredicated in one batch of 8·NB (absent producers clamped to a
 // valid address and ignored); a pass re-reads the batch while any granule is missing.
@@ -86,12 +108,7 @@ __device__ inline bool poll_nb(__amdgpu_buffer_rsrc_t rs, int base0, int pstride
       }
     if (!pend) break;
     if (spins == 0) t0 = __builtin_amdgcn_s_memrealtime();
-    if ((spins & 63) == 63 &&
-        (__builtin_amdgcn_s_memrealtime() - t0 > QTIMEOUT ||
-         __hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
-      __hip_atomic_store(abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return false;
-    }
+    if ((spins & 63) == 63 && p2_spin_over(t0, abort_flag, base0, ep)) return false;
     if (HMCX_P2_SLEEP) __builtin_amdgcn_s_sleep(1);
   }
   if (!valid) return true;
@@ -156,12 +173,7 @@ __device__ inline bool polln_nb(__amdgpu_buffer_rsrc_t rs, int base0, int pstrid
       }
     if (!pend) break;
     if (spins == 0) t0 = __builtin_amdgcn_s_memrealtime();
-    if ((spins & 63) == 63 &&
-        (__builtin_amdgcn_s_memrealtime() - t0 > QTIMEOUT ||
-         __hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
-      __hip_atomic_store(abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return false;
-    }
+    if ((spins & 63) == 63 && p2_spin_over(t0, abort_flag, base0, ep)) return false;
     if (HMCX_P2_SLEEP) __builtin_amdgcn_s_sleep(1);
   }
   if (!worked) work();
@@ -216,12 +228,7 @@ __device__ inline bool gather_u(__amdgpu_buffer_rsrc_t rs, int base0, int pstrid
       }
     if (!pend) break;
     if (spins == 0) t0 = __builtin_amdgcn_s_memrealtime();
-    if ((spins & 63) == 63 &&
-        (__builtin_amdgcn_s_memrealtime() - t0 > QTIMEOUT ||
-         __hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
-      __hip_atomic_store(abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return false;
-    }
+    if ((spins & 63) == 63 && p2_spin_over(t0, abort_flag, base0, ep)) return false;
     if (HMCX_P2_SLEEP) __builtin_amdgcn_s_sleep(1);
   }
   return true;
@@ -256,12 +263,7 @@ __device__ inline bool gather_st_u(__amdgpu_buffer_rsrc_t rs, int base0, int pst
       }
     if (!pend) break;
     if (spins == 0) t0 = __builtin_amdgcn_s_memrealtime();
-    if ((spins & 63) == 63 &&
-        (__builtin_amdgcn_s_memrealtime() - t0 > QTIMEOUT ||
-         __hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
-      __hip_atomic_store(abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return false;
-    }
+    if ((spins & 63) == 63 && p2_spin_over(t0, abort_flag, base0, ep)) return false;
     if (HMCX_P2_SLEEP) __builtin_amdgcn_s_sleep(1);
   }
   return true;
@@ -309,9 +311,7 @@ __device__ inline int p2_wait_decision(unsigned long long* w, unsigned ep, int* 
   for (int spins = 0;; ++spins) {
     const unsigned long long cur = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if ((cur >> 2) == (unsigned long long)ep) return (int)(cur & 3ull);
-    if ((spins & 63) == 63 &&
-        (__builtin_amdgcn_s_memrealtime() - t0 > QTIMEOUT ||
-         __hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+    if ((spins & 63) == 63 && p2_spin_over(t0, abort_flag, -1, ep)) {
       const int d = p2_decide(w, ep, P2_ABORT);
       if (d == P2_ABORT) __hip_atomic_store(abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return d;

@@ -301,8 +301,12 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
   double* stg = reinterpret_cast<double*>(profacc + 16);                             // [QSTAGE] spread gathers
   T* zbuf = reinterpret_cast<T*>(stg + QSTAGE);                                      // [Fo·KC + 16] noise
   T* pWs = zbuf + Fo * 16 + 16;                       // [BfP][16] momentum of the whole slice (bar)
-  // friction noise by the waves that do not poll A-RS (threads from NZ0 on), when they fit
-  const int NZ0 = ((nro * KC + 63) / 64) * 64;
+  // friction noise by the waves that do not poll A-RS (threads from NZ0 on), when they fit.  NZ0 comes
+  // from the plan's Ro, not this member's nro: zoff decides `bar`, the protocol of round B, which every
+  // workgroup must agree on — with a per-member nro, a member owning no rows (B = 40, D = 32: plan 2x2,
+  // rows 32-39 in row team 1) chose the all-reduce while its team ran RS + AG, and the launch waited out
+  // its 4 s timeout before the recovery re-ran it
+  const int NZ0 = ((Ro * KC + 63) / 64) * 64;
   const bool zoff = zoffa && !(spread & 1) && NZ0 + Fo * KC + K <= QTH;
   // B all-reduce (bara) needs the owners' noise in LDS (zoff) to fold it into their partials
   const bool bar = bara && zoff;
@@ -1023,6 +1027,11 @@ int sghmc_p2_t(hmcx_ctx* ctx, const hmcx_sampler_args* s, const PersistPlan2& pl
   a.arena_bytes = (int)(ngran * 16);
   a.ep0 = ep0;
   a.pad = pad;
+  static const bool dbg = getenv("HMCX_P2_DEBUG") && getenv("HMCX_P2_DEBUG")[0] == '1';
+  if (dbg)
+    fprintf(stderr, "[hmcx p2] B=%d D=%d K=%d plan %dx%d Br=%d Bf=%d BfP=%d Ro=%d Fo=%d; granule bases XA %d XD %d XB %d "
+            "XW %d XS %d XC %d; epochs %u..%u\n", s->B, s->D, K, pl.Gr, pl.Gf, pl.Br, pl.Bf, pl.BfP, pl.Ro, pl.Fo,
+            a.oXA, a.oXD, a.oXB, a.oXW, a.oXS, a.oXC, ep0, ep0 + rounds - 1);
   {
     const int HA = KC + 1;
     const bool fits = pl.Gf * pl.Ro * KC <= QSTAGE && pl.Gf * (HA + pl.Ro * KC) <= QSTAGE &&

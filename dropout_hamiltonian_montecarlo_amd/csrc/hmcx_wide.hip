@@ -743,7 +743,7 @@ static int sgld_wide_impl(hmcx_ctx* ctx, const hmcx_sampler_args* s, bool allow_
     HMCX_HIP(ctx, hipMemcpyAsync(&flag, ctx->abort_dev, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
     HMCX_HIP(ctx, hipStreamSynchronize(ctx->stream));
     if (flag) {
-      HMCX_HIP(ctx, hipMemsetAsync(ctx->abort_dev, 0, sizeof(int), ctx->stream));
+      HMCX_HIP(ctx, hipMemsetAsync(ctx->abort_dev, 0, ABORT_WORDS * sizeof(int), ctx->stream));
       HMCX_HIP(ctx, hipMemcpyAsync(s->W, snapW, nW * sizeof(T), hipMemcpyDeviceToDevice, ctx->stream));
       HMCX_HIP(ctx, hipMemcpyAsync(s->b, snapb, nb * sizeof(T), hipMemcpyDeviceToDevice, ctx->stream));
       if (snappW) {

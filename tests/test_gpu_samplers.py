@@ -330,6 +330,20 @@ def test_sgld_gpu_variant_step_api():
         np.testing.assert_allclose(pg[v].cpu().numpy(), po[v], rtol=1e-10, atol=1e-14)
 
 
+@pytest.mark.parametrize("name", ["sghmc_hot", "sghmc_mnist"])
+def test_persistent_small_shapes_finish_without_recovery(name, capfd):
+    """The persistent kernel finishes every call itself (no timed-out hand-off and kernel-per-phase
+    re-run) on shapes where some row-team member owns no rows (sghmc_hot: B = 40, plan 2x2, row team 1
+    holds 8 of its 32 rows).  Round 3's kernel chose round B's protocol per member there and one member
+    waited out the 4 s timeout; the recovery hid it behind a correct result."""
+    c = gi.TRAJ_CONFIGS[name]
+    post_r, _, tr_r, _ = _run_oracle(c)
+    post_g, _, tr_g, _ = _run_gpu(c, path=2)
+    assert [t["accepted"] for t in tr_g] == [t["accepted"] for t in tr_r]
+    np.testing.assert_allclose(post_g["weights"], post_r["weights"], rtol=1e-9, atol=1e-11)
+    assert "timed out" not in capfd.readouterr().err
+
+
 @pytest.mark.parametrize("path", [1, 2])
 def test_sghmc_step_api_returns_momentum(path):
     """sghmc.step(state, momentum, rng) returns (q, p, acceptprob) like cpu/sghmc.py:19-39 (A1
