@@ -909,9 +909,11 @@ int hmcx_sgld_run(hmcx_ctx* ctx, const hmcx_sampler_args* a) {
   if (rc) return rc;
   if (!a->pW != !a->pb) return set_error(ctx, HMCX_EINVAL, "sgld: pW and pb must both be set or both NULL");
   if (a->n_steps == 0) return HMCX_OK;
+  // the wide path stores the per-step state rows (out_trace) in its update kernel: one call; the
+  // kernel-per-phase path runs traced calls a step at a time with a snapshot launch after each
+  if (sgld_wide_eligible(a))
+    return a->dtype == HMCX_F64 ? sgld_wide_t<double>(ctx, a) : sgld_wide_t<float>(ctx, a);
   return run_traced(ctx, a, [ctx](const hmcx_sampler_args* s) {
-    if (sgld_wide_eligible(s))
-      return s->dtype == HMCX_F64 ? sgld_wide_t<double>(ctx, s) : sgld_wide_t<float>(ctx, s);
     return s->dtype == HMCX_F64 ? sgld_run_t<double>(ctx, s) : sgld_run_t<float>(ctx, s);
   });
 }

@@ -55,6 +55,7 @@ template <typename T> struct WideArgs {
   char* gx; int gx_bytes; unsigned ep;   // the context's granule arena and this launch's epoch
   int* abort_flag;                       // the context's sticky abort word (raised on a timed-out poll)
   int force_abort;                       // test knob (HMCX_WIDE_FORCE_ABORT): workgroup 0 raises the word
+  T* trace; int P;                       // out_trace row of this step ([C][P]: W of chain c as [D][K], then b), or null
 };
 
 // a store that leaves the XCD's L2 (sc1: written through, the line dropped) or a plain one: the
@@ -514,6 +515,7 @@ __global__ __launch_bounds__(GTH) void k_wgrad(WideArgs<T> a) {
     p = p + a.m_half_eps * gb;                                               // sgld.py:37
     if (gpu_var) a.pb[bi] = p;
     a.b[bi] = bb + p;                                                        // sgld.py:38
+    if (a.trace) a.trace[(size_t)ch * a.P + (size_t)a.D * K + c] = bb + p;  // the step's state row
   }
   if (eok) {
     const int cc = ek - c0;
@@ -526,6 +528,7 @@ __global__ __launch_bounds__(GTH) void k_wgrad(WideArgs<T> a) {
     p = p + a.m_half_eps * gr_;                                                // sgld.py:37
     if (gpu_var) a.pW[wi] = p;
     a.W[wi] = wv + p;                                                          // sgld.py:38
+    if (a.trace) a.trace[(size_t)ch * a.P + el] = wv + p;
   }
   WSTAMP(4);
   WSTAMP(5);
@@ -693,6 +696,9 @@ static int sgld_wide_impl(hmcx_ctx* ctx, const hmcx_sampler_args* s, bool allow_
     a.step = s->step_base + (uint32_t)i;
     a.noff = buf ? d_noff + (size_t)i * C : nullptr;
     a.want_diff = 1;
+    // sghmc_multicore.py:49-51's per-step state row, stored by k_wgrad's update itself
+    a.trace = s->out_trace ? (T*)s->out_trace + (size_t)i * C * (D * K + K) : nullptr;
+    a.P = D * K + K;
     unsigned long long* pr = i < nprof ? prof + (size_t)i * GALL * WPH : nullptr;
     a.prof = pr;
     if (fuse) {

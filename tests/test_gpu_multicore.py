@@ -158,3 +158,42 @@ def test_persistent_trace_rows_equal_one_step_calls(dtype, noise):
     assert [t["L"] for t in g.trace] == [t["L"] for t in h.trace]
     np.testing.assert_array_equal(res.steps[-1, 0, :D * K].astype(np.float64), fin["weights"].reshape(-1))
     assert 0 < np.sum(res.accepted) and len(np.unique(res.steps[:, 0, 0])) > 1   # the chain moves
+
+
+@pytest.mark.parametrize("chains", [1, 4])
+def test_wide_sgld_trace_rows_equal_one_step_calls(chains):
+    """The wide SGLD path (config 5's width: D = 2048, K = 38) stores the trace rows in its update
+    kernel (one call, no per-step sub-calls or snapshot launches): a traced 6-step call records after
+    every step exactly (bit for bit) the state that six one-step untraced calls reach, per chain —
+    one chain on the fused two-launch path, four on the three-launch path."""
+    from dropout_hamiltonian_montecarlo_amd.hamiltonian.models.gpu.softmax import softmax
+    from dropout_hamiltonian_montecarlo_amd.hamiltonian.inference.gpu.sgld import sgld
+    N, B, D, K = 1500, 250, 2048, 38
+    X, Y = gi.dataset(64, N, D, K)
+    start = {"weights": np.zeros((D, K)), "bias": np.zeros(K)}
+    rows = list(range(0, N - B + 1, B))
+
+    def make():
+        s = sgld(softmax({"alpha": 0.1}, dtype=torch.float64, device="cuda:0"), start, step_size=1e-3,
+                 noise="philox", seed=9, chains=chains)
+        s.out = io.StringIO()
+        return s
+
+    g = make()
+    g.record_steps = True
+    data = g._upload_data(X, Y)
+    st = g._init_state()
+    res = g._run(st, data, rows, [g.step_size] * len(rows), None, B)
+    assert res.steps.shape == (len(rows), chains, D * K + K)
+    h = make()
+    data_h = h._upload_data(X, Y)
+    st_h = h._init_state()
+    for i, r in enumerate(rows):
+        h._run(st_h, data_h, [r], [h.step_size], None, B)
+        sh = h._state_to_host(st_h)
+        for c in range(chains):
+            w = sh["weights"] if chains == 1 else sh["weights"][c]
+            b = sh["bias"] if chains == 1 else sh["bias"][c]
+            np.testing.assert_array_equal(res.steps[i, c, :D * K], w.reshape(-1))
+            np.testing.assert_array_equal(res.steps[i, c, D * K:], b)
+    assert len(np.unique(res.steps[:, 0, 0])) > 1                                # the chain moves
