@@ -246,13 +246,18 @@ class hmc:
 
     # ------------------------------------------------------------------ generic path (device grads)
     def _K(self, p):                                                         # hmc.py:74-79
+        """Σ_var ½·Σp²: one device reduction per variable into one buffer, one readback (the per-variable
+        sums are added on the host in the reference's variable order)."""
         K = 0
         ctx = nat.context(self.model.device)
-        for var in p.keys():
+        ss = torch.empty(len(p), dtype=torch.float64, device=self.model.device)
+        keep = []
+        for i, var in enumerate(p.keys()):
             v = p[var].reshape(-1)
-            ss = torch.empty(1, dtype=torch.float64, device=v.device)
-            ctx.check(ctx.lib.hmcx_sumsq(ctx.h, self.model.code, ptr(v), v.numel(), ptr(ss)), "hmcx_sumsq")
-            K += 0.5 * ss.item()
+            keep.append(v)
+            ctx.check(ctx.lib.hmcx_sumsq(ctx.h, self.model.code, ptr(v), v.numel(), ptr(ss[i:i + 1])), "hmcx_sumsq")
+        for s2 in ss.cpu().numpy():
+            K += 0.5 * float(s2)
         return K
 
     def _axpy(self, mode, a, x, y):
