@@ -394,13 +394,18 @@ def plantvillage_measure(n_steps, rank):
     m.ctx.set_timing(False)
     tf = V_FLOP_PER_STEP * n_steps / (kms * 1e-3) / 1e12
     xbytes = 2.0 * B * V_D * 8                    # X tile read by the forward and by the gradient GEMM
+    fused = os.environ.get("HMCX_WIDE_FUSE", "1") != "0"
     out = {"workload": "PlantVillage-like softmax SGLD, D=2048 features, K=38, batch 500, 1 chain (BASELINE config 5)",
            "dtype": "f64", "param_dim": V_P, "steps": n_steps, "us_per_step": kms * 1e3 / n_steps,
            "leapfrogs_per_s": n_steps / dt, "value": n_steps / dt * V_P, "unit": "leapfrog-steps/s x param-dim",
            "roofline": {"bound": "mfma", "achieved": tf, "peak": MFMA_PEAK_TFLOPS["f64"], "unit": "TFLOP/s",
                         "frac": tf / MFMA_PEAK_TFLOPS["f64"], "device_ms": kms,
                         "hbm_GBps_X": xbytes * n_steps / (kms * 1e-3) / 1e9,
-                        "kernel": "k_wfwd + k_wsoft + k_wgrad per step (+ logging forward every 10th)"}}
+                        "alg_GBps_X": xbytes / 2 * n_steps / (kms * 1e-3) / 1e9,
+                        "alg_GBps_X_note": "the minibatch tile X (B x D x 8 B) counted once per step; hbm_GBps_X "
+                                           "counts its two reads (forward and gradient GEMM)",
+                        "kernel": ("k_wfwd_sm (forward + softmax) + k_wgrad per step" if fused else
+                                   "k_wfwd + k_wsoft + k_wgrad per step") + " (+ logging forward every 10th)"}}
     return out
 
 

@@ -807,8 +807,8 @@ __global__ void k_trace_snapshot(const T* __restrict__ W, const T* __restrict__ 
 }
 
 // A traced run is a sequence of one-step runs, each followed by a snapshot launch on the same
-// stream (chain-batched, wide and kernel-per-phase paths); the single-chain persistent SGHMC kernel
-// stores the rows itself at the end of every step and keeps one launch per call.
+// stream — only the kernel-per-phase SGLD path still runs traced calls this way; every SGHMC path and
+// the wide SGLD path store the rows inside the call.
 template <typename F>
 static int run_traced(hmcx_ctx* ctx, const hmcx_sampler_args* a, F run_one) {
   if (!a->out_trace) return run_one(a);
@@ -874,12 +874,10 @@ int hmcx_sghmc_run(hmcx_ctx* ctx, const hmcx_sampler_args* a_in) {
   // the 2-D persistent path fills out_host itself (no device abort copy); the others are copied here
   const bool host_by_kernel = p2;
   if (a->out_abort && !p2) HMCX_HIP(ctx, hipMemsetAsync(a->out_abort, 0, sizeof(int32_t), ctx->stream));
-  if (a->out_trace && p2)   // the persistent kernel stores the trace rows itself
-    rc = a->dtype == HMCX_F64 ? sghmc_run_t<double>(ctx, a) : sghmc_run_t<float>(ctx, a);
-  else
-    rc = run_traced(ctx, a, [ctx](const hmcx_sampler_args* s) {
-      return s->dtype == HMCX_F64 ? sghmc_run_t<double>(ctx, s) : sghmc_run_t<float>(ctx, s);
-    });
+  // every SGHMC path stores the per-step state rows (out_trace) itself: the persistent kernel after each
+  // accept, the chain-batched and kernel-per-phase paths in the next step's init launch (the state the
+  // step kept) and in the closing commit launch — one call, no one-step sub-calls or snapshot launches
+  rc = a->dtype == HMCX_F64 ? sghmc_run_t<double>(ctx, a) : sghmc_run_t<float>(ctx, a);
   if (rc || !a->out_host) return rc;
   if (!host_by_kernel) {
     const size_t nsc = (size_t)a->n_steps * a->C;

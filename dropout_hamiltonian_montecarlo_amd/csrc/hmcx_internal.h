@@ -179,12 +179,14 @@ template <typename T> struct InitArgs {
   T* Wwork; T* bwork; T* pW; T* pb;
   double* kin0_part;         // [nDB][C]
   double* kin0b;             // [C]
+  T* trace; int P;           // out_trace row of the PREVIOUS step ([C][P]), stored from the state it kept, or null
 };
 
 template <typename T> struct CommitArgs {
   int D, K, C, N;
   const int32_t* acc;
   const T* Wwork; const T* bwork; T* W; T* b;
+  T* trace; int P;           // out_trace row of the call's last step ([C][P]), or null
 };
 
 template <typename T> struct AcceptArgs {

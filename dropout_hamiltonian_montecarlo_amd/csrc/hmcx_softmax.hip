@@ -524,6 +524,7 @@ __global__ __launch_bounds__(256) void k_sghmc_init(InitArgs<T> a) {
     const T p = (T)z;                                                     // hmc.py:86 N(0,1)
     T q = a.W[w];
     if (take) { q = a.Wwork[w]; a.W[w] = q; }                             // commit (sghmc.py:37)
+    if (a.trace) a.trace[(size_t)c * a.P + d * K + k] = q;                // sghmc_multicore.py:49-51 row
     a.pW[w] = p;
     a.Wwork[w] = drift ? q + a.eps * p : q;                               // sghmc.py:32 (iteration 0)
     kin += (double)p * (double)p;
@@ -546,6 +547,7 @@ __global__ __launch_bounds__(256) void k_sghmc_init(InitArgs<T> a) {
       const T p = (T)z;
       T q = a.b[col];
       if (take) { q = a.bwork[col]; a.b[col] = q; }
+      if (a.trace) a.trace[(size_t)c * a.P + a.D * K + tid] = q;
       a.pb[col] = p;
       a.bwork[col] = q;
       kb = (double)p * (double)p;
@@ -563,15 +565,22 @@ __global__ __launch_bounds__(256) void k_sghmc_init(InitArgs<T> a) {
 template <typename T>
 __global__ __launch_bounds__(256) void k_sghmc_commit(CommitArgs<T> a) {
   const int c = blockIdx.y, tid = threadIdx.x;
-  if (!a.acc[c]) return;
+  const bool acc = a.acc[c];
+  if (!acc && !a.trace) return;
   const int K = a.K, d0 = blockIdx.x * 16;
   for (int e = tid; e < 16 * K; e += 256) {
     const int i = e / K, k = e - (e / K) * K, d = d0 + i;
     if (d >= a.D) continue;
     const size_t w = (size_t)d * a.N + c * K + k;
-    a.W[w] = a.Wwork[w];
+    const T q = acc ? a.Wwork[w] : a.W[w];
+    if (acc) a.W[w] = q;
+    if (a.trace) a.trace[(size_t)c * a.P + d * K + k] = q;               // the last step's row
   }
-  if (blockIdx.x == 0 && tid < K) a.b[c * K + tid] = a.bwork[c * K + tid];
+  if (blockIdx.x == 0 && tid < K) {
+    const T q = acc ? a.bwork[c * K + tid] : a.b[c * K + tid];
+    if (acc) a.b[c * K + tid] = q;
+    if (a.trace) a.trace[(size_t)c * a.P + a.D * K + tid] = q;
+  }
 }
 
 // Deterministic parallel sum of a[i*stride] for i < n over a 64-thread block.
@@ -1203,6 +1212,10 @@ __global__ __launch_bounds__(256) void k_binit(InitArgs<T> a) {
     } else {
       q0 = a.W[w]; q1 = a.W[w + 1];
     }
+    if (a.trace) {                                                    // sghmc_multicore.py:49-51 row
+      a.trace[(size_t)c * a.P + d * K + k] = q0;
+      a.trace[(size_t)c * a.P + d * K + k + 1] = q1;
+    }
     a.pW[wc] = p0; a.pW[wc + 1] = p1;
     a.Wwork[wc] = drift ? q0 + a.eps * p0 : q0;                       // sghmc.py:32 (iteration 0)
     a.Wwork[wc + 1] = drift ? q1 + a.eps * p1 : q1;
@@ -1225,6 +1238,7 @@ __global__ __launch_bounds__(256) void k_binit(InitArgs<T> a) {
       const T p = (T)z;
       T q = a.b[col];
       if (take) { q = a.bwork[col]; a.b[col] = q; }
+      if (a.trace) a.trace[(size_t)c * a.P + a.D * K + j] = q;
       a.pb[col] = p;
       a.bwork[col] = q;
       kb = (double)p * (double)p;
@@ -1240,14 +1254,22 @@ __global__ __launch_bounds__(256) void k_binit(InitArgs<T> a) {
 template <typename T>
 __global__ __launch_bounds__(256) void k_bcommit(CommitArgs<T> a) {
   const int c = blockIdx.y, tid = threadIdx.x;
-  if (!a.acc[c]) return;
+  const bool acc = a.acc[c];
+  if (!acc && !a.trace) return;
   const int K = a.K, d0 = blockIdx.x * 16;
   for (int e = tid; e < 16 * K; e += 256) {
     const int i = e / K, k = e - (e / K) * K, d = d0 + i;
     if (d >= a.D) continue;
-    a.W[(size_t)d * a.N + c * K + k] = a.Wwork[((size_t)c * a.D + d) * K + k];
+    const size_t w = (size_t)d * a.N + c * K + k;
+    const T q = acc ? a.Wwork[((size_t)c * a.D + d) * K + k] : a.W[w];
+    if (acc) a.W[w] = q;
+    if (a.trace) a.trace[(size_t)c * a.P + d * K + k] = q;               // the last step's row
   }
-  if (blockIdx.x == 0 && tid < K) a.b[c * K + tid] = a.bwork[c * K + tid];
+  if (blockIdx.x == 0 && tid < K) {
+    const T q = acc ? a.bwork[c * K + tid] : a.b[c * K + tid];
+    if (acc) a.b[c * K + tid] = q;
+    if (a.trace) a.trace[(size_t)c * a.P + a.D * K + tid] = q;
+  }
 }
 
 // C chains, K = 10: per step k_sghmc_init, k_bfwd(LL) at q0, then per leapfrog iteration k_bfwd +
@@ -1337,6 +1359,8 @@ int sghmc_batch_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
     ia.W = (T*)s->W; ia.b = (T*)s->b;
     ia.Wwork = Wwork; ia.bwork = bwork; ia.pW = pW; ia.pb = pb;
     ia.kin0_part = k0p; ia.kin0b = k0b;
+    ia.P = D * K + K;
+    ia.trace = s->out_trace && st_i > 0 ? (T*)s->out_trace + (size_t)(st_i - 1) * C * ia.P : nullptr;
     hipLaunchKernelGGL((k_binit<T>), dim3(nDB16, (C + 15) / 16), dim3(256), 0, st, ia);
     HMCX_HIP(ctx, hipGetLastError());
 
@@ -1406,6 +1430,8 @@ int sghmc_batch_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
   ca.D = D; ca.K = K; ca.C = C; ca.N = N;
   ca.acc = s->out_accepted + (size_t)(s->n_steps - 1) * C;
   ca.Wwork = Wwork; ca.bwork = bwork; ca.W = (T*)s->W; ca.b = (T*)s->b;
+  ca.P = D * K + K;
+  ca.trace = s->out_trace ? (T*)s->out_trace + (size_t)(s->n_steps - 1) * C * ca.P : nullptr;
   hipLaunchKernelGGL((k_bcommit<T>), dim3(nDB16, C), dim3(256), 0, st, ca);
   HMCX_HIP(ctx, hipGetLastError());
   hipLaunchKernelGGL(k_fix_acc, dim3((unsigned)((nsc + 255) / 256)), dim3(256), 0, st, d_niter, d_u,
@@ -1494,6 +1520,8 @@ int sghmc_run_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
     ia.W = (T*)s->W; ia.b = (T*)s->b;
     ia.Wwork = Wwork; ia.bwork = bwork; ia.pW = pW; ia.pb = pb;
     ia.kin0_part = k0p; ia.kin0b = k0b;
+    ia.P = D * K + K;
+    ia.trace = s->out_trace && st_i > 0 ? (T*)s->out_trace + (size_t)(st_i - 1) * C * ia.P : nullptr;
     hipLaunchKernelGGL((k_sghmc_init<T>), dim3(t.nDB, C), dim3(256), 0, st, ia);
     HMCX_HIP(ctx, hipGetLastError());
 
@@ -1536,6 +1564,8 @@ int sghmc_run_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
   ca.D = D; ca.K = K; ca.C = C; ca.N = N;
   ca.acc = s->out_accepted + (size_t)(s->n_steps - 1) * C;
   ca.Wwork = Wwork; ca.bwork = bwork; ca.W = (T*)s->W; ca.b = (T*)s->b;
+  ca.P = D * K + K;
+  ca.trace = s->out_trace ? (T*)s->out_trace + (size_t)(s->n_steps - 1) * C * ca.P : nullptr;
   hipLaunchKernelGGL((k_sghmc_commit<T>), dim3(t.nDB, C), dim3(256), 0, st, ca);
   HMCX_HIP(ctx, hipGetLastError());
   hipLaunchKernelGGL(k_fix_acc, dim3((unsigned)((nsc + 255) / 256)), dim3(256), 0, st, d_niter, d_u,

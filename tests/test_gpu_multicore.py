@@ -197,3 +197,46 @@ def test_wide_sgld_trace_rows_equal_one_step_calls(chains):
             np.testing.assert_array_equal(res.steps[i, c, :D * K], w.reshape(-1))
             np.testing.assert_array_equal(res.steps[i, c, D * K:], b)
     assert len(np.unique(res.steps[:, 0, 0])) > 1                                # the chain moves
+
+
+@pytest.mark.parametrize("chains,path", [(16, 0), (4, 0), (1, 1)])
+def test_sghmc_trace_rows_equal_one_step_calls(chains, path):
+    """The chain-batched (C >= 16, K = 10) and kernel-per-phase SGHMC paths store the trace rows inside
+    the call — row s by step s + 1's init launch (the state step s kept), the last row by the closing
+    commit launch: a traced 8-step call records after every step exactly (bit for bit) the state that
+    eight one-step untraced calls reach, per chain, with the same accept flags."""
+    from dropout_hamiltonian_montecarlo_amd.hamiltonian.models.gpu.softmax import softmax
+    from dropout_hamiltonian_montecarlo_amd.hamiltonian.inference.gpu.sghmc import sghmc
+    N, B, D, K = 400, 50, 40, 10
+    X, Y = gi.dataset(65, N, D, K)
+    start = {"weights": np.zeros((D, K)), "bias": np.zeros(K)}
+    rows = list(range(0, N - B + 1, B))
+
+    def make():
+        s = sghmc(softmax({"alpha": 0.1}, dtype=torch.float64, device="cuda:0"), start, path_length=0.05,
+                  step_size=0.01, noise="philox", seed=4, chains=chains)
+        s.out = io.StringIO()
+        s.model.ctx.set_sghmc_path(path)
+        return s
+
+    g = make()
+    g.record_steps = True
+    data = g._upload_data(X, Y)
+    st = g._init_state()
+    res = g._run(st, data, rows, [g.step_size] * len(rows), None, B)
+    assert res.steps.shape == (len(rows), chains, D * K + K)
+    h = make()
+    data_h = h._upload_data(X, Y)
+    st_h = h._init_state()
+    acc = []
+    for i, r in enumerate(rows):
+        ri = h._run(st_h, data_h, [r], [h.step_size], None, B)
+        acc.append(np.asarray(ri.accepted).reshape(-1))
+        sh = h._state_to_host(st_h)
+        for c in range(chains):
+            w = sh["weights"] if chains == 1 else sh["weights"][c]
+            b = sh["bias"] if chains == 1 else sh["bias"][c]
+            np.testing.assert_array_equal(res.steps[i, c, :D * K], w.reshape(-1))
+            np.testing.assert_array_equal(res.steps[i, c, D * K:], b)
+    np.testing.assert_array_equal(np.asarray(res.accepted).reshape(len(rows), -1), np.array(acc))
+    assert len(np.unique(res.steps[:, 0, 0])) > 1                                # the chain moves
