@@ -77,6 +77,7 @@ template <typename T> struct BFwdArgs {
   int nX, nCT;                      // row tiles × chain tiles (XCD-grouped 1-D grid, xcd_tile)
   T* colsum_part;                   // [nRB][N]
   double* ll_part;                  // [nRB][C]
+  int nRB_all;                      // partial blocks of the call: the last row tile zero-fills those past its own
 };
 
 template <typename T> struct BGradArgs {
@@ -172,6 +173,9 @@ __global__ __launch_bounds__(64 * NWV) void k_bfwd(BFwdArgs<T> a) {
   constexpr int ROWS = 32 * MT;
   constexpr int NTH = 64 * NWV;
   constexpr int MW = NWV == 8 ? MT / 2 : MT;          // m-tiles per wave
+  // partials are laid out per 32-row block whatever the tile height (every launch of a call may pick
+  // its own): a 64-row tile writes its sums into block 2·bx and zeros into 2·bx + 1
+  constexpr int PREP = MT;
   static_assert(NWV == 4 || (NWV == 8 && MT == 2), "k_bfwd: 8 waves need 64-row tiles");
   __shared__ T Xs[ROWS * BXP];
   __shared__ T Ws[BCH * BWP];          // also the epilogue tile, 32 rows at a time
@@ -353,14 +357,20 @@ __global__ __launch_bounds__(64 * NWV) void k_bfwd(BFwdArgs<T> a) {
   }
   if (sghmc && tid < BNT) {                            // Σ_rows (y − ŷ') of this tile
     const int cs = tid / BKC, ch = chs[cs];
-    if (ch >= 0) a.colsum_part[(size_t)bx * N + ch * BKC + (tid - cs * BKC)] = cs_acc;
+    if (ch >= 0) {
+      a.colsum_part[(size_t)bx * PREP * N + ch * BKC + (tid - cs * BKC)] = cs_acc;
+      const int r1 = bx == a.nX - 1 ? max(a.nRB_all, (bx + 1) * PREP) : (bx + 1) * PREP;
+      for (int r = bx * PREP + 1; r < r1; ++r) a.colsum_part[(size_t)r * N + ch * BKC + (tid - cs * BKC)] = T(0);
+    }
   }
   if (tid < BCT) {
     const int ch = chs[tid];
     if (ch >= 0 && (!sghmc || a.iter == a.n_iter[ch] - 1)) {
       double v = 0.0;
       for (int i = 0; i < nrow; ++i) v += Lt[i][tid];
-      a.ll_part[(size_t)bx * a.C + ch] = v;
+      a.ll_part[(size_t)bx * PREP * a.C + ch] = v;
+      const int r1 = bx == a.nX - 1 ? max(a.nRB_all, (bx + 1) * PREP) : (bx + 1) * PREP;
+      for (int r = bx * PREP + 1; r < r1; ++r) a.ll_part[(size_t)r * a.C + ch] = 0.0;
     }
   }
 }

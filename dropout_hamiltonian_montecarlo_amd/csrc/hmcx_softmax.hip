@@ -1279,10 +1279,13 @@ template <typename T>
 int sghmc_batch_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
   const int B = s->B, D = s->D, K = s->K, C = s->C, N = C * K;
   // row tiles of 64 (k_bfwd<T,2>) whenever the step's first iteration has >= 32 tiles of chains;
-  // colsum/ll partials are laid out per 64-row tile (a 32-row launch writes two tiles' worth)
+  // colsum/ll partials are laid out per 32-row block (a 64-row tile writes its sums and a zero block)
   const bool big = C >= 512;
-  const int RT = big ? 64 : 32;
-  const int nRB = (B + RT - 1) / RT, nDB = (D + BRW - 1) / BRW, nDB16 = (D + 15) / 16;
+  const int nX64 = (B + 63) / 64, nRB = big ? 2 * nX64 : (B + 31) / 32;
+  const int nDB = (D + BRW - 1) / BRW, nDB16 = (D + 15) / 16;
+  // compaction-tail launches (< one workgroup per CU at 64-row tiles): 32-row tiles, twice the workgroups
+  // (HMCX_BTAIL32=0: the 8-wave 64-row kernel, round 3)
+  const bool tail32 = !(getenv("HMCX_BTAIL32") && getenv("HMCX_BTAIL32")[0] == '0');
   const int nDB2 = (D + BRW2 - 1) / BRW2;            // k_bgradw<T, 4> feature tiles
   // dynamic LDS of the wide gradient kernel (set once per kernel)
   const size_t lds4 = BGW<T, 4>::lds();
@@ -1370,7 +1373,8 @@ int sghmc_batch_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
     f.mode = FWD_LL; f.iter = -1; f.c_act = C;                      // E_current at q0 (all chains)
     f.W = (const T*)s->W; f.b = (const T*)s->b; f.pb = pb;
     f.ll_part = ll0;
-    f.nX = nRB; f.nCT = (C + BCT - 1) / BCT;
+    f.nX = big ? nX64 : nRB; f.nCT = (C + BCT - 1) / BCT;
+    f.nRB_all = nRB;
     if (big) hipLaunchKernelGGL((k_bfwd<T, 2, 0>), dim3(xcd_grid(f.nX, f.nCT)), dim3(256), 0, st, f);
     else hipLaunchKernelGGL((k_bfwd<T, 1, 0>), dim3(xcd_grid(f.nX, f.nCT)), dim3(256), 0, st, f);
     HMCX_HIP(ctx, hipGetLastError());
@@ -1390,10 +1394,14 @@ int sghmc_batch_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
       int c_act = 0;
       while (c_act < C && ni_h[perm[(size_t)st_i * C + c_act]] > it) ++c_act;
       f.iter = it; f.c_act = c_act;
-      f.nX = nRB; f.nCT = (c_act + BCT - 1) / BCT;
-      // launches that leave CUs without a second workgroup: the 8-wave variant of the 64-row tile
+      f.nX = big ? nX64 : nRB; f.nCT = (c_act + BCT - 1) / BCT;
+      // launches that leave CUs without a second workgroup: 32-row tiles (or the 8-wave 64-row kernel)
       static const bool bf8_off = getenv("HMCX_BFWD8") && getenv("HMCX_BFWD8")[0] == '0';
-      if (big && !bf8_off && f.nX * f.nCT <= ctx->num_cus)
+      const bool tail = big && f.nX * f.nCT <= ctx->num_cus;
+      if (tail && tail32) {
+        f.nX = (B + 31) / 32;
+        hipLaunchKernelGGL((k_bfwd<T, 1, 1>), dim3(xcd_grid(f.nX, f.nCT)), dim3(256), 0, st, f);
+      } else if (tail && !bf8_off)
         hipLaunchKernelGGL((k_bfwd<T, 2, 1, 8>), dim3(xcd_grid(f.nX, f.nCT)), dim3(512), 0, st, f);
       else if (big) hipLaunchKernelGGL((k_bfwd<T, 2, 1>), dim3(xcd_grid(f.nX, f.nCT)), dim3(256), 0, st, f);
       else hipLaunchKernelGGL((k_bfwd<T, 1, 1>), dim3(xcd_grid(f.nX, f.nCT)), dim3(256), 0, st, f);

@@ -67,6 +67,13 @@ def test_replica_chains_match_oracle(name, chains):
         np.testing.assert_allclose(logp_g[ch], logp_r, rtol=1e-10)
 
 
+def test_replica_chains_tail_64row_kernel_match_oracle(monkeypatch):
+    """HMCX_BTAIL32=0: the compaction-tail forwards run the 8-wave 64-row kernel instead of 32-row tiles
+    (both write the 32-row partial layout) — same oracle parity at 1024 chains."""
+    monkeypatch.setenv("HMCX_BTAIL32", "0")
+    test_replica_chains_match_oracle("sghmc_mnist", 1024)
+
+
 def test_batched_chains_equal_single_chain_runs():
     """Philox noise: chain c of a 16-chain batched run == the single-chain run with chain=c."""
     c = dict(gi.TRAJ_CONFIGS["sghmc_small"])
