@@ -785,65 +785,6 @@ static int check_sampler(hmcx_ctx* ctx, const hmcx_sampler_args* a, bool sghmc) 
   return HMCX_OK;
 }
 
-// Per-step trace (out_trace): state after step s of chain c as param vectors (state dtype)
-// [weights row-major (d·K + k) | bias], the row the reference appends to its HDF5 backend after
-// every step (sghmc_multicore.py:49-51).  W is chain-interleaved [D][C·K].
-extern "C++" {
-template <typename T>
-__global__ void k_trace_snapshot(const T* __restrict__ W, const T* __restrict__ b, int D, int K, int C,
-                                 T* __restrict__ out) {
-  const long long P = (long long)D * K + K, n = P * C, DK = (long long)D * K;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
-    const long long c = i / P, e = i - c * P;
-    T v;
-    if (e < DK) {
-      const long long d = e / K, k = e - d * K;
-      v = W[d * C * K + c * K + k];
-    } else {
-      v = b[c * K + (e - DK)];
-    }
-    out[i] = v;
-  }
-}
-
-// A traced run is a sequence of one-step runs, each followed by a snapshot launch on the same
-// stream — only the kernel-per-phase SGLD path still runs traced calls this way; every SGHMC path and
-// the wide SGLD path store the rows inside the call.
-template <typename F>
-static int run_traced(hmcx_ctx* ctx, const hmcx_sampler_args* a, F run_one) {
-  if (!a->out_trace) return run_one(a);
-  const int C = a->C;
-  const long long P = (long long)a->D * a->K + a->K, n = P * C;
-  const unsigned grid = (unsigned)std::min<long long>((n + 255) / 256, 4096);
-  for (int i = 0; i < a->n_steps; ++i) {
-    hmcx_sampler_args s = *a;
-    const size_t iC = (size_t)i * C;
-    s.n_steps = 1;
-    s.row0 = a->row0 + i;
-    s.eps = a->eps + i;
-    if (a->n_iter) s.n_iter = a->n_iter + iC;
-    if (a->u_accept) s.u_accept = a->u_accept + iC;
-    if (a->want_ll) s.want_ll = a->want_ll + i;
-    if (a->noise_off) s.noise_off = a->noise_off + iC;
-    s.step_base = a->step_base + (uint32_t)i;
-    if (a->out_A) s.out_A = a->out_A + iC;
-    if (a->out_accepted) s.out_accepted = a->out_accepted + iC;
-    if (a->out_ll) s.out_ll = a->out_ll + iC;
-    if (a->out_E) s.out_E = a->out_E + 2 * iC;
-    s.out_trace = nullptr;
-    int rc = run_one(&s);
-    if (rc) return rc;
-    if (a->dtype == HMCX_F64)
-      hipLaunchKernelGGL(k_trace_snapshot<double>, dim3(grid), dim3(256), 0, ctx->stream, (const double*)a->W,
-                         (const double*)a->b, a->D, a->K, C, (double*)a->out_trace + (size_t)i * n);
-    else
-      hipLaunchKernelGGL(k_trace_snapshot<float>, dim3(grid), dim3(256), 0, ctx->stream, (const float*)a->W,
-                         (const float*)a->b, a->D, a->K, C, (float*)a->out_trace + (size_t)i * n);
-    HMCX_HIP(ctx, hipGetLastError());
-  }
-  return HMCX_OK;
-}
-}  // extern "C++"
 
 int hmcx_sghmc_run(hmcx_ctx* ctx, const hmcx_sampler_args* a_in) {
   HMCX_GUARD_CTX(ctx);
@@ -907,13 +848,10 @@ int hmcx_sgld_run(hmcx_ctx* ctx, const hmcx_sampler_args* a) {
   if (rc) return rc;
   if (!a->pW != !a->pb) return set_error(ctx, HMCX_EINVAL, "sgld: pW and pb must both be set or both NULL");
   if (a->n_steps == 0) return HMCX_OK;
-  // the wide path stores the per-step state rows (out_trace) in its update kernel: one call; the
-  // kernel-per-phase path runs traced calls a step at a time with a snapshot launch after each
+  // both SGLD paths store the per-step state rows (out_trace) in their update kernels: one call
   if (sgld_wide_eligible(a))
     return a->dtype == HMCX_F64 ? sgld_wide_t<double>(ctx, a) : sgld_wide_t<float>(ctx, a);
-  return run_traced(ctx, a, [ctx](const hmcx_sampler_args* s) {
-    return s->dtype == HMCX_F64 ? sgld_run_t<double>(ctx, s) : sgld_run_t<float>(ctx, s);
-  });
+  return a->dtype == HMCX_F64 ? sgld_run_t<double>(ctx, a) : sgld_run_t<float>(ctx, a);
 }
 
 int hmcx_hmc_mvn_run(hmcx_ctx* ctx, const hmcx_hmc_mvn_args* a) {

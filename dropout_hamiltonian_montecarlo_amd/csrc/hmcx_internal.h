@@ -165,6 +165,7 @@ template <typename T> struct GradArgs {
   double* kinb;       // SGHMC: [C] Σ pb² at the chain's last iteration
   int noise_mode; const double* noise; const int64_t* noff;
   uint64_t seed; uint32_t chain0, step, slot;
+  T* trace;           // SGLD: out_trace row of this step ([C][P]), or null
 };
 
 // SGHMC step start: commit the previous step's accepted proposal, draw momentum, first drift.

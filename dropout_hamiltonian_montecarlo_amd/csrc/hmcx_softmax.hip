@@ -395,10 +395,12 @@ __global__ __launch_bounds__(NW * 64) void k_grad(GradArgs<T> a) {
       p = p + a.m_half_eps * gr;
       a.pW[idx] = p;
       a.W[idx] = wreg[q] + p;                                             // gpu/sgld.py:19
+      if (a.trace) a.trace[(size_t)(c0 + j / K) * a.P + (size_t)(d0 + i) * K + j % K] = wreg[q] + p;
     } else {
       T p = a.noise_scale * zreg[q];
       p = p + a.m_half_eps * gr;
       a.W[idx] = wreg[q] + p;
+      if (a.trace) a.trace[(size_t)(c0 + j / K) * a.P + (size_t)(d0 + i) * K + j % K] = wreg[q] + p;   // sghmc_multicore.py:49-51
     }
   }
   if (mode == GRAD_SGHMC) {
@@ -484,6 +486,7 @@ __global__ __launch_bounds__(NW * 64) void k_grad(GradArgs<T> a) {
           p = p + a.m_half_eps * gr;
           if (mode == GRAD_SGLD_GPU) a.pb[col] = p;
           a.b[col] = bb + p;
+          if (a.trace) a.trace[(size_t)c * a.P + DK + k] = bb + p;
         }
       }
     }
@@ -1640,6 +1643,7 @@ int sgld_run_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
     g.W = (T*)s->W; g.b = (T*)s->b; g.pW = (T*)s->pW; g.pb = (T*)s->pb;
     g.noise_mode = s->noise_mode; g.noise = s->noise; g.noff = d_noff + (size_t)st_i * C;
     g.seed = s->seed; g.chain0 = s->chain0; g.step = s->step_base + (uint32_t)st_i; g.slot = 0;
+    g.trace = s->out_trace ? (T*)s->out_trace + (size_t)st_i * C * g.P : nullptr;
     HMCX_HIP(ctx, launch_grad<T>(g, t, st));
     if (s->want_ll && s->want_ll[st_i] && s->out_ll) {
       FwdArgs<T> fl = fwd_args<T>(Xs, Ys, s->W, s->b, B, D, K, C, t, FWD_LL);

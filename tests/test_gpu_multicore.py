@@ -64,7 +64,7 @@ def test_multicore_one_worker_vs_oracle(kind, tmp_path):
 
 @pytest.mark.parametrize("kind", ["sgld", "sghmc"])
 def test_multicore_traced_equals_untraced(kind, tmp_path):
-    """ncores = 4 Philox chains: the traced run (one-step sub-calls + snapshot kernel) ends in
+    """ncores = 4 Philox chains: the traced run (trace rows stored inside the call) ends in
     exactly the state of the untraced run, each chain's last recorded row is its final state,
     and the backend files hold the same rows (float32) as the in-memory run."""
     softmax, sghmc_mc, sgld_mc = _classes()
@@ -239,4 +239,40 @@ def test_sghmc_trace_rows_equal_one_step_calls(chains, path):
             np.testing.assert_array_equal(res.steps[i, c, :D * K], w.reshape(-1))
             np.testing.assert_array_equal(res.steps[i, c, D * K:], b)
     np.testing.assert_array_equal(np.asarray(res.accepted).reshape(len(rows), -1), np.array(acc))
+    assert len(np.unique(res.steps[:, 0, 0])) > 1                                # the chain moves
+
+
+@pytest.mark.parametrize("chains", [4, 16])
+def test_sgld_kernel_per_phase_trace_rows_equal_one_step_calls(chains):
+    """SGLD on the kernel-per-phase path (several chains at K <= 16) stores the trace rows in its
+    gradient launch's update: a traced 8-step call records after every step exactly (bit for bit) the
+    state that eight one-step untraced calls reach, per chain."""
+    from dropout_hamiltonian_montecarlo_amd.hamiltonian.models.gpu.softmax import softmax
+    from dropout_hamiltonian_montecarlo_amd.hamiltonian.inference.gpu.sgld import sgld
+    N, B, D, K = 400, 50, 40, 10
+    X, Y = gi.dataset(66, N, D, K)
+    start = {"weights": np.zeros((D, K)), "bias": np.zeros(K)}
+    rows = list(range(0, N - B + 1, B))
+
+    def make():
+        s = sgld(softmax({"alpha": 0.1}, dtype=torch.float64, device="cuda:0"), start, step_size=1e-3,
+                 noise="philox", seed=12, chains=chains)
+        s.out = io.StringIO()
+        return s
+
+    g = make()
+    g.record_steps = True
+    data = g._upload_data(X, Y)
+    st = g._init_state()
+    res = g._run(st, data, rows, [g.step_size] * len(rows), None, B)
+    assert res.steps.shape == (len(rows), chains, D * K + K)
+    h = make()
+    data_h = h._upload_data(X, Y)
+    st_h = h._init_state()
+    for i, r in enumerate(rows):
+        h._run(st_h, data_h, [r], [h.step_size], None, B)
+        sh = h._state_to_host(st_h)
+        for c in range(chains):
+            np.testing.assert_array_equal(res.steps[i, c, :D * K], sh["weights"][c].reshape(-1))
+            np.testing.assert_array_equal(res.steps[i, c, D * K:], sh["bias"][c])
     assert len(np.unique(res.steps[:, 0, 0])) > 1                                # the chain moves
