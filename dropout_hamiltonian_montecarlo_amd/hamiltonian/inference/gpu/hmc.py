@@ -260,6 +260,43 @@ class hmc:
             K += 0.5 * float(s2)
         return K
 
+    def _sumsq_into(self, p, out):
+        """Σp² of each variable of p into out[i] (device, no readback)."""
+        ctx = nat.context(self.model.device)
+        keep = []
+        for i, var in enumerate(p.keys()):
+            v = p[var].reshape(-1)
+            keep.append(v)
+            ctx.check(ctx.lib.hmcx_sumsq(ctx.h, self.model.code, ptr(v), v.numel(), ptr(out[i:i + 1])), "hmcx_sumsq")
+        return keep
+
+    @staticmethod
+    def _K_from(sums):                                                      # hmc.py:74-79
+        K = 0
+        for s2 in sums:
+            K += 0.5 * float(s2)
+        return K
+
+    def _energies(self, q_new, p_new, q, p, args):
+        """E_new, E_cur (hmc.py:57-58).  A model with energy_parts_device (the MLP) gets all four terms
+        enqueued into one device buffer and read back once, in the reference's order of evaluation;
+        otherwise through negative_log_posterior and _K."""
+        m = self.model
+        if not hasattr(m, "energy_parts_device"):
+            E_new = m.negative_log_posterior(q_new, **args) + self._K(p_new)
+            E_cur = m.negative_log_posterior(q, **args) + self._K(p)
+            return E_new, E_cur
+        nq, npv = len(q_new), len(p_new)
+        buf = torch.empty(2 * (1 + nq + npv), dtype=torch.float64, device=m.device)
+        o = [0, 1 + nq, 1 + nq + npv, 2 + 2 * nq + npv, 2 * (1 + nq + npv)]
+        keep = [m.energy_parts_device(q_new, buf[o[0]:o[1]], **args), self._sumsq_into(p_new, buf[o[1]:o[2]]),
+                m.energy_parts_device(q, buf[o[2]:o[3]], **args), self._sumsq_into(p, buf[o[3]:o[4]])]
+        h = buf.cpu().numpy()
+        del keep
+        E_new = m.nlp_from_parts(h[o[0]:o[1]], q_new) + self._K_from(h[o[1]:o[2]])
+        E_cur = m.nlp_from_parts(h[o[2]:o[3]], q) + self._K_from(h[o[3]:o[4]])
+        return E_new, E_cur
+
     def _axpy(self, mode, a, x, y):
         """y −= a·x (mode 0) / y += a·x (mode 1) on the device (hmcx_axpy)."""
         ctx = nat.context(self.model.device)
@@ -270,10 +307,13 @@ class hmc:
         dev, dt = m.device, m.dtype
         q = {k: torch.as_tensor(np.asarray(v) if not isinstance(v, torch.Tensor) else v).to(dev, dt).contiguous()
              for k, v in state.items()}
-        p = {k: torch.as_tensor(v).to(dev, dt).contiguous() for k, v in self.draw_momentum(rng).items()}
+        p_host = self.draw_momentum(rng)
+        p = {k: torch.as_tensor(v).to(dev, dt).contiguous() for k, v in p_host.items()}
         q_new = {k: v.clone() for k, v in q.items()}
         p_new = {k: v.clone() for k, v in p.items()}
-        positions, momentums = [deepcopy(state)], [{k: v.cpu().numpy() for k, v in p.items()}]
+        # the recorded momentum is the host draw in the model's dtype (what a device round trip returns)
+        npdt = torch.empty(0, dtype=dt).numpy().dtype
+        positions, momentums = [deepcopy(state)], [{k: np.asarray(v).astype(npdt) for k, v in p_host.items()}]
         epsilon = self.step_size
         path_length = np.ceil(2 * np.random.rand() * self.path_length / epsilon)
         grad_q = m.grad(q, **args)
@@ -285,8 +325,7 @@ class hmc:
                 self._axpy(0, epsilon, grad_q[var], p_new[var])                # hmc.py:53
         for var in self.start.keys():
             self._axpy(0, 2.0, p_new[var], p_new[var])                         # hmc.py:55-56: p − 2p = −p
-        E_new = m.negative_log_posterior(q_new, **args) + self._K(p_new)
-        E_cur = m.negative_log_posterior(q, **args) + self._K(p)
+        E_new, E_cur = self._energies(q_new, p_new, q, p, args)
         acceptprob = min(1, np.exp(E_cur - E_new))
         accepted = bool(np.isfinite(acceptprob) and (np.random.rand() < acceptprob))
         if accepted:
@@ -295,6 +334,29 @@ class hmc:
             self.trace.append({'L': float(path_length), 'A': float(acceptprob), 'accepted': accepted,
                                'eps': float(epsilon)})
         return q, p, positions, momentums, acceptprob
+
+    def _loss_and_state(self, q, args):
+        """negative_log_posterior(q) (hmc.py:113) and q on the host.  With energy_parts_device and a
+        device state: the loss pieces and the state (widened to float64, exactly) in one buffer, one
+        readback."""
+        m = self.model
+        keys = list(self.start.keys())
+        if not (hasattr(m, "energy_parts_device") and all(isinstance(q[v], torch.Tensor) for v in keys)):
+            loss = m.negative_log_posterior(q, **args)
+            return loss, {v: q[v].cpu().numpy() if isinstance(q[v], torch.Tensor) else q[v] for v in keys}
+        nq = len(q)
+        sizes = [q[v].numel() for v in keys]
+        buf = torch.empty(1 + nq + sum(sizes), dtype=torch.float64, device=m.device)
+        keep = m.energy_parts_device(q, buf[:1 + nq], **args)
+        buf[1 + nq:].copy_(torch.cat([q[v].reshape(-1) for v in keys]))
+        h = buf.cpu().numpy()
+        del keep
+        npdt = torch.empty(0, dtype=m.dtype).numpy().dtype
+        qh, o = {}, 1 + nq
+        for v, n in zip(keys, sizes):
+            qh[v] = h[o:o + n].astype(npdt).reshape(tuple(q[v].shape))
+            o += n
+        return m.nlp_from_parts(h[:1 + nq], q), qh
 
     def _sample_generic(self, niter, nburn, burnin, rng, tuning, args):
         q, p = self.start, None
@@ -312,9 +374,9 @@ class hmc:
             q, p, positions, momentums, _ = self.step(q, p, rng, **args)
             sample_positions.append(positions)
             sample_momentums.append(momentums)
-            loss[i] = self.model.negative_log_posterior(q, **args)
+            loss[i], qh = self._loss_and_state(q, args)
             for var in self.start.keys():
-                posterior[var].append(q[var].cpu().numpy() if isinstance(q[var], torch.Tensor) else q[var])
+                posterior[var].append(qh[var])
             if self.verbose and (i % (niter / 10) == 0):
                 print('loss: {0:.4f}'.format(loss[i]), file=self.out)
         for var in self.start.keys():

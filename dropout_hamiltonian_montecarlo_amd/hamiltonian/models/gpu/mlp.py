@@ -162,6 +162,33 @@ class mlp:
     def negative_log_posterior(self, par, masks=None, **args):           # mlp.py:80-82
         return self.log_likelihood(par, masks=masks, **args) + self.log_prior(par, **args)
 
+    def energy_parts_device(self, par, out, masks=None, **args):
+        """The device pieces of negative_log_posterior without a readback: out[0] = the loss
+        (log_likelihood), out[1 + i] = Σθ² of the i-th variable of par.  nlp_from_parts adds them up on
+        the host exactly as negative_log_posterior does, so a sampler can enqueue several energies and
+        read them back once.  Returns the device tensors the launches read (keep them until then)."""
+        X, y = self._xy(args)
+        B = X.shape[0]
+        _, mp = self._params(par)
+        m = self._masks(masks, B)
+        ctx = context(self.device)
+        ctx.check(ctx.lib.hmcx_mlp_loss(ctx.h, self.code, ptr(X), ptr(y), B, self.n_in, self.n_mid, self.n_out, mp,
+                                        ptr(m), ptr(out[0:1]), None), "hmcx_mlp_loss")
+        keep = [m]
+        for i, var in enumerate(par.keys()):
+            v = self._dev(par[var]).contiguous()
+            keep.append(v)
+            ctx.check(ctx.lib.hmcx_sumsq(ctx.h, self.code, ptr(v), v.numel(), ptr(out[1 + i:2 + i])), "hmcx_sumsq")
+        return keep
+
+    def nlp_from_parts(self, parts, par):
+        """negative_log_posterior from energy_parts_device's values (same float64 operations, same order)."""
+        ll = np.float64(parts[0])
+        K = 0.0
+        for i, var in enumerate(par.keys()):
+            K -= 0.5 * self.alpha * float(parts[1 + i]) / int(np.prod(np.shape(par[var])))
+        return ll + K
+
     def loss(self, par, masks=None, **args):
         """North-star surface name: the sampler energy U = negative_log_posterior."""
         return self.negative_log_posterior(par, masks=masks, **args)
