@@ -2,9 +2,11 @@
 through libhmcx's C ABI (include/hmcx.h hmcx_comm_* / hmcx_allgather_chain_stats /
 hmcx_allreduce_f64); torch.distributed (gloo) is only the control plane.  bench.py launched by
 torchrun with one rank and HMCX_DIST_FORCE=1 runs the timing max/sum reductions and the
-per-parameter summary all-gather through that communicator on the GPU.  N > 1 ranks need one GPU
-each (the driver's 8-GPU run); the N = 2 logic itself is covered by the gloo tests in
-tests/test_parallel_cpu.py and tests/test_bench_launch.py."""
+per-parameter summary all-gather through that communicator on the GPU.  N > 1 RCCL ranks need one GPU
+each (the driver's 8-GPU run); N > 1 here runs ranks that share cuda:0 over gloo — self-launched (2 and
+4 ranks, the latter with every leg at its default) and under torch.distributed.run (the driver's
+invocation form) — and the N = 2 logic is also covered by tests/test_parallel_cpu.py and
+tests/test_bench_launch.py."""
 import json
 import os
 import socket
@@ -106,3 +108,23 @@ def test_bench_four_ranks_shared_gpu_default_legs():
     assert line["cpu_baseline"]["value"] > 0 and line["cpu_baseline"]["calibration_ratio"] > 0
     for leg in ("chain_batched", "mlp", "plantvillage_sgld"):
         assert line[leg] is not None and line[leg]["value"] > 0, leg
+
+
+def test_bench_torchrun_two_ranks_shared_gpu():
+    """The driver's SCALE invocation form — `python -m torch.distributed.run --nproc-per-node N … bench.py
+    --gpus N` — at N = 2 on one GPU (ranks share cuda:0, gloo): bench.py runs as the launcher's rank,
+    rank 0 prints the one JSON line with n_gpus 2 and both chains in the diagnostics."""
+    port = str(_free_port())
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(HMCX_BENCH_SHARED_GPU="1", HMCX_DIST_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", port, "bench.py", "--gpus", "2", "--path", "kernels",
+           "--steps", "5", "--warmup", "2", "--cpu-seconds", "0", "--batched-chains", "0", "--mlp-steps", "0",
+           "--sgld-steps", "0"]
+    r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["config"]["chains"] == 2 and line["value"] > 0
+    assert line["scaling"] == "weak" and line["diagnostics"]["per_parameter"]["chains"] == 2
