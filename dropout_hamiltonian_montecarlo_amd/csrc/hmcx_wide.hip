@@ -1,6 +1,7 @@
 // hmcx_wide.hip — SGLD for wide softmax shapes (K ≤ 64 classes; designed for BASELINE config 5:
-// PlantVillage-like conv features, D = 2048, K = 38, batch 500), one or several chains, three
-// launches per step.
+// PlantVillage-like conv features, D = 2048, K = 38, batch 500), one or several chains: two launches
+// per step (k_wfwd_sm, k_wgrad) where the forward grid is co-resident, else three (k_wfwd, k_wsoft,
+// k_wgrad).
 //
 // Mathematics and op order: cpu/sgld.py:31-46 (p = N(0,(2ε)²) then p += −½ε·g, q += p) with the
 // gradient of cpu/softmax.py:38-61 (clip, softmax, diff = y − ŷ, g = −(Xᵀ·diff − αW)), as in the
@@ -21,8 +22,9 @@
 //            reduction — then updates those weights in place; feature tile 0 of each group also
 //            sums its diff columns and updates the group's biases.  Its loads are issued before the
 //            Philox noise is drawn, so the noise hides in their latency.
-// Measured (config 5, f64, one chain, MI355X): 22.8 µs per step against 29.1 for the previous
-// LDS-staged forward + one-workgroup-per-feature-tile gradient.
+//   k_wfwd_sm k_wfwd + k_wsoft in one launch: the row team's partial logits travel as tagged granules.
+// Measured (config 5, f64, one chain, MI355X): 20.6 µs per step fused, 21.9 on the three launches,
+// 29.1 for the round-2 LDS-staged forward + one-workgroup-per-feature-tile gradient.
 #include "hmcx_common.h"
 #include "hmcx_internal.h"
 #include "hmcx_p2x.h"
