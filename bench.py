@@ -443,6 +443,21 @@ def main():
         parallel.finalize()
 
 
+def warmup_calls(warmup, chunk):
+    """Step counts of the untimed warm-up calls of the headline leg: the same enqueue / collect protocol as
+    the timed region, in at least two calls when there are two steps or more — the first call fills the
+    sampler's argument caches, the second runs the cached steady-state path (sghmc._enqueue_quick) the
+    timed calls take, so its first execution is not inside the clock.  tools/pmc_summary.py counts these
+    dispatches to find the timed ones."""
+    calls, done = [], 0
+    first = min(chunk, max(1, warmup // 2))
+    while done < warmup:
+        n = min(first if done == 0 else chunk, warmup - done)
+        calls.append(n)
+        done += n
+    return calls
+
+
 def bench(args, parallel):
     import torch
     rank, world, local = parallel.init()
@@ -477,16 +492,10 @@ def bench(args, parallel):
         return s._enqueue(state, data, rows, [EPS] * n_steps, None, B)
 
     CHUNK = nb                                       # one call per epoch (120 steps)
-    # warm-up (untimed): the same enqueue / collect protocol as the timed region, in at least two calls
-    # when there are two steps or more — the first call fills the sampler's argument caches, the
-    # second runs the cached steady-state path (sghmc._enqueue_quick) the timed calls take, so its
-    # first execution is not inside the clock
     keep_trace = os.environ.get("HMCX_BENCH_TRACE") == "1"
     s.trace = [] if keep_trace else None
     done = 0
-    first = min(CHUNK, max(1, args.warmup // 2))
-    while done < args.warmup:
-        n = min(first if done == 0 else CHUNK, args.warmup - done)
+    for n in warmup_calls(args.warmup, CHUNK):
         s._collect(enqueue(n, done))
         done += n
     torch.cuda.synchronize()

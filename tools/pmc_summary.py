@@ -17,6 +17,9 @@ import json
 import os
 import sys
 
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import warmup_calls  # noqa: E402  (bench.py's warm-up protocol, the single definition)
+
 
 def per_launch(d, counter, kname):
     f = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
@@ -41,13 +44,7 @@ def main():
     lf = float(b["leapfrogs"])
     steps = int(b["steps"])
     chunk = 120                                         # bench.py: one call per epoch of 60000 / 500 rows
-    # warm-up dispatches before the timed ones: bench.py's warm-up protocol (a first call of
-    # min(chunk, max(1, warmup // 2)) steps, then calls of up to `chunk` steps)
-    warm, w0, done = int(b["warmup"]), 0, 0
-    first = min(chunk, max(1, warm // 2))
-    while done < warm:
-        done += min(first if done == 0 else chunk, warm - done)
-        w0 += 1
+    w0 = len(warmup_calls(int(b["warmup"]), chunk))    # warm-up dispatches before the timed ones
     fm = sum(fetch[w0:w0 + calls]) / calls
     wm = sum(write[w0:w0 + calls]) / calls
     per_launch_bytes = (2.0 * fm + wm) * 1024.0
