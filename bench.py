@@ -35,6 +35,11 @@ ALPHA, EPS, LAMBDA = 0.01, 1e-3, 1e-2
 FLOP_PER_LEAPFROG = 4.0 * B * D * K          # X·W and Xᵀ·diff: 15.68 MFLOP
 DIAG_STEPS, DIAG_THIN = 240, 4               # untimed diagnostics run after the timed region
 MFMA_PEAK_TFLOPS = {"f64": 78.6, "f32": 157.3}   # dense MFMA, MI355X spec (f32: MI355X_MICROARCH.md)
+SEED = 20251015                              # Philox key of the headline chains (chain id = rank)
+# kernel time of one persistent launch = a + b·steps + c·leapfrogs (µs), least squares over 48 calls of
+# 1 … 120 steps (tools/probe_launch_fixed.py, profiles/r03_launch_fixed.txt): the model behind
+# predicted_speedup
+LAUNCH_FIT_US = (19.0, 11.14, 7.965)
 
 
 def parse():
@@ -57,6 +62,39 @@ def parse():
                     help="launcher check without a GPU: ranks rendezvous over gloo, reduce a dummy count "
                          "and rank 0 prints the JSON line shape (tests/test_bench_launch.py)")
     return ap.parse_args()
+
+
+def aggregate_ranks(per_rank, P_dim=P):
+    """The multi-GPU line from every rank's own numbers (list ordered by rank, each {"leapfrogs": lf_r,
+    "seconds": t_r}): `value` is the makespan rate Σ_r lf_r ÷ max_r t_r (the contract's max-over-ranks
+    clock), `value_chain_throughput` the sum of the ranks' own rates Σ_r lf_r ÷ t_r (north_star's
+    "chain-throughput": independent chains, each GPU's rate counted over its own timed region).  With
+    random path lengths (sghmc.py:25) the ranks do unequal work over the same steps, so the makespan
+    rate is below the chain throughput by the spread of Σ L − 1 across chains."""
+    lf = [float(r["leapfrogs"]) for r in per_rank]
+    t = [float(r["seconds"]) for r in per_rank]
+    return {"value_makespan": sum(lf) / max(t) * P_dim,
+            "value_chain_throughput": sum(l_ / t_ for l_, t_ in zip(lf, t)) * P_dim,
+            "per_rank_leapfrogs": lf, "per_rank_ms": [x * 1e3 for x in t]}
+
+
+def predicted_scaling(warmup, steps, path_length=LAMBDA, eps=EPS, seed=SEED, worlds=(1, 2, 4, 8), fit=LAUNCH_FIT_US,
+                      calls_per_rank=1):
+    """What the N-GPU line should show, before any N > 1 run: the timed leapfrogs of chains 0 … N−1
+    from the host twin of the device schedule (hmcx_philox_schedule — the same path lengths the kernels
+    draw) and each rank's kernel time from the launch fit; speedups under both definitions of
+    aggregate_ranks, relative to rank 0 alone."""
+    from dropout_hamiltonian_montecarlo_amd import _native as nat
+    L, n_iter, _ = nat.philox_schedule(seed, 0, max(worlds), warmup, path_length, np.full(steps, eps))
+    lf = n_iter.astype(np.float64).sum(axis=0)                 # [chains]: Σ max(0, L − 1) over the timed steps
+    t_us = fit[0] * calls_per_rank + fit[1] * steps + fit[2] * lf
+    base = lf[0] / t_us[0]
+    out = {"chain_leapfrogs": lf.tolist(), "fit_us": list(fit), "source": "hmcx_philox_schedule (host twin) + "
+           "LAUNCH_FIT_US (profiles/r03_launch_fixed.txt)"}
+    for n in worlds:
+        out[str(n)] = {"makespan": float(lf[:n].sum() / t_us[:n].max() / base),
+                       "chain_throughput": float((lf[:n] / t_us[:n]).sum() / base)}
+    return out
 
 
 def launch_ranks(n, argv):
@@ -138,11 +176,12 @@ def dry_run(args):
     try:
         t = parallel.allreduce_max(0.001 * (rank + 1))
         lf = parallel.allreduce_sum(10.0 * (rank + 1))
+        ranks = aggregate_ranks(parallel.gather_objects({"leapfrogs": 10.0 * (rank + 1), "seconds": 0.001 * (rank + 1)}))
         env = {k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
         envs = parallel.gather_objects(env)
         if rank == 0:
             print(json.dumps({"metric": "dry-run", "value": lf / t, "n_gpus": world, "steps": args.steps,
-                              "warmup": args.warmup, "leapfrogs": lf, "t_max": t, "rank_env": envs,
+                              "warmup": args.warmup, "leapfrogs": lf, "t_max": t, "rank_env": envs, "ranks": ranks,
                               "config": {"chains": world, "local_rank_devices": [e["LOCAL_RANK"] for e in envs]}}))
     finally:
         parallel.finalize()
@@ -477,7 +516,7 @@ def bench(args, parallel):
     model.ctx.set_sghmc_path({"auto": 0, "kernels": 1, "persistent": 2}[args.path])
     chain0, _ = parallel.chain_block(world, rank, world)     # one chain per rank: Philox key chain0
     s = sghmc(model, {"weights": np.zeros((D, K)), "bias": np.zeros(K)}, path_length=LAMBDA, step_size=EPS,
-              noise="philox", seed=20251015, chain=chain0)
+              noise="philox", seed=SEED, chain=chain0)
     s.out = io.StringIO()
     data = s._upload_data(X, Y)                      # dataset resident in HBM before timing
     state = s._init_state()
@@ -492,6 +531,7 @@ def bench(args, parallel):
         return s._enqueue(state, data, rows, [EPS] * n_steps, None, B)
 
     CHUNK = nb                                       # one call per epoch (120 steps)
+    rec0 = recoveries()
     keep_trace = os.environ.get("HMCX_BENCH_TRACE") == "1"
     s.trace = [] if keep_trace else None
     done = 0
@@ -552,6 +592,11 @@ def bench(args, parallel):
     t_max = parallel.allreduce_max(elapsed, device=dev)
     lf_total = parallel.allreduce_sum(lf_local, device=dev)
     value = lf_total / t_max * P
+    # every rank's own leapfrogs and clock (control plane, small objects): both aggregates of the line
+    per_rank = parallel.gather_objects({"leapfrogs": lf_local, "seconds": elapsed, "kernel_ms": kern_ms})
+    ranks = aggregate_ranks(per_rank)
+    ranks["per_rank_kernel_ms"] = [r["kernel_ms"] for r in per_rank]
+    rec = {"headline": recovery_delta(rec0)}
 
     # cross-chain diagnostics (untimed, after the timed region): DIAG_STEPS more steps of the same
     # chain return the state after every step (out_trace); per-parameter Welford mean / M2 and a
@@ -578,34 +623,55 @@ def bench(args, parallel):
     batched = None
     if args.batched_chains > 0:
         model.ctx.set_sghmc_path(0)
+        r0 = recoveries()
         batched = batched_chains(model, X, Y, data, args.batched_chains, 24, rank)
         if args.batched_chains != 2048:       # round 2's operating point, for comparison
             b2 = batched_chains(model, X, Y, data, 2048, 24, rank)
             batched["sweep"] = {"2048": {"frac": b2["roofline"]["frac"], "leapfrogs_per_s": b2["leapfrogs_per_s"]},
                                 str(args.batched_chains): {"frac": batched["roofline"]["frac"],
                                                            "leapfrogs_per_s": batched["leapfrogs_per_s"]}}
+        batched["recoveries"] = rec["chain_batched"] = recovery_delta(r0)
         parallel.barrier()
     mlp_out = None
     if args.mlp_steps > 0:
         lab = np.argmax(Y, axis=1)
+        r0 = recoveries()
         mlp_out = mlp_measure(X, lab, args.mlp_steps, rank)
         mlp_out["f64"] = mlp_measure(X, lab, args.mlp_steps, rank, dtype="f64")   # the parity dtype's cost
+        mlp_out["recoveries"] = rec["mlp"] = recovery_delta(r0)
         parallel.barrier()
     v_out = None
     if args.sgld_steps > 0:
+        r0 = recoveries()
         v_out = plantvillage_measure(args.sgld_steps, rank)
+        v_out["recoveries"] = rec["plantvillage_sgld"] = recovery_delta(r0)
         parallel.barrier()
+    # re-runs after timed-out exchanges on any rank, per leg (must all be 0: a fallback would be timed as
+    # if it were the fused / persistent kernel)
+    rec_all = parallel.gather_objects(rec)
+    recov = {leg: sum(sum(r[leg].values()) for r in rec_all) for leg in rec}
     parallel.barrier()
     if rank == 0:
+        ranks["predicted"] = predicted_scaling(args.warmup, args.steps, calls_per_rank=n_calls)
         report(args, world, value, t_max, lf_total, lf_local, n_calls, kern_ms, kern_n, diag_par, diag,
-               batched, mlp_out, v_out, X, Y)
+               batched, mlp_out, v_out, X, Y, ranks, recov)
     # closing barrier: every rank waits here until rank 0 has run its CPU baselines and printed, so the
     # RCCL communicator and the process group are torn down by all ranks together (main()'s finally)
     parallel.barrier()
 
 
+def recoveries():
+    from dropout_hamiltonian_montecarlo_amd import _native as nat
+    return nat.recoveries_all()
+
+
+def recovery_delta(before):
+    now = recoveries()
+    return {k: now[k] - before.get(k, 0) for k in now}
+
+
 def report(args, world, value, t_max, lf_total, lf_local, n_calls, kern_ms, kern_n, diag_par, diag,
-           batched, mlp_out, v_out, X, Y):
+           batched, mlp_out, v_out, X, Y, ranks, recov):
     """Rank 0: the JSON line (and the CPU baselines, after every rank's GPU work)."""
     from dropout_hamiltonian_montecarlo_amd import parallel
     CHUNK = N_DATA // B                              # steps per call (one epoch), as in bench()
@@ -634,6 +700,9 @@ def report(args, world, value, t_max, lf_total, lf_local, n_calls, kern_ms, kern
                    "impl": path},
         "leapfrogs_per_s": lf_total / t_max,
         "leapfrogs": lf_total,
+        "value_definition": "makespan: leapfrogs of all ranks / max-over-ranks timed region x P",
+        "ranks": ranks,
+        "recoveries": recov,
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                      "frac": achieved / peak, "traffic": pmc_traffic(args.dtype, path, lf_local / n_calls),
                      "traffic_source": "PMC 2*FETCH_SIZE+WRITE_SIZE per leapfrog of the driver-shape launch "
@@ -646,6 +715,10 @@ def report(args, world, value, t_max, lf_total, lf_local, n_calls, kern_ms, kern
         "diagnostics": {"per_parameter": diag_par,
                         "source": "%d untimed steps after the timed region, state after every step; Welford "
                                   "mean/M2 per parameter and every %dth draw, one all_gather" % (DIAG_STEPS, DIAG_THIN),
+                        "note": "burn-in, not a convergence check: the chains start at zero (2.-MNIST.ipynb) and "
+                                "have taken %d steps when these draws begin, so R-hat / ESS here describe the "
+                                "transient; they exercise the gather path (RCCL at N > 1), not mixing"
+                                % (args.warmup + args.steps),
                         "rhat_ll": float(np.ravel(diag["rhat"])[0]), "ess_ll": float(np.ravel(diag["ess"])[0]),
                         "gather": parallel.backend_name() if parallel.dist.is_initialized() else "local"},
         "cpu_baseline": None,

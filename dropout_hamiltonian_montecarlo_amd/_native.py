@@ -96,7 +96,7 @@ EXPORTS = ("hmcx_version", "hmcx_create", "hmcx_destroy", "hmcx_last_error", "hm
            "hmcx_sgld_run", "hmcx_hmc_mvn_run", "hmcx_mlp_masks", "hmcx_mlp_grad", "hmcx_mlp_loss",
            "hmcx_mlp_sghmc_run", "hmcx_logistic_grad", "hmcx_logistic_loglik", "hmcx_logistic_predict",
            "hmcx_sumsq", "hmcx_sgd_run", "hmcx_hmc_run", "hmcx_axpy", "hmcx_mvn_eval",
-           "hmcx_clear_abort", "hmcx_philox_schedule", "hmcx_host_wait", "hmcx_set_mlp_fuse",
+           "hmcx_clear_abort", "hmcx_get_recoveries", "hmcx_note_recovery", "hmcx_philox_schedule", "hmcx_host_wait", "hmcx_set_mlp_fuse",
            "hmcx_comm_unique_id", "hmcx_comm_init", "hmcx_comm_destroy", "hmcx_allgather_chain_stats",
            "hmcx_allreduce_f64")
 
@@ -145,6 +145,9 @@ def load_library():
                                              c_void_p, c_void_p, c_void_p]
         lib.hmcx_sghmc_run.argtypes = [c_void_p, ctypes.POINTER(SamplerArgs)]
         lib.hmcx_clear_abort.argtypes = [c_void_p]
+        if hasattr(lib, "hmcx_get_recoveries"):        # absent in older builds loaded for A/B runs
+            lib.hmcx_get_recoveries.argtypes = [c_void_p, c_i64p]
+            lib.hmcx_note_recovery.argtypes = [c_void_p, c_int]
         lib.hmcx_host_wait.argtypes = [c_void_p, c_void_p]
         lib.hmcx_philox_schedule.argtypes = [ctypes.c_uint64, ctypes.c_uint32, c_int, ctypes.c_uint32, c_int,
                                              c_double, c_dblp, c_dblp, c_i32p, c_dblp]
@@ -226,6 +229,19 @@ class Context:
         """Lower the context's persistent-launch abort word (include/hmcx.h hmcx_clear_abort)."""
         self.check(self.lib.hmcx_clear_abort(self.h), "hmcx_clear_abort")
 
+    RECOVERY_KINDS = ("persistent_sghmc", "mlp_fused", "sgld_wide_fused")   # include/hmcx.h hmcx_recovery
+
+    def recoveries(self):
+        """Re-runs after timed-out exchanges since this context was created, by kind
+        (include/hmcx.h hmcx_get_recoveries): all zero unless a fallback path ran."""
+        out = (ctypes.c_int64 * len(self.RECOVERY_KINDS))()
+        self.check(self.lib.hmcx_get_recoveries(self.h, out), "hmcx_get_recoveries")
+        return dict(zip(self.RECOVERY_KINDS, (int(v) for v in out)))
+
+    def note_recovery(self, kind):
+        """Record a re-run the host layer performed (include/hmcx.h hmcx_note_recovery)."""
+        self.check(self.lib.hmcx_note_recovery(self.h, self.RECOVERY_KINDS.index(kind)), "hmcx_note_recovery")
+
     mlp_fuse = True
 
     def set_mlp_fuse(self, on):
@@ -285,6 +301,17 @@ def _release_contexts():
         if getattr(c, "h", None) and c.h.value:
             c.lib.hmcx_destroy(c.h)
             c.h = c_void_p()
+
+
+def recoveries_all():
+    """Summed recovery counts over every context of this process (zeros when none exists)."""
+    tot = dict.fromkeys(Context.RECOVERY_KINDS, 0)
+    with _lock:
+        ctxs = list(_ctxs.values())
+    for c in ctxs:
+        for k, v in c.recoveries().items():
+            tot[k] += v
+    return tot
 
 
 def ptr(t):

@@ -518,6 +518,7 @@ int hmcx_destroy(hmcx_ctx* ctx) {
   if (ctx->abort_host) (void)hipHostFree(ctx->abort_host);
   if (ctx->abort_dev) (void)hipFree(ctx->abort_dev);
   if (ctx->mlp_abort_dev) (void)hipFree(ctx->mlp_abort_dev);
+  if (ctx->wide_abort_dev) (void)hipFree(ctx->wide_abort_dev);
   if (ctx->zeros_dev) (void)hipFree(ctx->zeros_dev);
   if (ctx->gx_arena) (void)hipFree(ctx->gx_arena);
   for (auto& g : ctx->graveyard) {
@@ -556,6 +557,20 @@ int hmcx_clear_abort(hmcx_ctx* ctx) {
             w[2], w[3]);
   }
   HMCX_HIP(ctx, hipMemsetAsync(ctx->abort_dev, 0, ABORT_WORDS * sizeof(int), ctx->stream));
+  ++ctx->recoveries[HMCX_RECOVERY_PERSISTENT];
+  return HMCX_OK;
+}
+
+int hmcx_get_recoveries(const hmcx_ctx* ctx, int64_t* counts) {
+  if (!ctx || !counts) return HMCX_EINVAL;
+  for (int k = 0; k < HMCX_RECOVERY_KINDS; ++k) counts[k] = ctx->recoveries[k];
+  return HMCX_OK;
+}
+
+int hmcx_note_recovery(hmcx_ctx* ctx, int kind) {
+  HMCX_GUARD_CTX(ctx);
+  if (kind < 0 || kind >= HMCX_RECOVERY_KINDS) return set_error(ctx, HMCX_EINVAL, "unknown recovery kind");
+  ++ctx->recoveries[kind];
   return HMCX_OK;
 }
 

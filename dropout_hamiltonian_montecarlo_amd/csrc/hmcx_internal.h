@@ -62,6 +62,11 @@ struct hmcx_ctx {
   // fused MLP launches (hmcx_mlp.hip MM_L23): their own abort word, reported per call (out_abort)
   int* mlp_abort_dev = nullptr;
   int mlp_nofuse = 0;                  // hmcx_set_mlp_fuse(ctx, 0): the sampler runs unfused
+  // fused wide-SGLD forward + softmax (hmcx_wide.hip k_wfwd_sm): its own abort word, never the
+  // persistent SGHMC kernels' sticky one — read and lowered only by the wide call that raised it
+  int* wide_abort_dev = nullptr;
+  // re-runs after timed-out exchanges, by hmcx_recovery kind (hmcx_get_recoveries)
+  int64_t recoveries[HMCX_RECOVERY_KINDS] = {0, 0, 0};
 };
 constexpr int ABORT_SLOTS = 64;
 constexpr int ABORT_WORDS = 4;       // abort_dev: the word, then workgroup / granule base / epoch of the first timeout

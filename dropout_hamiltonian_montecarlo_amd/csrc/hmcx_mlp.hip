@@ -1069,7 +1069,7 @@ struct MlpAccept {
 // One workgroup of 26 × 32 threads: group g < 24 sums the NPART partials of (state g/12, kind, variable),
 // groups 24/25 the loss partials of the current / proposed state — each lane a fixed-order strided
 // sum, then a fixed-order tree.
-__global__ __launch_bounds__(1024) void k_mlp_accept(MlpAccept a) {
+static __global__ __launch_bounds__(1024) void k_mlp_accept(MlpAccept a) {
   __shared__ double sh[26][32];
   const int t = threadIdx.x, g = t >> 5, j = t & 31;
   double x = 0.0;
@@ -1118,7 +1118,7 @@ __global__ void k_mlp_commit(VarTab vt, const int32_t* acc) {
   for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) dst[i] = src[i];
 }
 
-__global__ void k_loss_final(const double* lpart, int nlb, int B, double* out) {
+static __global__ void k_loss_final(const double* lpart, int nlb, int B, double* out) {
   double s = 0.0;
   for (int b = 0; b < nlb; ++b) s += lpart[b];
   *out = s / (double)B;
@@ -1166,9 +1166,10 @@ void net_init(MlpNet<T>& net, int B, int n_in, int n_mid, int n_out, hipStream_t
 
 // Launch k_mm for a call site with compile-time operand layouts (TA: A stored [K][M], TB: B stored
 // [N][K]); k-contiguous operands take the 16-byte vector path when aligned.  Takes the pending update.
-template <typename T, int EPI, int TA, int TB, int AOP = OP_PLAIN, int BOP = OP_PLAIN>
+// BAT: the call site passes a problem table (k_mmb); plain call sites instantiate k_mm only.
+template <typename T, int EPI, int TA, int TB, int AOP = OP_PLAIN, int BOP = OP_PLAIN, bool BAT = false>
 hipError_t mm(MlpNet<T>& net, MMArgs<T>& a, const MMProbs<T>* prp = nullptr) {
-  if (a.ta != TA || a.tb != TB) return hipErrorInvalidValue;
+  if (a.ta != TA || a.tb != TB || (prp && !BAT)) return hipErrorInvalidValue;
   a.pend = net.pend;
   net.pend.n = 0;
   MMProbs<T> pr{};
@@ -1188,12 +1189,14 @@ hipError_t mm(MlpNet<T>& net, MMArgs<T>& a, const MMProbs<T>* prp = nullptr) {
   hipStream_t st = net.st;
   auto go = [&](auto mkc) {
     constexpr int MK = decltype(mkc)::value;
-    if (pr.n > 0) {
-      if (av && bv) hipLaunchKernelGGL((k_mmb<T, EPI, AOP, BOP, TA, TB, !TA, TB, MK>), grid, blk, 0, st, a, pr);
-      else if (av) hipLaunchKernelGGL((k_mmb<T, EPI, AOP, BOP, TA, TB, !TA, 0, MK>), grid, blk, 0, st, a, pr);
-      else if (bv) hipLaunchKernelGGL((k_mmb<T, EPI, AOP, BOP, TA, TB, 0, TB, MK>), grid, blk, 0, st, a, pr);
-      else hipLaunchKernelGGL((k_mmb<T, EPI, AOP, BOP, TA, TB, 0, 0, MK>), grid, blk, 0, st, a, pr);
-      return;
+    if constexpr (BAT) {
+      if (pr.n > 0) {
+        if (av && bv) hipLaunchKernelGGL((k_mmb<T, EPI, AOP, BOP, TA, TB, !TA, TB, MK>), grid, blk, 0, st, a, pr);
+        else if (av) hipLaunchKernelGGL((k_mmb<T, EPI, AOP, BOP, TA, TB, !TA, 0, MK>), grid, blk, 0, st, a, pr);
+        else if (bv) hipLaunchKernelGGL((k_mmb<T, EPI, AOP, BOP, TA, TB, 0, TB, MK>), grid, blk, 0, st, a, pr);
+        else hipLaunchKernelGGL((k_mmb<T, EPI, AOP, BOP, TA, TB, 0, 0, MK>), grid, blk, 0, st, a, pr);
+        return;
+      }
     }
     if (av && bv) hipLaunchKernelGGL((k_mm<T, EPI, AOP, BOP, TA, TB, !TA, TB, MK>), grid, blk, 0, st, a);
     else if (av) hipLaunchKernelGGL((k_mm<T, EPI, AOP, BOP, TA, TB, !TA, 0, MK>), grid, blk, 0, st, a);
@@ -1340,7 +1343,7 @@ hipError_t mlp_layer1_batch(MlpNet<T>& net, const T* const* W1, T* const* out, i
     pr.p[p].A = net.X; pr.p[p].B = W1[p]; pr.p[p].C = out[p];
   }
   mm_set<T>(a, net.B, net.n_mid, net.n_in, net.X, net.n_in, 0, W1[0], net.n_in, 1, out[0], net.n_mid);
-  return mm<T, MM_STORE, 0, 1>(net, a, &pr);
+  return mm<T, MM_STORE, 0, 1, OP_PLAIN, OP_PLAIN, true>(net, a, &pr);
 }
 
 // One sub-step's share of a batched launch: its positions, masks, scratch net (ga2, ga1, gz and the
@@ -1431,7 +1434,7 @@ hipError_t mlp_forward_batch(MlpNet<T>& net, const SubStep<T>* ss, int np) {
   MMArgs<T> a;
   MMProbs<T> pr{};
   l23_build(net, sp, np, 0, a, pr);
-  return mm<T, MM_L23, 0, 1, OP_H1>(net, a, &pr);
+  return mm<T, MM_L23, 0, 1, OP_H1, OP_PLAIN, true>(net, a, &pr);
 }
 
 // mask kind of a launch (one per launch: every sub-grid reads the same kind)
@@ -1974,7 +1977,7 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
           MMArgs<T> a;
           MMProbs<T> pr{};
           l23_build(net, fa, na, 0, a, pr);
-          HMCX_HIP(ctx, (mm<T, MM_L23, 0, 1, OP_H1>(net, a, &pr)));
+          HMCX_HIP(ctx, (mm<T, MM_L23, 0, 1, OP_H1, OP_PLAIN, true>(net, a, &pr)));
           HMCX_HIP(ctx, mlp_l23_ga1<T>(net, fb, nb, ga, nga));
           // the W1 gradient with every pending bias / W3 update in its extra plane; then the next
           // iteration's layer 1 beside this iteration's W2 gradient (which needs neither)
@@ -2096,17 +2099,26 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
   return HMCX_OK;
 }
 
+// HMCX_MLP_DTYPES (bit 0 float, bit 1 double; both by default): the build compiles this file once per
+// dtype (__graft_entry__.UNITS), so the two halves of its template instantiations build in parallel.
+#ifndef HMCX_MLP_DTYPES
+#define HMCX_MLP_DTYPES 3
+#endif
+#if HMCX_MLP_DTYPES & 1
 template int mlp_masks_t<float>(hmcx_ctx*, int, int, uint64_t, uint32_t, uint32_t, uint32_t, void*);
-template int mlp_masks_t<double>(hmcx_ctx*, int, int, uint64_t, uint32_t, uint32_t, uint32_t, void*);
 template int mlp_grad_t<float>(hmcx_ctx*, const void*, const int32_t*, int, int, int, int, const hmcx_mlp_params*,
                                const void*, double, hmcx_mlp_params*, double*);
-template int mlp_grad_t<double>(hmcx_ctx*, const void*, const int32_t*, int, int, int, int, const hmcx_mlp_params*,
-                                const void*, double, hmcx_mlp_params*, double*);
 template int mlp_loss_t<float>(hmcx_ctx*, const void*, const int32_t*, int, int, int, int, const hmcx_mlp_params*,
                                const void*, double*, void*);
+template int mlp_sghmc_t<float>(hmcx_ctx*, const hmcx_mlp_sghmc_args*);
+#endif
+#if HMCX_MLP_DTYPES & 2
+template int mlp_masks_t<double>(hmcx_ctx*, int, int, uint64_t, uint32_t, uint32_t, uint32_t, void*);
+template int mlp_grad_t<double>(hmcx_ctx*, const void*, const int32_t*, int, int, int, int, const hmcx_mlp_params*,
+                                const void*, double, hmcx_mlp_params*, double*);
 template int mlp_loss_t<double>(hmcx_ctx*, const void*, const int32_t*, int, int, int, int, const hmcx_mlp_params*,
                                 const void*, double*, void*);
-template int mlp_sghmc_t<float>(hmcx_ctx*, const hmcx_mlp_sghmc_args*);
 template int mlp_sghmc_t<double>(hmcx_ctx*, const hmcx_mlp_sghmc_args*);
+#endif
 
 }  // namespace hmcx

@@ -305,15 +305,19 @@ __device__ inline int p2_decide(unsigned long long* w, unsigned ep, int d) {
   return (int)(cur & 3ull);
 }
 // Waits (bounded) for the launch's decision; on timeout or a raised abort word it proposes abort —
-// and adopts whatever was decided first.  A decided abort raises the context's sticky abort word.
+// and adopts whatever was decided first.  Only a decided abort raises the context's sticky abort word
+// (and records where): a COMMIT that lands between the last load and the swap leaves the word down,
+// so the next launch is not stopped for nothing.
 __device__ inline int p2_wait_decision(unsigned long long* w, unsigned ep, int* abort_flag) {
   unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   for (int spins = 0;; ++spins) {
     const unsigned long long cur = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if ((cur >> 2) == (unsigned long long)ep) return (int)(cur & 3ull);
-    if ((spins & 63) == 63 && p2_spin_over(t0, abort_flag, -1, ep)) {
+    if ((spins & 63) == 63 &&
+        (__builtin_amdgcn_s_memrealtime() - t0 > QTIMEOUT ||
+         __hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
       const int d = p2_decide(w, ep, P2_ABORT);
-      if (d == P2_ABORT) __hip_atomic_store(abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (d == P2_ABORT) p2_timeout(abort_flag, -1, ep);
       return d;
     }
     if (HMCX_P2_SLEEP) __builtin_amdgcn_s_sleep(1);

@@ -348,10 +348,13 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
 
   // ---- phase A: partial logits X[R_r,F_f]·W[F_f] → XA(par, r, f) [nrow][KC], then A-RS consume:
   //      Zo[ii][k] = Σ_f' partials of my rows (f' order)
-  auto roundA = [&]() -> bool {
+  // Two A rounds may be in flight (the step-start round of E_current and iteration 0's): each is
+  // published into region parity `par` with its own epoch (epA[par]), and consumed from the same.
+  unsigned epA[2] = {0u, 0u};
+  auto roundA = [&](int par) -> bool {
     const int tid = opaque((int)threadIdx.x), lane = tid & 63, wave = tid >> 6, lr = lane & 15;   // not hoisted (registers)
-    ++ep;
-    const int reg = a.oXA + (((int)(uA & 1) * Gr + r) * Gf + f) * Br * KC;
+    epA[par] = ++ep;
+    const int reg = a.oXA + ((par * Gr + r) * Gf + f) * Br * KC;
     // zero-padded tail skipped; config 2: 49 features in every feature team → 13 k-steps (a constant:
     // the k loop unrolls completely)
     const int nkp = SP ? 13 : WPA == 1 ? (nfeat + 3) / 4 : (BfP / 4) / WPA;
@@ -363,7 +366,7 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int row = mt * 16 + M::row(lane, q);
-          if (row < nrow && lr < KC) put_t(al2, rs, reg + row * KC + lr, (double)c[q], ep);
+          if (row < nrow && lr < KC) put_t(al2, rs, reg + row * KC + lr, (double)c[q], epA[par]);
         }
       } else {
 #pragma unroll
@@ -376,14 +379,15 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
         const int i = e / KC, k = e - (e / KC) * KC;
         T v = Zp[i * 16 + k];
         for (int p = 1; p < WPA; ++p) v += Zp[(p * Br + i) * 16 + k];
-        put_t(al2, rs, reg + e, (double)v, ep);
+        put_t(al2, rs, reg + e, (double)v, epA[par]);
       }
     }
     return true;
   };
-  auto consumeA = [&]() -> bool {
+  auto consumeA = [&](int par) -> bool {
     const int tid = opaque((int)threadIdx.x), lane = tid & 63, wave = tid >> 6, lr = lane & 15;   // not hoisted (registers)
-    const int base0 = a.oXA + ((int)(uA & 1) * Gr + r) * Gf * Br * KC;
+    const int base0 = a.oXA + (par * Gr + r) * Gf * Br * KC;
+    const unsigned ep = epA[par];
     ++uA;
     if (spread & 1) {
       const int ni = nro * KC;
@@ -438,10 +442,13 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
     double kb0 = 0.0;
     for (int k = 0; k < K; ++k) kb0 += (double)pbsh[k] * (double)pbsh[k];
 
-    // ---- it = -1: log-likelihood of my rows at the step-start state (E_current)
+    // ---- it = -1: log-likelihood of my rows at the step-start state (E_current).  (Round 5 measured
+    //      issuing iteration 0's A round before consuming this one, both rounds in flight: 1.724 vs
+    //      1.701 ms per driver-shape launch, 3 A/B pairs — slower, not kept.)
     double ll0 = 0.0, ll_last = 0.0;
     prof.stamp(11);
-    roundA();
+    const int parm1 = (int)(uA & 1);
+    roundA(parm1);
     if (n > 0) {
       // iteration 0's drift of the whole F_f slice by p0 (every member computes it identically;
       // sghmc.py:32), by the waves that do not poll this A-RS round, while the partials travel —
@@ -463,7 +470,7 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
         }
       }
     }
-    if (!consumeA()) return;
+    if (!consumeA(parm1)) return;
     {
       const int k = lane & 15, grp = tid >> 4;
       const bool kv = k < K;
@@ -496,7 +503,8 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
 
       // ===== A-RS: partial logits → owners of the row slices
       prof.stamp(1);
-      roundA();
+      const int parA = (int)(uA & 1);
+      roundA(parA);
       tstamp(s, it, 0);
       // B-AR: the previous iteration's bias sub-step runs here, after this workgroup's A partials went
       // out (it only has to be done before the softmax), then b' of this iteration
@@ -529,7 +537,7 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
         if (tid < K) zb = noise1<T>(a, s, (uint32_t)(it + 1), (uint32_t)(D * K + tid));
       }
       prof.stamp(3);
-      if (!consumeA()) return;
+      if (!consumeA(parA)) return;
       if (zoff) {                                       // consumeA ended in a barrier
         zn = own ? zbuf[tid] : T(0);
         zb = tid < K ? zbuf[nfo * KC + tid] : T(0);

@@ -55,7 +55,7 @@ template <typename T> struct WideArgs {
   int wt;                                // slab / diff stored write-through (sc1; HMCX_WIDE_WT=0: plain)
   // fused forward + softmax (k_wfwd_sm): the row team's partial logits travel as tagged granules
   char* gx; int gx_bytes; unsigned ep;   // the context's granule arena and this launch's epoch
-  int* abort_flag;                       // the context's sticky abort word (raised on a timed-out poll)
+  int* abort_flag;                       // the wide forward's own abort word (raised on a timed-out poll)
   int force_abort;                       // test knob (HMCX_WIDE_FORCE_ABORT): workgroup 0 raises the word
   T* trace; int P;                       // out_trace row of this step ([C][P]: W of chain c as [D][K], then b), or null
 };
@@ -247,7 +247,7 @@ template <typename T> __device__ inline T wide_ld(__amdgpu_buffer_rsrc_t rs, int
 // (hmcx_granule.h), workgroup z owns rows [z·R, z·R + R) (R = ⌈32/S⌉), gathers their S partials
 // (pairs dealt over all threads, landing in LDS), sums them in slice order — the order k_wsoft sums
 // the slab in, so the logits are bit-identical — and runs the softmax rows.  The grid must be
-// co-resident (checked on the host); polls are bounded (2 s) and raise the context's abort word.
+// co-resident (checked on the host); polls are bounded (2 s) and raise the wide abort word.
 constexpr int WSM_STAGE = 8 * WTH;       // gathered (slice, row, class) partials per workgroup (LDS)
 template <typename T, int KB>
 __global__ __launch_bounds__(WTH) void k_wfwd_sm(WideArgs<T> a) {
@@ -410,16 +410,22 @@ __device__ inline double wide_noise(const WideArgs<T>& a, int ch, uint32_t e) {
 // workgroups, 129 CUs with two and twice the load traffic and MFMA issue of the others).  The bias
 // gradient Σ_rows diff falls out of the same diff loads; feature tile 0 of each group applies it (no
 // bias block, no column-sum partials from k_wsoft).
+// Group widths are even (config 5: 20 + 18), so a group's first class starts a 16-byte pair: the f64
+// kernel with two column tiles loads its diff operands as class PAIRS (one 16-byte load per lane and
+// row: classes c0 + 2·lr and c0 + 2·lr + 1), and its two accumulators hold the even and the odd classes
+// of the group — one load instruction per k-step instead of two, and fewer, fuller L2 requests
+// (the gradient's load phase is bound by the requests a CU keeps in flight).
 struct WGroups { int G, GW, NT; };
 __host__ __device__ inline WGroups wide_groups(int K) {
   if (K <= 16) return {1, K, 1};
-  const int gw = (K + 1) / 2;
+  const int gw = ((K + 1) / 2 + 1) & ~1;
   return {2, gw, (gw + 15) / 16};
 }
 
 template <typename T, int NT, int U>
 __global__ __launch_bounds__(GTH) void k_wgrad(WideArgs<T> a) {
   using M = mfma16<T>;
+  constexpr bool PAIR = NT == 2 && sizeof(T) == 8;    // class-pair operands (wide_groups)
   __shared__ T red[GNW][16][NT * 16 + 1];
   __shared__ T cs[GNW][NT * 16];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lg = lane >> 4;
@@ -443,8 +449,8 @@ __global__ __launch_bounds__(GTH) void k_wgrad(WideArgs<T> a) {
   bool cok[NT];
 #pragma unroll
   for (int j = 0; j < NT; ++j) {
-    col[j] = c0 + j * 16 + lr;
-    cok[j] = col[j] < c1;
+    col[j] = PAIR ? c0 + 2 * lr + j : c0 + j * 16 + lr;      // PAIR: col[0] even, col[1] = col[0] + 1
+    cok[j] = PAIR ? c0 + 2 * lr < c1 : col[j] < c1;
   }
   // my epilogue element: feature d0 + tid / GW, class c0 + tid % GW (threads 0 … 16·GW − 1)
   const int ei = tid / gr.GW, ek = c0 + (tid - (tid / gr.GW) * gr.GW);
@@ -467,13 +473,22 @@ __global__ __launch_bounds__(GTH) void k_wgrad(WideArgs<T> a) {
       const bool ok = ks + u < kb1 && row < B;
       const size_t rr = ok ? (size_t)row : 0;
       av[u] = a.X[rr * a.D + dcol];
+      if constexpr (PAIR) {
+        // classes c0 + 2·lr, c0 + 2·lr + 1 (the odd one may be the padding past c1: its column is unused)
+        const int off = (ok && cok[0]) ? (row * KP + col[0]) * (int)sizeof(T) : 0x7fffffff;
+        typedef double dd2 __attribute__((ext_vector_type(2)));
+        const dd2 q = __builtin_bit_cast(dd2, __builtin_amdgcn_raw_buffer_load_b128(drs, off, 0, 0));
+        bv[u][0] = (T)q.x;
+        bv[u][1] = (T)q.y;
+      } else {
 #pragma unroll
-      for (int j = 0; j < NT; ++j) {
-        const int off = (ok && cok[j]) ? (row * KP + col[j]) * (int)sizeof(T) : 0x7fffffff;
-        if constexpr (sizeof(T) == 8)
-          bv[u][j] = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(drs, off, 0, 0));
-        else
-          bv[u][j] = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(drs, off, 0, 0));
+        for (int j = 0; j < NT; ++j) {
+          const int off = (ok && cok[j]) ? (row * KP + col[j]) * (int)sizeof(T) : 0x7fffffff;
+          if constexpr (sizeof(T) == 8)
+            bv[u][j] = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(drs, off, 0, 0));
+          else
+            bv[u][j] = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(drs, off, 0, 0));
+        }
       }
       if (!(ok && dok)) av[u] = T(0);
     }
@@ -495,13 +510,14 @@ __global__ __launch_bounds__(GTH) void k_wgrad(WideArgs<T> a) {
   WSTAMP(2);
 #pragma unroll
   for (int j = 0; j < NT; ++j) {
+    const int cc = PAIR ? 2 * lr + j : j * 16 + lr;     // class of accumulator column lr, within the group
 #pragma unroll
-    for (int q = 0; q < 4; ++q) red[wave][M::row(lane, q)][j * 16 + lr] = acc[j][q];
+    for (int q = 0; q < 4; ++q) red[wave][M::row(lane, q)][cc] = acc[j][q];
     // the four row groups of a column (lanes lr, lr + 16, lr + 32, lr + 48), symmetric pairs
     T v = csum[j];
     v += __shfl_xor(v, 16, 64);
     v += __shfl_xor(v, 32, 64);
-    if (lg == 0) cs[wave][j * 16 + lr] = v;
+    if (lg == 0) cs[wave][cc] = v;
   }
   __syncthreads();
   WSTAMP(3);
@@ -656,7 +672,10 @@ static int sgld_wide_impl(hmcx_ctx* ctx, const hmcx_sampler_args* s, bool allow_
   int rc;
   unsigned ep0 = 0;
   if (fuse) {
-    if ((rc = abort_precheck(ctx))) return rc;
+    if (!ctx->wide_abort_dev) {        // its own word (hmcx_internal.h), allocated on first use
+      HMCX_HIP(ctx, hipMalloc((void**)&ctx->wide_abort_dev, sizeof(int)));
+      HMCX_HIP(ctx, hipMemsetAsync(ctx->wide_abort_dev, 0, sizeof(int), ctx->stream));
+    }
     unsigned nfwd = 0;
     for (int i = 0; i < s->n_steps; ++i) nfwd += 1u + ((s->want_ll && s->want_ll[i] && s->out_ll) ? 1u : 0u);
     if ((rc = gx_reserve(ctx, (size_t)nRB * S * C * WRB * K * 16))) return rc;
@@ -675,7 +694,7 @@ static int sgld_wide_impl(hmcx_ctx* ctx, const hmcx_sampler_args* s, bool allow_
   const int force_abort = getenv("HMCX_WIDE_FORCE_ABORT") ? atoi(getenv("HMCX_WIDE_FORCE_ABORT")) : -1;
   WideArgs<T> a{};
   a.gx = ctx->gx_arena; a.gx_bytes = (int)std::min<size_t>(ctx->gx_bytes, 0x7fffffff);
-  a.abort_flag = ctx->abort_dev;
+  a.abort_flag = ctx->wide_abort_dev;        // polled only by k_wfwd_sm (null before the first fused call)
   a.W = (T*)s->W; a.b = (T*)s->b; a.pW = (T*)s->pW; a.pb = (T*)s->pb;
   a.B = B; a.D = D; a.K = K; a.KP = KP; a.S = S; a.Dz = Dz; a.nSB = nSB; a.C = C;
   a.slab = slab; a.diff = diff; a.llp = llp;
@@ -744,14 +763,17 @@ static int sgld_wide_impl(hmcx_ctx* ctx, const hmcx_sampler_args* s, bool allow_
   if ((rc = gs.finish())) return rc;
   if ((rc = timing_end(ctx, ctx->stream))) return rc;
   if (fuse) {
-    // a timed-out team round raised the abort word (the launch's workgroups then stopped early): put the
-    // call's start state back, lower the word and run the call again on the three-launch path — same
-    // operands, same noise, so the result is the one the fused call would have given
+    // a timed-out team round raised the wide abort word (the launch's workgroups then stopped early): put
+    // the call's start state back, lower the word and run the call again on the three-launch path — same
+    // operands, same noise, so the result is the one the fused call would have given.  The check waits
+    // for the stream, so a fused hmcx_sgld_run call returns only when its kernels are done (one wait
+    // per call: sample() makes one call per epoch); the re-run is counted (hmcx_get_recoveries)
     int flag = 0;
-    HMCX_HIP(ctx, hipMemcpyAsync(&flag, ctx->abort_dev, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    HMCX_HIP(ctx, hipMemcpyAsync(&flag, ctx->wide_abort_dev, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
     HMCX_HIP(ctx, hipStreamSynchronize(ctx->stream));
     if (flag) {
-      HMCX_HIP(ctx, hipMemsetAsync(ctx->abort_dev, 0, ABORT_WORDS * sizeof(int), ctx->stream));
+      HMCX_HIP(ctx, hipMemsetAsync(ctx->wide_abort_dev, 0, sizeof(int), ctx->stream));
+      ++ctx->recoveries[HMCX_RECOVERY_WIDE_FUSED];
       HMCX_HIP(ctx, hipMemcpyAsync(s->W, snapW, nW * sizeof(T), hipMemcpyDeviceToDevice, ctx->stream));
       HMCX_HIP(ctx, hipMemcpyAsync(s->b, snapb, nb * sizeof(T), hipMemcpyDeviceToDevice, ctx->stream));
       if (snappW) {

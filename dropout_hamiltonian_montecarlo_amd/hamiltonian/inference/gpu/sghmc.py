@@ -444,6 +444,7 @@ class sghmc(sgmcmc):
             for k, t in zip(MLP_PARAM_NAMES, saved):
                 state[k].copy_(t)
             ctx.set_mlp_fuse(False)
+            ctx.note_recovery("mlp_fused")
             ctx.check(ctx.lib.hmcx_mlp_sghmc_run(ctx.h, a), "hmcx_mlp_sghmc_run (unfused re-run)")
         self.global_step += n_steps
         h = {k: v.cpu().numpy() for k, v in outs.items()}

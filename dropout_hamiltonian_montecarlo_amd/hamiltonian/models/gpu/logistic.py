@@ -14,6 +14,13 @@ from dropout_hamiltonian_montecarlo_amd._native import HmcxError, context, dtype
 from .softmax import _batch, as_device
 
 
+
+def _log0(x):
+    """np.log without the divide-by-zero RuntimeWarning at α = 0 (−inf, as the reference computes it:
+    its model files silence warnings, models/cpu/softmax.py:1-2)."""
+    with np.errstate(divide="ignore"):
+        return np.log(x)
+
 class logistic:
     _hmcx_model = 'logistic'
 
@@ -59,7 +66,7 @@ class logistic:
             dim = v.numel()
             ss = torch.empty(1, dtype=torch.float64, device=self.device)
             ctx.check(ctx.lib.hmcx_sumsq(ctx.h, self.code, ptr(v), dim, ptr(ss)), "hmcx_sumsq")
-            K += dim * 0.5 * np.log(self.hyper['alpha'] / (2 * np.pi))
+            K += dim * 0.5 * _log0(self.hyper['alpha'] / (2 * np.pi))
             K -= 0.5 * self.hyper['alpha'] * ss.item()
         return K
 

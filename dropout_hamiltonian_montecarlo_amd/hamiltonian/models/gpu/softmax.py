@@ -32,6 +32,13 @@ def _batch(args):
     return X, y
 
 
+
+def _log0(x):
+    """np.log without the divide-by-zero RuntimeWarning at α = 0 (−inf, as the reference computes it:
+    its model files silence warnings, models/cpu/softmax.py:1-2)."""
+    with np.errstate(divide="ignore"):
+        return np.log(x)
+
 class softmax:
     _hmcx_model = 'softmax'
 
@@ -99,7 +106,7 @@ class softmax:
         if self.prior == 'cpu':
             for var in par.keys():
                 dim = int(np.prod(tuple(par[var].shape)))
-                K -= 0.5 * dim * np.log(2 * np.pi) - 0.5 * dim * np.log(self.hyper['alpha'])
+                K -= 0.5 * dim * np.log(2 * np.pi) - 0.5 * dim * _log0(self.hyper['alpha'])
             return K
         ctx = context(self.device)
         for var in par.keys():                                            # gpu/softmax.py:29-39
@@ -116,7 +123,7 @@ class softmax:
         K = 0
         for shp in shapes:
             dim = int(np.prod(shp))
-            K -= 0.5 * dim * np.log(2 * np.pi) - 0.5 * dim * np.log(self.hyper['alpha'])
+            K -= 0.5 * dim * np.log(2 * np.pi) - 0.5 * dim * _log0(self.hyper['alpha'])
         return K
 
     def negative_log_posterior(self, par, **args):                        # softmax.py:74-79

@@ -209,6 +209,24 @@ int hmcx_host_wait(hmcx_ctx* ctx, const void* out_host);
  * which lowers the word (stream-ordered) and drops the deferred checks still pending. */
 int hmcx_clear_abort(hmcx_ctx* ctx);
 
+/* Fallback bookkeeping.  Every path that re-runs work after a timed-out cross-workgroup exchange
+ * is counted per context, so a test suite, smoke check or benchmark can require that none happened
+ * (a re-run gives the right result, which is exactly why it must not go unnoticed):
+ *   HMCX_RECOVERY_PERSISTENT  hmcx_clear_abort calls: the caller re-runs persistent SGHMC calls
+ *   HMCX_RECOVERY_MLP_FUSED   hmcx_mlp_sghmc_run calls re-run unfused after their out_abort verdict
+ *                             (the host code that re-runs records it: hmcx_note_recovery)
+ *   HMCX_RECOVERY_WIDE_FUSED  hmcx_sgld_run calls whose fused forward + softmax timed out and that
+ *                             re-ran on the three-launch path inside the call
+ * counts: host int64_t[HMCX_RECOVERY_KINDS], totals since hmcx_create. */
+enum hmcx_recovery {
+  HMCX_RECOVERY_PERSISTENT = 0,
+  HMCX_RECOVERY_MLP_FUSED = 1,
+  HMCX_RECOVERY_WIDE_FUSED = 2,
+  HMCX_RECOVERY_KINDS = 3
+};
+int hmcx_get_recoveries(const hmcx_ctx* ctx, int64_t* counts);
+int hmcx_note_recovery(hmcx_ctx* ctx, int kind);
+
 /* Host-side Philox schedule of noise='philox' SGHMC steps (sghmc.py:25 path length, :36 accept
  * uniform), bit-identical to the device generator: for step s < n_steps and chain c < C
  *   L[s*C+c] = ceil(2·u_path·path_length / eps[s]),  n_iter = max(0, L − 1),  u = u_accept

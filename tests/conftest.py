@@ -10,6 +10,8 @@ if REPO not in sys.path:
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device); run with -m gpu")
+    config.addinivalue_line("markers", "allow_recovery: the test forces a timed-out exchange on purpose, so "
+                                       "a re-run (include/hmcx.h hmcx_get_recoveries) is expected")
 
 
 @pytest.fixture(scope="session")
@@ -17,15 +19,41 @@ def golden_dir():
     return os.path.join(REPO, "tests", "golden")
 
 
-@pytest.fixture(autouse=True)
-def _reset_sghmc_path(request):
-    """GPU tests share one hmcx context per device: a test that picks an SGHMC path (1 kernels, 2 the
-    2-D persistent kernel, 3 row space) must not leave it for the next test."""
-    yield
-    if request.node.get_closest_marker("gpu") is None:
-        return
+def _contexts():
     nat = sys.modules.get("dropout_hamiltonian_montecarlo_amd._native")
-    if nat is None:
+    return nat, list(getattr(nat, "_ctxs", {}).values()) if nat is not None else []
+
+
+@pytest.fixture(autouse=True)
+def _gpu_context_guard(request):
+    """GPU tests share one hmcx context per device.
+
+    - No silent fallback: a GPU test fails if any re-run after a timed-out exchange happened during it
+      (persistent SGHMC, fused MLP, fused wide SGLD; include/hmcx.h hmcx_get_recoveries) — a fallback
+      gives the oracle's result, which is exactly why the parity tests alone cannot see it.  Tests that
+      force a timeout carry @pytest.mark.allow_recovery.
+    - A test that picks an SGHMC path (1 kernels, 2 persistent) or turns the fused MLP launches off must
+      not leave that choice to the next test."""
+    gpu = request.node.get_closest_marker("gpu") is not None
+    before = {}
+    if gpu:
+        nat, ctxs = _contexts()
+        before = {id(c): c.recoveries() for c in ctxs if getattr(c, "h", None)}
+    yield
+    if not gpu:
         return
-    for ctx in list(getattr(nat, "_ctxs", {}).values()):
-        ctx.set_sghmc_path(0)
+    nat, ctxs = _contexts()
+    moved = {}
+    for c in ctxs:
+        if not getattr(c, "h", None):
+            continue
+        now = c.recoveries()
+        was = before.get(id(c), dict.fromkeys(now, 0))
+        d = {k: now[k] - was[k] for k in now if now[k] != was[k]}
+        if d:
+            moved[str(c.device)] = d
+        c.set_sghmc_path(0)
+        if not c.mlp_fuse:
+            c.set_mlp_fuse(True)
+    if moved and request.node.get_closest_marker("allow_recovery") is None:
+        pytest.fail("silent fallback: re-runs after timed-out exchanges during this test: %s" % moved)

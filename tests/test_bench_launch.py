@@ -31,6 +31,13 @@ def test_bench_spawns_n_ranks_dry_run(n):
     # sum over ranks of 10·(r+1) leapfrogs, max over ranks of 1 ms·(r+1)
     assert d["leapfrogs"] == 10.0 * n * (n + 1) / 2
     assert abs(d["t_max"] - 0.001 * n) < 1e-12
+    # both aggregates of the N-GPU line from the gathered per-rank numbers (bench.aggregate_ranks):
+    # makespan Σ lf / max t and chain throughput Σ lf_r / t_r, each × P = 7850
+    rk = d["ranks"]
+    assert rk["per_rank_leapfrogs"] == [10.0 * (r + 1) for r in range(n)]
+    assert rk["per_rank_ms"] == pytest.approx([1.0 * (r + 1) for r in range(n)])
+    assert rk["value_makespan"] == pytest.approx(10.0 * n * (n + 1) / 2 / (0.001 * n) * 7850)
+    assert rk["value_chain_throughput"] == pytest.approx(n * 10000.0 * 7850)
     envs = d["rank_env"]
     assert [e["RANK"] for e in envs] == [str(r) for r in range(n)]
     assert [e["LOCAL_RANK"] for e in envs] == [str(r) for r in range(n)]
@@ -60,3 +67,25 @@ def test_bench_respects_external_launcher_env():
     assert all(p.returncode == 0 for p in procs), [o[1][-2000:] for o in outs]
     d = json.loads([ln for ln in outs[0][0].splitlines() if ln.startswith("{")][-1])
     assert d["n_gpus"] == 2 and not [ln for ln in outs[1][0].splitlines() if ln.startswith("{")]
+
+
+def test_aggregate_ranks_hand_computed():
+    sys.path.insert(0, REPO)
+    import bench
+    per = [{"leapfrogs": 182, "seconds": 1.70e-3}, {"leapfrogs": 234, "seconds": 2.11e-3}]
+    a = bench.aggregate_ranks(per, P_dim=1)
+    assert a["value_makespan"] == pytest.approx((182 + 234) / 2.11e-3)
+    assert a["value_chain_throughput"] == pytest.approx(182 / 1.70e-3 + 234 / 2.11e-3)
+    assert a["per_rank_leapfrogs"] == [182.0, 234.0]
+
+
+def test_predicted_scaling_uses_the_device_schedule():
+    """The host twin of the Philox schedule gives chains 0-7 the timed leapfrogs of the driver's shape
+    (--steps 20 --warmup 5); chain 0's 182 is what BENCH_r04 measured on the GPU."""
+    sys.path.insert(0, REPO)
+    import bench
+    pr = bench.predicted_scaling(5, 20)
+    assert pr["chain_leapfrogs"] == [182, 159, 196, 183, 148, 198, 234, 198]
+    assert pr["1"]["makespan"] == pytest.approx(1.0) and pr["1"]["chain_throughput"] == pytest.approx(1.0)
+    # makespan is held back by the slowest chain (234 leapfrogs); chain throughput is not
+    assert 6.0 < pr["8"]["makespan"] < 7.2 and 7.5 < pr["8"]["chain_throughput"] < 8.5

@@ -291,6 +291,7 @@ def _mlp_f64_run(monkeypatch=None, force=None):
     return post, logp, s.trace, m
 
 
+@pytest.mark.allow_recovery
 def test_mlp_fused_timeout_is_recovered_in_process(monkeypatch, capfd):
     """A fused MLP launch whose exchange times out (forced) makes its call report out_abort; the
     sampler restores the state, re-runs the call unfused and continues: the trajectory equals the
@@ -302,6 +303,7 @@ def test_mlp_fused_timeout_is_recovered_in_process(monkeypatch, capfd):
         err = capfd.readouterr().err
         assert "re-running the call unfused" in err
         assert not m.ctx.mlp_fuse
+        assert m.ctx.recoveries()["mlp_fused"] >= 1                   # counted (hmcx_get_recoveries)
         assert [t["L"] for t in tr] == [t["L"] for t in ref_tr]
         assert [t["accepted"] for t in tr] == [t["accepted"] for t in ref_tr]
         for k in ref_post:
@@ -311,6 +313,7 @@ def test_mlp_fused_timeout_is_recovered_in_process(monkeypatch, capfd):
         m.ctx.set_mlp_fuse(True)
 
 
+@pytest.mark.allow_recovery
 def test_mlp_timeout_leaves_softmax_persistent_path_alone(monkeypatch):
     """The MLP abort word is its own: after a forced MLP timeout the persistent single-chain softmax
     SGHMC kernel (which has its own sticky word) still runs and matches the oracle."""

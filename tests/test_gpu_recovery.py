@@ -1,5 +1,4 @@
-"""In-process recovery of the persistent single-chain SGHMC kernels (csrc/hmcx_persist2.hip,
-csrc/hmcx_rowspace.hip).
+"""In-process recovery of the persistent single-chain SGHMC kernel (csrc/hmcx_persist2.hip).
 
 A launch whose workgroups time out in a hand-off writes nothing to W/b and raises the context's
 sticky abort word, so every launch queued behind it returns untouched too (include/hmcx.h
@@ -12,7 +11,7 @@ import os
 import numpy as np
 import pytest
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.allow_recovery]
 
 torch = pytest.importorskip("torch")
 
@@ -42,7 +41,9 @@ def test_forced_abort_is_recovered_in_process(name, path, monkeypatch, capfd):
     """HMCX_P2_FORCE_ABORT=1: in every persistent launch the last workgroup gives up at step 1
     (the other workgroups then abort in their polls) — the first epoch's call and the one already
     queued behind it (sample() pipelines epoch calls) are both re-run."""
+    from dropout_hamiltonian_montecarlo_amd import _native as nat
     c = gi.TRAJ_CONFIGS[name]
+    before = nat.recoveries_all()["persistent_sghmc"]
     monkeypatch.setenv("HMCX_P2_FORCE_ABORT", "1")
     try:
         got = _run_gpu(c, path=path)
@@ -50,6 +51,7 @@ def test_forced_abort_is_recovered_in_process(name, path, monkeypatch, capfd):
         _restore_path()
     err = capfd.readouterr().err
     assert "hand-off timed out" in err
+    assert nat.recoveries_all()["persistent_sghmc"] > before        # counted (hmcx_get_recoveries)
     _check_vs_oracle(c, got)
 
 
@@ -109,6 +111,17 @@ def test_abort_word_reported_through_c_abi(monkeypatch):
         assert m.ctx.lib.hmcx_synchronize(m.ctx.h) != 0
         assert b"timed out" in m.ctx.lib.hmcx_last_error(m.ctx.h)
         torch.testing.assert_close(st["weights"], W0, rtol=0, atol=0)      # untouched
+        # the persistent word is still raised: a fused wide-SGLD call on the same context polls its own
+        # word (hmcx_internal.h wide_abort_dev), so it neither fails nor re-runs, and matches the oracle
+        wide = dict(kind="sgld", N=1000, B=500, D=2048, K=38, alpha=0.01, step_size=1e-4, path_length=1.0,
+                    burnin=1, epochs=1, data_seed=41, np_seed=2, rng_seed=3)
+        monkeypatch.setenv("HMCX_SGLD_WIDE", "1")
+        monkeypatch.setenv("HMCX_WIDE_FUSE", "1")
+        rec0 = m.ctx.recoveries()
+        post_g, logp_g, _, _ = _run_gpu(wide)
+        assert m.ctx.recoveries() == rec0
+        post_r, logp_r, _, _ = _run_oracle(wide)
+        np.testing.assert_allclose(post_g["weights"], post_r["weights"], rtol=1e-9, atol=1e-12)
         m.ctx.clear_abort()
         monkeypatch.delenv("HMCX_P2_FORCE_ABORT")
         assert m.ctx.lib.hmcx_sghmc_run(m.ctx.h, a) == 0

@@ -237,6 +237,7 @@ def test_sgld_wide_path_vs_oracle(K, D, B, fuse, monkeypatch):
     assert [l for l in log_g.splitlines() if "loss" in l] == [l for l in log_r.splitlines() if "loss" in l]
 
 
+@pytest.mark.allow_recovery
 def test_sgld_wide_fused_timeout_reruns_unfused(monkeypatch, capfd):
     """A timed-out team round of the fused forward (forced: HMCX_WIDE_FORCE_ABORT=<step> raises the
     abort word in that step's launch) makes the call put its start state back and run again on the
@@ -246,12 +247,15 @@ def test_sgld_wide_fused_timeout_reruns_unfused(monkeypatch, capfd):
     monkeypatch.setenv("HMCX_WIDE_FORCE_ABORT", "1")
     c = dict(kind="sgld", N=1000, B=500, D=2048, K=38, alpha=0.01, step_size=1e-4, path_length=1.0,
              burnin=1, epochs=2, data_seed=41, np_seed=2, rng_seed=3)
+    from dropout_hamiltonian_montecarlo_amd import _native as nat
     post_r, logp_r, _, _ = _run_oracle(c)
+    before = nat.recoveries_all()["sgld_wide_fused"]
     post_g, logp_g, _, _ = _run_gpu(c)
     for v in ("weights", "bias"):
         np.testing.assert_allclose(post_g[v], post_r[v], rtol=1e-9, atol=1e-12)
     np.testing.assert_allclose(logp_g, logp_r, rtol=1e-10)
     assert "re-run on the three-launch path" in capfd.readouterr().err
+    assert nat.recoveries_all()["sgld_wide_fused"] > before          # every forced call counted (hmcx_get_recoveries)
 
 
 @pytest.mark.parametrize("dtype", ["f64", "f32"])

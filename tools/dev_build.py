@@ -30,27 +30,29 @@ def deps(path, seen):
     return seen
 
 
-def stale(src):
-    obj = os.path.join(objdir, os.path.splitext(src)[0] + ".o")
-    if src in force or not os.path.exists(obj):
+def stale(unit):
+    src, objname, _ = unit
+    obj = os.path.join(objdir, objname)
+    if src in force or objname in force or not os.path.exists(obj):
         return True
     t = os.path.getmtime(obj)
     return any(os.path.getmtime(f) > t for f in deps(os.path.join(g.CSRC, src), set()))
 
 
-def compile_one(src):
-    obj = os.path.join(objdir, os.path.splitext(src)[0] + ".o")
-    r = subprocess.run([g._hipcc()] + g.FLAGS + ["-c", os.path.join(g.CSRC, src), "-o", obj],
+def compile_one(unit):
+    src, objname, extra = unit
+    obj = os.path.join(objdir, objname)
+    r = subprocess.run([g._hipcc()] + g.FLAGS + extra + ["-c", os.path.join(g.CSRC, src), "-o", obj],
                        capture_output=True, text=True)
     if r.returncode != 0:
-        sys.exit("hipcc failed for %s:\n%s" % (src, r.stderr[-6000:]))
-    print("compiled", src, flush=True)
+        sys.exit("hipcc failed for %s:\n%s" % (objname, r.stderr[-6000:]))
+    print("compiled", objname, flush=True)
 
 
-todo = [s for s in g.SOURCES if stale(s)]
+todo = sorted([u for u in g.UNITS if stale(u)], key=lambda u: u[0] != "hmcx_mlp.hip")
 with ThreadPoolExecutor(max_workers=8) as ex:
     list(ex.map(compile_one, todo))
-objs = [os.path.join(objdir, os.path.splitext(s)[0] + ".o") for s in g.SOURCES]
+objs = [os.path.join(objdir, u[1]) for u in g.UNITS]
 r = subprocess.run([g._hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", "-o", g.LIB] + objs +
                    ["-ldl", "-Wl,-rpath," + g.ROCM_LIB], capture_output=True, text=True)
 if r.returncode != 0:
