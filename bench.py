@@ -614,8 +614,9 @@ def bench(args, parallel):
         thin.append(st[DIAG_THIN - 1::DIAG_THIN, 0])
         done += n
     s.record_steps = False
-    n_draws, means, M2, tr = parallel.gather_summaries(wf, np.concatenate(thin)[None], device=dev)
-    diag_par = parallel.summary_diagnostics(n_draws, means, M2, tr)
+    # R̂ / split-R̂ / ESS per parameter on the device, where the all-gather left the summaries
+    n_draws, means, M2, tr = parallel.gather_summaries(wf, np.concatenate(thin)[None], device=dev, keep_device=True)
+    diag_par = parallel.summary_diagnostics_device(n_draws, means, M2, tr) if rank == 0 else None
     trace = np.concatenate(lls)[None, :, None]       # [1 chain, T, 1]
     allt = parallel.gather_traces(trace, device=dev)
     diag = parallel.chain_diagnostics(allt) if allt.shape[1] >= 4 else {"rhat": np.nan, "ess": np.nan}

@@ -98,7 +98,7 @@ EXPORTS = ("hmcx_version", "hmcx_create", "hmcx_destroy", "hmcx_last_error", "hm
            "hmcx_sumsq", "hmcx_sgd_run", "hmcx_hmc_run", "hmcx_axpy", "hmcx_mvn_eval",
            "hmcx_clear_abort", "hmcx_get_recoveries", "hmcx_note_recovery", "hmcx_philox_schedule", "hmcx_host_wait", "hmcx_set_mlp_fuse",
            "hmcx_comm_unique_id", "hmcx_comm_init", "hmcx_comm_destroy", "hmcx_allgather_chain_stats",
-           "hmcx_allreduce_f64")
+           "hmcx_allreduce_f64", "hmcx_chain_diagnostics")
 
 _lib = None
 _lock = threading.Lock()
@@ -169,6 +169,9 @@ def load_library():
             lib.hmcx_comm_destroy.argtypes = [c_void_p]
             lib.hmcx_allgather_chain_stats.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_uint64]
             lib.hmcx_allreduce_f64.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_uint64, c_int]
+        if hasattr(lib, "hmcx_chain_diagnostics"):
+            lib.hmcx_chain_diagnostics.argtypes = [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                                                   ctypes.c_int64, c_void_p]
         lib.hmcx_logistic_grad.argtypes = [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
                                            c_void_p, c_void_p, c_double, c_void_p, c_void_p]
         lib.hmcx_logistic_loglik.argtypes = [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int,

@@ -3,8 +3,12 @@
 The reference has no diagnostics (its multi-chain modules only concatenate posteriors,
 /root/reference/hamiltonian/inference/cpu/sghmc_multicore.py:86-94); BASELINE config 4 asks for
 the cross-chain R̂/ESS gather.  Standard definitions (Gelman et al., BDA3 §11.4-11.5):
-split-R̂ over chain halves, ESS with Geyer's initial monotone sequence.  Host NumPy on the
-gathered (small) chain summaries — this runs once per sampling run, not on the hot path.
+split-R̂ over chain halves, ESS with Geyer's initial monotone sequence.
+
+Two implementations of the same definitions: `device_diagnostics` runs them on the GPU where the RCCL
+all-gather leaves the chain summaries (libhmcx hmcx_chain_diagnostics, csrc/hmcx_diag.hip, one thread
+per parameter); the NumPy functions below are the host version used by CPU-only (gloo) runs and as the
+reference the device kernel is tested against (tests/test_gpu_rccl.py).
 """
 import numpy as np
 
@@ -75,3 +79,25 @@ def ess(chains):
     out = np.where(ok, out, np.nan)
     shape = x.shape[2:]
     return out.reshape(shape) if shape else out[0]
+
+
+def device_diagnostics(trace, means=None, M2=None, n=0, device=None):
+    """R̂ from per-chain moments, split-R̂ and ESS per parameter on the device (hmcx_chain_diagnostics).
+    trace: [C, T, P] (a device float64 tensor, e.g. the RCCL all-gather's output, or an array copied to
+    `device`); means / M2: [C, P] over n draws (optional).  Returns numpy arrays (rhat, split_rhat, ess),
+    each [P] (rhat NaN without moments)."""
+    import torch
+    from . import _native as nat
+    dev = trace.device if isinstance(trace, torch.Tensor) else torch.device(device or "cuda")
+    t = torch.as_tensor(trace, dtype=torch.float64, device=dev).contiguous()
+    C, T, P = t.shape
+    mu = m2 = None
+    if means is not None:
+        mu = torch.as_tensor(means, dtype=torch.float64, device=dev).contiguous()
+        m2 = torch.as_tensor(M2, dtype=torch.float64, device=dev).contiguous()
+    out = torch.empty(3 * P, dtype=torch.float64, device=dev)
+    ctx = nat.context(dev)
+    ctx.check(ctx.lib.hmcx_chain_diagnostics(ctx.h, C, T, P, nat.ptr(t), nat.ptr(mu), nat.ptr(m2), int(n),
+                                             nat.ptr(out)), "hmcx_chain_diagnostics")
+    o = out.cpu().numpy().reshape(3, P)
+    return o[0], o[1], o[2]

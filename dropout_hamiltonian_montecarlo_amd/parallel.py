@@ -173,7 +173,7 @@ def gather_objects(obj):
     return out
 
 
-def gather_traces(local_traces, device=None):
+def gather_traces(local_traces, device=None, keep_device=False):
     """All-gather per-chain traces.  local_traces: array [c_local, T, P] (same T, P on every rank;
     c_local may differ, as chain_block gives the first n % world ranks one chain more) → array
     [Σ c_local, T, P] ordered by (rank, local chain).  Uneven blocks are padded to the largest
@@ -187,8 +187,10 @@ def gather_traces(local_traces, device=None):
     if x.shape[0] < cmax:
         x = torch.cat([x, x.new_zeros((cmax - x.shape[0],) + tuple(x.shape[1:]))], dim=0)
     if _rccl is not None:                                        # data plane: one RCCL all-gather
-        allx = _rccl.allgather(x.to(_rccl.ctx.device).reshape(-1)).reshape((world,) + tuple(x.shape)).cpu()
-        out = list(allx)
+        allx = _rccl.allgather(x.to(_rccl.ctx.device).reshape(-1)).reshape((world,) + tuple(x.shape))
+        if keep_device:                                          # stays where the diagnostics kernel reads it
+            return torch.cat([o[:c] for o, c in zip(allx, allc)], dim=0)
+        out = list(allx.cpu())
     else:
         out = [torch.empty_like(x) for _ in range(world)]
         dist.all_gather(out, x)
@@ -222,16 +224,22 @@ class Welford:
         return self
 
 
-def gather_summaries(welford, trace, device=None):
+def gather_summaries(welford, trace, device=None, keep_device=False):
     """All-gather the per-chain summaries of this rank (Welford over [c_local, P], thinned trace
     [c_local, T, P]; the same T, P on every rank, c_local may differ) in one data collective: returns
-    (n, mean [C, P], M2 [C, P], trace [C, T, P]) over all C chains, ordered by rank."""
+    (n, mean [C, P], M2 [C, P], trace [C, T, P]) over all C chains, ordered by rank.  keep_device: the
+    three arrays are device tensors (the RCCL all-gather's own buffer; a copy of them when the gather
+    ran over gloo or there is one rank) for summary_diagnostics_device."""
     c, P = welford.mean.shape
     trace = np.asarray(trace, dtype=np.float64).reshape(c, -1, P)
     T = trace.shape[1]
     packed = np.concatenate([welford.mean[:, None, :], welford.M2[:, None, :], trace], axis=1)   # [c, 2+T, P]
-    allp = gather_traces(packed, device=device)
+    allp = gather_traces(packed, device=device, keep_device=keep_device)
+    if keep_device and not isinstance(allp, torch.Tensor):
+        allp = torch.as_tensor(allp, dtype=torch.float64, device=device)
     n = allreduce_max(welford.n, device=device)
+    if keep_device:
+        return int(n), allp[:, 0, :].contiguous(), allp[:, 1, :].contiguous(), allp[:, 2:2 + T, :].contiguous()
     return int(n), allp[:, 0, :], allp[:, 1, :], allp[:, 2:2 + T, :]
 
 
@@ -262,6 +270,23 @@ def summary_diagnostics(n, means, M2, trace):
         return {"min": float(x.min()), "median": float(np.median(x)), "max": float(x.max())}
     return {"chains": int(means.shape[0]), "draws_per_chain": int(n), "trace_draws_per_chain": int(trace.shape[1]),
             "params": int(means.shape[1]), "rhat": q(r), "split_rhat": q(sr), "ess": q(es)}
+
+
+def summary_diagnostics_device(n, means, M2, trace):
+    """summary_diagnostics with R̂ / split-R̂ / ESS computed on the device (diagnostics.device_diagnostics,
+    hmcx_chain_diagnostics) from the gathered device tensors; the distribution over parameters is taken
+    on the host."""
+    r, sr, es = diagnostics.device_diagnostics(trace, means, M2, n)
+
+    def q(x):
+        x = np.asarray(x, dtype=np.float64).ravel()
+        x = x[np.isfinite(x)]
+        if x.size == 0:
+            return None
+        return {"min": float(x.min()), "median": float(np.median(x)), "max": float(x.max())}
+    return {"chains": int(means.shape[0]), "draws_per_chain": int(n), "trace_draws_per_chain": int(trace.shape[1]),
+            "params": int(means.shape[1]), "rhat": q(r), "split_rhat": q(sr), "ess": q(es),
+            "computed_on": "device (hmcx_chain_diagnostics)"}
 
 
 def chain_diagnostics(all_traces):

@@ -413,6 +413,19 @@ int hmcx_allgather_chain_stats(hmcx_ctx* ctx, hmcx_comm* comm, const double* sen
  * leapfrog total and max-over-ranks time */
 int hmcx_allreduce_f64(hmcx_ctx* ctx, hmcx_comm* comm, const double* send, double* recv, uint64_t count, int op);
 
+/* Cross-chain convergence diagnostics on the device (the reference has none — its
+ * multi-chain layer concatenates posteriors, hamiltonian/inference/cpu/sghmc_multicore.py:86-94,
+ * read back by hmc.py:132-138 backend_mean).  Per parameter p < P of C chains:
+ *   out[p]       R̂ from per-chain moments (means / M2 [C][P] over n_moments draws; NaN when means
+ *                is NULL),
+ *   out[P + p]   split-R̂ of the traces (chains halved: 2C sequences of T/2 draws),
+ *   out[2P + p]  bulk ESS (Geyer's initial monotone sequence on the split sequences),
+ * with the definitions of dropout_hamiltonian_montecarlo_amd/diagnostics.py (BDA3 §11.4-11.5).
+ * trace: device [C][T][P] float64 (T >= 4) — e.g. the buffer hmcx_allgather_chain_stats filled;
+ * means, M2, out: device float64.  Stream-ordered; returns before the kernel completes. */
+int hmcx_chain_diagnostics(hmcx_ctx* ctx, int C, int T, int P, const double* trace, const double* means,
+                           const double* M2, int64_t n_moments, double* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -105,6 +105,18 @@ n, means, M2, tr = parallel.gather_summaries(wu, mine[:, ::2])
 assert means.shape == (5, 3) and tr.shape == (5, 2, 3)
 np.testing.assert_array_equal(means[:, 0], np.arange(5.0))
 assert parallel.gather_objects(rank) == list(range(world))
+# the N-GPU bench line's aggregation (bench.aggregate_ranks) over the gathered per-rank numbers: rank r
+# did 100·(r+1) + 7 leapfrogs in 1.5·(r+1) ms; makespan Σ lf / max t, chain throughput Σ lf_r / t_r
+import bench
+per = parallel.gather_objects({"leapfrogs": 100.0 * (rank + 1) + 7, "seconds": 1.5e-3 * (rank + 1)})
+agg = bench.aggregate_ranks(per, P_dim=1)
+lf = [100.0 * (r + 1) + 7 for r in range(world)]
+ts = [1.5e-3 * (r + 1) for r in range(world)]
+assert agg["per_rank_leapfrogs"] == lf
+assert abs(agg["value_makespan"] - sum(lf) / max(ts)) < 1e-6 * agg["value_makespan"]
+assert abs(agg["value_chain_throughput"] - sum(l / t for l, t in zip(lf, ts))) < 1e-6 * agg["value_chain_throughput"]
+assert world != 2 or abs(agg["value_makespan"] - 314.0 / 3e-3) < 1e-3      # hand-computed: (107 + 207) / 3 ms
+assert world != 2 or abs(agg["value_chain_throughput"] - (107.0 / 1.5e-3 + 207.0 / 3e-3)) < 1e-3
 parallel.barrier()
 parallel.finalize()
 print("ok", rank)
