@@ -65,6 +65,14 @@ class MlpSghmcArgs(ctypes.Structure):
                 ("out_loss", c_void_p), ("out_nlp", c_void_p), ("out_E", c_void_p), ("out_abort", c_void_p)]
 
 
+class MlpLeapfrogArgs(ctypes.Structure):
+    _fields_ = [("dtype", c_int), ("B", c_int), ("n_in", c_int), ("n_mid", c_int), ("n_out", c_int),
+                ("n_iter", c_int), ("order", c_int * 6), ("eps", c_double), ("alpha", c_double),
+                ("X", c_void_p), ("y", c_void_p), ("q", MlpParams), ("p", MlpParams), ("g", MlpParams),
+                ("mask_mode", c_int), ("masks", c_void_p), ("seed", ctypes.c_uint64), ("chain", ctypes.c_uint32),
+                ("step", ctypes.c_uint32), ("slot0", ctypes.c_uint32)]
+
+
 class SgdArgs(ctypes.Structure):
     _fields_ = [("dtype", c_int), ("model", c_int), ("B", c_int), ("D", c_int), ("K", c_int), ("n_steps", c_int),
                 ("alpha", c_double), ("step_size", c_double), ("gamma", c_double),
@@ -86,6 +94,7 @@ class HmcArgs(ctypes.Structure):
 
 MODEL_SOFTMAX, MODEL_LOGISTIC = 0, 1
 MLP_MASK_SLOT0 = 0x80000000
+MLP_MASKS_NONE, MLP_MASKS_FIXED, MLP_MASKS_PHILOX = 0, 1, 2
 
 
 # Every symbol include/hmcx.h declares (checked by tests/test_capi.py).
@@ -94,7 +103,7 @@ EXPORTS = ("hmcx_version", "hmcx_create", "hmcx_destroy", "hmcx_last_error", "hm
            "hmcx_philox_uniforms", "hmcx_philox_normals", "hmcx_philox_normals_f64",
            "hmcx_softmax_grad", "hmcx_softmax_loglik", "hmcx_softmax_predict", "hmcx_sghmc_run",
            "hmcx_sgld_run", "hmcx_hmc_mvn_run", "hmcx_mlp_masks", "hmcx_mlp_grad", "hmcx_mlp_loss",
-           "hmcx_mlp_sghmc_run", "hmcx_logistic_grad", "hmcx_logistic_loglik", "hmcx_logistic_predict",
+           "hmcx_mlp_sghmc_run", "hmcx_mlp_hmc_leapfrog", "hmcx_logistic_grad", "hmcx_logistic_loglik", "hmcx_logistic_predict",
            "hmcx_sumsq", "hmcx_sgd_run", "hmcx_hmc_run", "hmcx_axpy", "hmcx_mvn_eval",
            "hmcx_clear_abort", "hmcx_get_recoveries", "hmcx_note_recovery", "hmcx_philox_schedule", "hmcx_host_wait", "hmcx_set_mlp_fuse",
            "hmcx_comm_unique_id", "hmcx_comm_init", "hmcx_comm_destroy", "hmcx_allgather_chain_stats",
@@ -161,6 +170,8 @@ def load_library():
         lib.hmcx_mlp_loss.argtypes = [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                                       ctypes.POINTER(MlpParams), c_void_p, c_void_p, c_void_p]
         lib.hmcx_mlp_sghmc_run.argtypes = [c_void_p, ctypes.POINTER(MlpSghmcArgs)]
+        if hasattr(lib, "hmcx_mlp_hmc_leapfrog"):
+            lib.hmcx_mlp_hmc_leapfrog.argtypes = [c_void_p, ctypes.POINTER(MlpLeapfrogArgs)]
         if hasattr(lib, "hmcx_set_mlp_fuse"):          # absent in older builds loaded for A/B runs
             lib.hmcx_set_mlp_fuse.argtypes = [c_void_p, c_int]
         if hasattr(lib, "hmcx_comm_init"):

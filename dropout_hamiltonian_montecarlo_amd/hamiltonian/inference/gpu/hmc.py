@@ -14,9 +14,12 @@ Device paths:
   momentum, every kick/drift (fused into the gradient kernels' epilogues), the energies, the MH
   accept and the commit run on the device; the host only draws the schedule (path lengths, accept
   uniforms and, in noise='numpy' mode, the momenta) in the reference's order;
-* other libhmcx models (the MLP): the reference's loop with device gradients (model.grad) and the
-  leapfrog arithmetic / kinetic energies as libhmcx calls (hmcx_axpy, hmcx_sumsq).
+* the MLP: a step's whole leapfrog trajectory is ONE hmcx_mlp_hmc_leapfrog call (device gradients,
+  kicks and drifts enqueued from C in the reference's order); the energies go out as device pieces
+  read back once.  A model that overrides grad (or HMCX_HMC_HOST_LOOP=1) runs the reference's loop
+  with device gradients (model.grad) and hmcx_axpy / hmcx_sumsq from the host instead.
 """
+import os
 import sys
 from copy import deepcopy
 
@@ -27,6 +30,10 @@ from dropout_hamiltonian_montecarlo_amd import _native as nat
 from dropout_hamiltonian_montecarlo_amd._native import HmcxError, ptr
 
 from .sghmc import _n_iter
+
+
+def _host_loop():
+    return os.environ.get("HMCX_HMC_HOST_LOOP", "0") == "1"
 
 
 class hmc:
@@ -316,15 +323,20 @@ class hmc:
         positions, momentums = [deepcopy(state)], [{k: np.asarray(v).astype(npdt) for k, v in p_host.items()}]
         epsilon = self.step_size
         path_length = np.ceil(2 * np.random.rand() * self.path_length / epsilon)
-        grad_q = m.grad(q, **args)
-        for _ in range(_n_iter(path_length)):
+        if hasattr(m, "leapfrog_device") and m.leapfrog_device_ok() and not _host_loop():
+            # the whole trajectory in one libhmcx call (hmcx_mlp_hmc_leapfrog): the same kernels in the
+            # same order as the loop below, enqueued from C
+            m.leapfrog_device(q_new, p_new, _n_iter(path_length), epsilon, list(self.start.keys()), **args)
+        else:
+            grad_q = m.grad(q, **args)
+            for _ in range(_n_iter(path_length)):
+                for var in self.start.keys():
+                    self._axpy(0, 0.5 * epsilon, grad_q[var], p_new[var])      # hmc.py:50
+                    self._axpy(1, epsilon, p_new[var], q_new[var])             # hmc.py:51
+                    grad_q = m.grad(q_new, **args)
+                    self._axpy(0, epsilon, grad_q[var], p_new[var])            # hmc.py:53
             for var in self.start.keys():
-                self._axpy(0, 0.5 * epsilon, grad_q[var], p_new[var])          # hmc.py:50
-                self._axpy(1, epsilon, p_new[var], q_new[var])                 # hmc.py:51
-                grad_q = m.grad(q_new, **args)
-                self._axpy(0, epsilon, grad_q[var], p_new[var])                # hmc.py:53
-        for var in self.start.keys():
-            self._axpy(0, 2.0, p_new[var], p_new[var])                         # hmc.py:55-56: p − 2p = −p
+                self._axpy(0, 2.0, p_new[var], p_new[var])                     # hmc.py:55-56: p − 2p = −p
         E_new, E_cur = self._energies(q_new, p_new, q, p, args)
         acceptprob = min(1, np.exp(E_cur - E_new))
         accepted = bool(np.isfinite(acceptprob) and (np.random.rand() < acceptprob))

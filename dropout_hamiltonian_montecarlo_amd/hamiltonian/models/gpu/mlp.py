@@ -16,10 +16,14 @@ on the device from Philox (hmcx_mlp_masks, keyed by the model's seed and a call 
 ``masks='off'`` disables dropout; an explicit ``masks=[m1, m2, m3]`` (each [B, n_mid]) injects
 them — the parity mode against oracle/models.py::mlp.
 """
+import ctypes
+
 import numpy as np
 import torch
 
-from dropout_hamiltonian_montecarlo_amd._native import HmcxError, MlpParams, MLP_MASK_SLOT0, context, dtype_code, ptr
+from dropout_hamiltonian_montecarlo_amd._native import (HmcxError, MlpLeapfrogArgs, MlpParams, MLP_MASK_SLOT0,
+                                                        MLP_MASKS_FIXED, MLP_MASKS_NONE, MLP_MASKS_PHILOX, context,
+                                                        dtype_code, ptr)
 
 from .softmax import _batch, as_device
 
@@ -129,6 +133,55 @@ class mlp:
         ctx.check(ctx.lib.hmcx_mlp_grad(ctx.h, self.code, ptr(X), ptr(y), B, self.n_in, self.n_mid, self.n_out, mp,
                                         ptr(m), self.alpha, gp, None), "hmcx_mlp_grad")
         return {k: g for k, g in zip(MLP_PARAM_NAMES, gs)}
+
+    def leapfrog_device_ok(self):
+        """hmc.step may hand the whole trajectory to leapfrog_device only when grad is this class's own
+        (a subclass that overrides grad, e.g. to inject masks per call, keeps the host loop)."""
+        return type(self).grad is mlp.grad
+
+    def leapfrog_device(self, q, p, n_iter, eps, keys, masks=None, **args):
+        """hmc.py:46-56 for the MLP in one libhmcx call (hmcx_mlp_hmc_leapfrog): q and p (dicts of device
+        tensors of the model's dtype, keyed in the sampler's start order `keys`) are advanced in place
+        and p is negated at the end.  The 1 + 6·n_iter gradient calls take their masks as grad() would:
+        masks=None draws fresh Philox masks per call (the same slots as that many grad() calls),
+        'off' disables dropout, explicit masks are used by every call.  Returns the gradient at the
+        final position."""
+        X, y = self._xy(args)
+        B = X.shape[0]
+        order = [MLP_PARAM_NAMES.index(k) for k in keys]
+        if sorted(order) != list(range(6)):
+            raise HmcxError("mlp: leapfrog keys must be the six parameters, got %s" % (list(keys),))
+        a = MlpLeapfrogArgs()
+        a.dtype, a.B, a.n_in, a.n_mid, a.n_out, a.n_iter = self.code, B, self.n_in, self.n_mid, self.n_out, int(n_iter)
+        for i, v in enumerate(order):
+            a.order[i] = v
+        a.eps, a.alpha = float(eps), self.alpha
+        a.X, a.y = X.data_ptr(), y.data_ptr()
+        gs = {}
+        for k in MLP_PARAM_NAMES:
+            for t in (q[k], p[k]):
+                if not (isinstance(t, torch.Tensor) and t.device == self.device and t.dtype == self.dtype
+                        and t.is_contiguous() and tuple(t.shape) == self.shapes[k]):
+                    raise HmcxError("mlp: leapfrog state %s must be a contiguous %s device tensor of shape %s"
+                                    % (k, self.dtype, self.shapes[k]))
+            i = MLP_PARAM_NAMES.index(k)
+            gs[k] = torch.empty_like(q[k])
+            a.q.p[i], a.p.p[i], a.g.p[i] = q[k].data_ptr(), p[k].data_ptr(), gs[k].data_ptr()
+        keep = None
+        if masks is None:
+            keep = torch.empty((3, B, self.n_mid), dtype=self.dtype, device=self.device)
+            a.mask_mode, a.masks = MLP_MASKS_PHILOX, keep.data_ptr()
+            a.seed, a.chain, a.step = self.seed, 0, 0xFFFFFFFF
+            a.slot0 = (MLP_MASK_SLOT0 + self._mask_calls) & 0xFFFFFFFF
+            self._mask_calls += 1 + 6 * int(n_iter)
+        else:
+            keep = self._masks(masks, B)
+            a.mask_mode = MLP_MASKS_NONE if keep is None else MLP_MASKS_FIXED
+            a.masks = None if keep is None else keep.data_ptr()
+        ctx = context(self.device)
+        ctx.check(ctx.lib.hmcx_mlp_hmc_leapfrog(ctx.h, ctypes.byref(a)), "hmcx_mlp_hmc_leapfrog")
+        del keep                                        # stream-ordered: the allocator reuses it after the launches
+        return gs
 
     def loss_device(self, par, masks=None, **args):
         X, y = self._xy(args)

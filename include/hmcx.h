@@ -389,6 +389,35 @@ typedef struct hmcx_mlp_sghmc_args {
 } hmcx_mlp_sghmc_args;
 int hmcx_mlp_sghmc_run(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* a);
 
+/* Full-batch HMC leapfrog trajectory of the MLP in one call: replaces the per-variable loop of
+ * hamiltonian/inference/cpu/hmc.py:46-56 as the GPU hmc.step runs it on the MLP (the reference's
+ * gpu/hmc.py step with models/gpu/mlp.py grad).  With g = grad(q) first, per iteration and per
+ * variable v in order[0..5]:  p_v −= ε/2·g_v;  q_v += ε·p_v;  g = grad(q);  p_v −= ε·g_v  (hmc.py:50-53),
+ * then p = −p (hmc.py:55-56, as p − 2·p).  grad is hmcx_mlp_grad (∇ mean CE + ½·alpha·θ, all six
+ * variables, 1 + 6·n_iter calls); the kicks and drifts are hmcx_axpy's — the same kernels in the same
+ * order as the host loop, so the trajectory is bit-identical to it.  Masks per gradient call:
+ *   HMCX_MLP_MASKS_NONE    no dropout;
+ *   HMCX_MLP_MASKS_FIXED   masks [3][B][n_mid] (dtype) for every call;
+ *   HMCX_MLP_MASKS_PHILOX  call k draws hmcx_mlp_masks(seed, chain, step, slot0 + k) into masks (scratch).
+ * q and p are advanced in place; g holds the gradient at the final position on return. */
+#define HMCX_MLP_MASKS_NONE 0
+#define HMCX_MLP_MASKS_FIXED 1
+#define HMCX_MLP_MASKS_PHILOX 2
+typedef struct hmcx_mlp_leapfrog_args {
+  int dtype;
+  int B, n_in, n_mid, n_out, n_iter;
+  int order[6];            /* canonical variable indices 0=W1 .. 5=b3 in the caller's start order */
+  double eps, alpha;
+  const void* X;           /* device [B][n_in] */
+  const int32_t* y;        /* device [B] labels */
+  hmcx_mlp_params q, p, g; /* device: position, momentum (in/out), gradient (out) */
+  int mask_mode;
+  void* masks;             /* device [3][B][n_mid]: FIXED input / PHILOX scratch */
+  uint64_t seed;
+  uint32_t chain, step, slot0;
+} hmcx_mlp_leapfrog_args;
+int hmcx_mlp_hmc_leapfrog(hmcx_ctx* ctx, const hmcx_mlp_leapfrog_args* a);
+
 /* on = 0: hmcx_mlp_sghmc_run stops fusing layer 2 and layer 3 into one launch (no cross-workgroup
  * exchange; one more launch per forward) — the recovery path after out_abort; on = 1 restores it. */
 int hmcx_set_mlp_fuse(hmcx_ctx* ctx, int on);

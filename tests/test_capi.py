@@ -37,7 +37,8 @@ def test_argument_validation_without_device(nat):
 
 
 _MIRRORS = [("SamplerArgs", "hmcx_sampler_args"), ("SgdArgs", "hmcx_sgd_args"), ("MvnArgs", "hmcx_hmc_mvn_args"),
-            ("MlpParams", "hmcx_mlp_params"), ("MlpSghmcArgs", "hmcx_mlp_sghmc_args"), ("HmcArgs", "hmcx_hmc_args")]
+            ("MlpParams", "hmcx_mlp_params"), ("MlpSghmcArgs", "hmcx_mlp_sghmc_args"), ("HmcArgs", "hmcx_hmc_args"),
+            ("MlpLeapfrogArgs", "hmcx_mlp_leapfrog_args")]
 
 
 def test_struct_layout_matches_header(nat, tmp_path):

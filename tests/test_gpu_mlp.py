@@ -503,3 +503,49 @@ def test_hmc_mlp_generic_loop_matches_oracle():
     for k in start:
         np.testing.assert_allclose(np.asarray(post_g[k]), np.asarray(post_o[k]), rtol=1e-8, atol=1e-10)
     np.testing.assert_allclose(loss_g, loss_o, rtol=1e-10)
+
+
+@pytest.mark.parametrize("dtype,masks", [("f64", None), ("f32", None), ("f64", "off"), ("f64", "fixed")])
+def test_hmc_mlp_device_leapfrog_equals_host_loop(monkeypatch, dtype, masks):
+    """hmcx_mlp_hmc_leapfrog (a step's whole trajectory in one call) against the host loop it replaces
+    (HMCX_HMC_HOST_LOOP=1: model.grad + hmcx_axpy per variable, hmc.py:46-56): the same kernels in the
+    same order, so path lengths, accept flags, acceptance probabilities, losses and the posterior are
+    bit-identical — with Philox masks per gradient call (the same slots as the host loop's grad calls),
+    without dropout, and with one injected mask set."""
+    from dropout_hamiltonian_montecarlo_amd.hamiltonian.models.gpu.mlp import mlp
+    from dropout_hamiltonian_montecarlo_amd.hamiltonian.inference.gpu.hmc import hmc
+    n_in, n_mid, n_out, N = 24, 20, 5, 60
+    rs = np.random.RandomState(21)
+    X = rs.rand(N, n_in)
+    y = rs.randint(0, n_out, N)
+    start = {k: rs.normal(0, 0.2, s) for k, s in om.mlp_param_shapes(n_in, n_mid, n_out).items()}
+    # a non-canonical start order: the sub-steps follow the caller's keys
+    keys = ['/l2/W', '/l1/b', '/l3/b', '/l1/W', '/l3/W', '/l2/b']
+    start = {k: start[k] for k in keys}
+    args = dict(X_train=X, y_train=y)
+    if masks == "off":
+        args["masks"] = "off"
+    elif masks == "fixed":
+        args["masks"] = [(rs.rand(N, n_mid) >= 0.1) / 0.9 for _ in range(3)]
+    tdt = torch.float64 if dtype == "f64" else torch.float32
+
+    def run(host):
+        if host:
+            monkeypatch.setenv("HMCX_HMC_HOST_LOOP", "1")
+        else:
+            monkeypatch.delenv("HMCX_HMC_HOST_LOOP", raising=False)
+        m = mlp({"alpha": 0.01}, n_in, n_mid, n_out, dtype=tdt, device="cuda:0", seed=5)
+        s = hmc(m, start, path_length=0.03, step_size=0.005, verbose=True)
+        s.trace, s.out = [], io.StringIO()
+        np.random.seed(3)
+        post, loss, _, _ = s.sample(4, 1, np.random.RandomState(4), **args)
+        return s.trace, post, loss, m._mask_calls
+
+    tr_h, post_h, loss_h, calls_h = run(True)
+    tr_d, post_d, loss_d, calls_d = run(False)
+    assert max(t["L"] for t in tr_h) >= 3
+    assert tr_d == tr_h
+    assert calls_d == calls_h
+    np.testing.assert_array_equal(loss_d, loss_h)
+    for k in start:
+        np.testing.assert_array_equal(np.asarray(post_d[k]), np.asarray(post_h[k]))
