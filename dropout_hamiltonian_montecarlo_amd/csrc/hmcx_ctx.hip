@@ -450,39 +450,6 @@ static int host_mark(hmcx_ctx* ctx, const void* out_host) {
   return HMCX_OK;
 }
 
-// hmc.py:46-56 on the MLP, every launch enqueued from here (the host loop made 3 ctypes calls and a
-// gradient call per variable per iteration); the kernels and their order are the host loop's.
-template <typename T>
-static int mlp_leapfrog_t(hmcx_ctx* ctx, const hmcx_mlp_leapfrog_args* a) {
-  const int64_t dim[6] = {(int64_t)a->n_mid * a->n_in, a->n_mid, (int64_t)a->n_mid * a->n_mid, a->n_mid,
-                          (int64_t)a->n_out * a->n_mid, a->n_out};
-  uint32_t slot = a->slot0;
-  auto grad = [&]() -> int {
-    const void* m = nullptr;
-    if (a->mask_mode == HMCX_MLP_MASKS_PHILOX) {
-      if (int rc = mlp_masks_t<T>(ctx, a->B, a->n_mid, a->seed, a->chain, a->step, slot++, a->masks)) return rc;
-      m = a->masks;
-    } else if (a->mask_mode == HMCX_MLP_MASKS_FIXED) {
-      m = a->masks;
-    }
-    hmcx_mlp_params g = a->g;
-    return mlp_grad_t<T>(ctx, a->X, a->y, a->B, a->n_in, a->n_mid, a->n_out, &a->q, m, a->alpha, &g, nullptr);
-  };
-  if (int rc = grad()) return rc;
-  for (int it = 0; it < a->n_iter; ++it)
-    for (int i = 0; i < 6; ++i) {
-      const int v = a->order[i];
-      int rc = axpy_t<T>(ctx, 0, dim[v], 0.5 * a->eps, a->g.p[v], a->p.p[v]);      // hmc.py:50
-      if (!rc) rc = axpy_t<T>(ctx, 1, dim[v], a->eps, a->p.p[v], a->q.p[v]);       // :51
-      if (!rc) rc = grad();                                                        // :52
-      if (!rc) rc = axpy_t<T>(ctx, 0, dim[v], a->eps, a->g.p[v], a->p.p[v]);       // :53
-      if (rc) return rc;
-    }
-  for (int v = 0; v < 6; ++v)                                                       // :55-56
-    if (int rc = axpy_t<T>(ctx, 0, dim[v], 2.0, a->p.p[v], a->p.p[v])) return rc;
-  return HMCX_OK;
-}
-
 }  // namespace hmcx
 
 // =================================================================== C ABI

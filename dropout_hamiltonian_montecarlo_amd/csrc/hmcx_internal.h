@@ -246,6 +246,7 @@ template <typename T> int mlp_grad_t(hmcx_ctx*, const void*, const int32_t*, int
 template <typename T> int mlp_loss_t(hmcx_ctx*, const void*, const int32_t*, int, int, int, int,
                                      const hmcx_mlp_params*, const void*, double*, void*);
 template <typename T> int mlp_sghmc_t(hmcx_ctx*, const hmcx_mlp_sghmc_args*);
+template <typename T> int mlp_leapfrog_t(hmcx_ctx*, const hmcx_mlp_leapfrog_args*);
 template <typename T> int mlp_masks_t(hmcx_ctx*, int, int, uint64_t, uint32_t, uint32_t, uint32_t, void*);
 
 }  // namespace hmcx

@@ -1711,6 +1711,72 @@ int mlp_grad_t(hmcx_ctx* ctx, const void* X, const int32_t* y, int B, int n_in, 
   return HMCX_OK;
 }
 
+// The full-batch HMC trajectory of hmcx_mlp_hmc_leapfrog (hmc.py:46-56): g = grad(q); per iteration and
+// variable v = order[i]: p_v −= ε/2·g_v, q_v += ε·p_v, g = grad(q), p_v −= ε·g_v; then p = −p.  Of each
+// gradient only two components are ever read — g_v (this sub-step's second kick) and g_v' of the next
+// variable (its first kick) — so each call computes just those, with mlp_grad_t's kernels and flags
+// for them (identical bits), and the layer-1 output xw is reused until W1 itself moves.
+template <typename T>
+int mlp_leapfrog_t(hmcx_ctx* ctx, const hmcx_mlp_leapfrog_args* s) {
+  MlpNet<T> net{};
+  net_init(net, s->B, s->n_in, s->n_mid, s->n_out, ctx->stream);
+  net.X = (const T*)s->X; net.y = s->y;                       // unfused (see mlp_grad_t)
+  Workspace ws(ctx);
+  double* lpart;
+  do { ws.reset(); mlp_workspace<T>(ws, net); lpart = ws.take<double>(net.nlb); } while (ws.retry());
+  if (ws.failed) return HMCX_ENOMEM;
+  const void* mptr = s->mask_mode == HMCX_MLP_MASKS_NONE ? nullptr : s->masks;
+  const MaskSrc<T> ms{(const T*)mptr, nullptr, T(1), s->B * s->n_mid, 0, 0, 0, 0};
+  if (mptr && (uintptr_t)mptr % 16) net.vec_masks = false;
+  T *q[6], *p[6], *g[6];
+  int64_t dim[6];
+  for (int v = 0; v < 6; ++v) {
+    q[v] = (T*)s->q.p[v]; p[v] = (T*)s->p.p[v]; g[v] = (T*)s->g.p[v];
+    dim[v] = net.nvar(v);
+  }
+  uint32_t slot = s->slot0;
+  // the gradient components `want` (bit v) at q, in mlp_grad_t's order: forward (+ the layer-3 backward
+  // pieces the wanted components use), layer-1 backward, W1 / W2 gradients, then the bias / W3 updates
+  auto grad = [&](unsigned want) -> int {
+    if (s->mask_mode == HMCX_MLP_MASKS_PHILOX)
+      if (int rc = mlp_masks_t<T>(ctx, s->B, s->n_mid, s->seed, s->chain, s->step, slot++, s->masks)) return rc;
+    const bool l1 = want & 3u;
+    HMCX_HIP(ctx, mlp_forward<T>(net, q, ms, lpart,
+                                 L3Want{(want & 15u) != 0, (want & 8u) != 0, (want & 32u) != 0, (want & 16u) != 0}));
+    if (l1) HMCX_HIP(ctx, mlp_ga1<T>(net, q, ms, true));
+    Upd<T> u{};
+    u.half_alpha = (T)(0.5 * s->alpha);
+    for (int v : {0, 2})
+      if (want & (1u << v)) {
+        u.W = q[v]; u.G = g[v];
+        HMCX_HIP(ctx, mlp_wgrad<T>(net, q, ms, v, UPD_GRAD, u));
+      }
+    for (int v : {1, 3, 4, 5})
+      if (want & (1u << v)) {
+        u.W = q[v]; u.G = g[v];
+        set_pending(net, v, UPD_GRAD, u);
+        HMCX_HIP(ctx, flush_pending(net));
+      }
+    return HMCX_OK;
+  };
+  const int* o = s->order;
+  if (int rc = grad(1u << o[0])) return rc;
+  for (int it = 0; it < s->n_iter; ++it)
+    for (int i = 0; i < 6; ++i) {
+      const int v = o[i];
+      const bool tail = it == s->n_iter - 1 && i == 5;        // no next kick follows
+      int rc = axpy_t<T>(ctx, 0, dim[v], 0.5 * s->eps, g[v], p[v]);                    // hmc.py:50
+      if (!rc) rc = axpy_t<T>(ctx, 1, dim[v], s->eps, p[v], q[v]);                     // :51
+      if (v == 0) net.xw_valid = false;
+      if (!rc) rc = grad((1u << v) | (tail ? 0u : 1u << o[(i + 1) % 6]));              // :52
+      if (!rc) rc = axpy_t<T>(ctx, 0, dim[v], s->eps, g[v], p[v]);                     // :53
+      if (rc) return rc;
+    }
+  for (int v = 0; v < 6; ++v)                                                           // :55-56
+    if (int rc = axpy_t<T>(ctx, 0, dim[v], 2.0, p[v], p[v])) return rc;
+  return HMCX_OK;
+}
+
 template <typename T>
 int mlp_loss_t(hmcx_ctx* ctx, const void* X, const int32_t* y, int B, int n_in, int n_mid, int n_out,
                const hmcx_mlp_params* par, const void* masks, double* loss, void* logits) {
@@ -2111,6 +2177,7 @@ template int mlp_grad_t<float>(hmcx_ctx*, const void*, const int32_t*, int, int,
 template int mlp_loss_t<float>(hmcx_ctx*, const void*, const int32_t*, int, int, int, int, const hmcx_mlp_params*,
                                const void*, double*, void*);
 template int mlp_sghmc_t<float>(hmcx_ctx*, const hmcx_mlp_sghmc_args*);
+template int mlp_leapfrog_t<float>(hmcx_ctx*, const hmcx_mlp_leapfrog_args*);
 #endif
 #if HMCX_MLP_DTYPES & 2
 template int mlp_masks_t<double>(hmcx_ctx*, int, int, uint64_t, uint32_t, uint32_t, uint32_t, void*);
@@ -2119,6 +2186,7 @@ template int mlp_grad_t<double>(hmcx_ctx*, const void*, const int32_t*, int, int
 template int mlp_loss_t<double>(hmcx_ctx*, const void*, const int32_t*, int, int, int, int, const hmcx_mlp_params*,
                                 const void*, double*, void*);
 template int mlp_sghmc_t<double>(hmcx_ctx*, const hmcx_mlp_sghmc_args*);
+template int mlp_leapfrog_t<double>(hmcx_ctx*, const hmcx_mlp_leapfrog_args*);
 #endif
 
 }  // namespace hmcx
