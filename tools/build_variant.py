@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """A/B variant of lib/libhmcx.so: the built objects of lib/obj with ONE unit recompiled under extra
 flags, linked as lib/<name> (loaded with HMCX_LIB=<name>, tools/gpu_lib_ab.sh).
-    python tools/build_variant.py libhmcx_base.so hmcx_persist2.hip -DHMCX_P2_MERGE=0"""
+    python tools/build_variant.py libhmcx_base.so hmcx_persist2.hip -DHMCX_P2_MERGE=0
+SRC=<path> compiles that file in place of the unit's source (e.g. `git show HEAD:<path>` saved elsewhere:
+the committed version against the working tree)."""
 import os
 import subprocess
 import sys
@@ -17,7 +19,8 @@ for s, objname, ex in g.UNITS:
     obj = os.path.join(objdir, objname)
     if s == src:
         obj = os.path.join(objdir, "variant_" + objname)
-        subprocess.run([g._hipcc()] + g.FLAGS + ex + extra + ["-c", os.path.join(g.CSRC, s), "-o", obj], check=True)
+        path = os.environ.get("SRC") or os.path.join(g.CSRC, s)
+        subprocess.run([g._hipcc()] + g.FLAGS + ex + extra + (["-x", "hip"] if os.environ.get("SRC") else []) + ["-c", path, "-o", obj], check=True)
     objs.append(obj)
 out = os.path.join(g.PKG, "lib", name)
 subprocess.run([g._hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out] + objs +
