@@ -33,6 +33,8 @@ def test_argument_validation_without_device(nat):
     # null context → EINVAL, no HIP call made
     assert lib.hmcx_softmax_grad(None, 1, None, None, 1, 1, 1, 1, None, None, 0.0, None, None) == -1
     assert lib.hmcx_sghmc_run(None, None) == -1
+    assert lib.hmcx_mlp_hmc_leapfrog(None, None) == -1
+    assert lib.hmcx_chain_diagnostics(None, 1, 4, 1, None, None, None, 0, None) == -1
     assert lib.hmcx_last_error(None) == b"null context"
 
 
