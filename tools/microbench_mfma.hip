@@ -1,12 +1,13 @@
 // f64 / f32 16x16x4 MFMA issue cost for ONE wave per SIMD (256-thread workgroups, one per CU):
-// cycles per MFMA (s_memtime) with 1, 2, 4 and 8 independent accumulator chains.
+// cycles per MFMA (s_memtime) with 1, 2, 4 and 8 independent accumulator chains; "x2" rows run
+// 512-thread workgroups (two waves per SIMD) and report cycles per instruction per wave.
 #include <hip/hip_runtime.h>
 #include <cstdio>
 typedef double d4 __attribute__((ext_vector_type(4)));
 typedef float f4 __attribute__((ext_vector_type(4)));
 
 template <int NA>
-__global__ __launch_bounds__(256) void k64(double* out, unsigned long long* cyc, int reps) {
+__global__ __launch_bounds__(512) void k64(double* out, unsigned long long* cyc, int reps) {
   d4 c[NA];
   for (int i = 0; i < NA; ++i) c[i] = d4{0, 0, 0, 0};
   double a = 1e-3 * threadIdx.x, b = 2e-3;
@@ -18,7 +19,7 @@ __global__ __launch_bounds__(256) void k64(double* out, unsigned long long* cyc,
   double s = 0;
   for (int i = 0; i < NA; ++i) s += c[i][0];
   unsigned long long t1 = __builtin_amdgcn_s_memtime();
-  out[blockIdx.x * 256 + threadIdx.x] = s;
+  out[blockIdx.x * 512 + threadIdx.x] = s;
   if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
 }
 template <int NA>
@@ -56,10 +57,10 @@ __global__ __launch_bounds__(256) void kv64(double* out, unsigned long long* cyc
 }
 
 template <typename F>
-void run(const char* name, F kern, int na, double* o, unsigned long long* c, int reps) {
-  hipLaunchKernelGGL(kern, dim3(256), dim3(256), 0, 0, o, c, reps);
+void run(const char* name, F kern, int na, double* o, unsigned long long* c, int reps, int nt = 256) {
+  hipLaunchKernelGGL(kern, dim3(256), dim3(nt), 0, 0, o, c, reps);
   hipDeviceSynchronize();
-  hipLaunchKernelGGL(kern, dim3(256), dim3(256), 0, 0, o, c, reps);
+  hipLaunchKernelGGL(kern, dim3(256), dim3(nt), 0, 0, o, c, reps);
   hipDeviceSynchronize();
   unsigned long long h[256];
   hipMemcpy(h, c, sizeof(h), hipMemcpyDeviceToHost);
@@ -71,13 +72,16 @@ void run(const char* name, F kern, int na, double* o, unsigned long long* c, int
 int main() {
   double* o;
   unsigned long long* c;
-  hipMalloc(&o, 256 * 256 * 8);
+  hipMalloc(&o, 256 * 512 * 8);
   hipMalloc(&c, 256 * 8);
   const int reps = 4096;
   run("mfma_f64_16x16x4", k64<1>, 1, o, c, reps);
   run("mfma_f64_16x16x4", k64<2>, 2, o, c, reps);
   run("mfma_f64_16x16x4", k64<4>, 4, o, c, reps);
   run("mfma_f64_16x16x4", k64<8>, 8, o, c, reps);
+  run("mfma_f64_16x16x4 x2", k64<1>, 1, o, c, reps, 512);
+  run("mfma_f64_16x16x4 x2", k64<2>, 2, o, c, reps, 512);
+  run("mfma_f64_16x16x4 x2", k64<4>, 4, o, c, reps, 512);
   run("mfma_f32_16x16x4", k32<1>, 1, o, c, reps);
   run("mfma_f32_16x16x4", k32<2>, 2, o, c, reps);
   run("mfma_f32_16x16x4", k32<4>, 4, o, c, reps);
