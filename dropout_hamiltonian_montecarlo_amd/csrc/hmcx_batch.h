@@ -33,11 +33,20 @@ constexpr int BCH = 32;           // depth of one staged k-chunk
 constexpr int BXP = BCH + 2;      // 34: k_bfwd X chunk
 constexpr int BXPG = 48;          // k_bgrad X chunk [row][32 features]
 constexpr int BWP = BNT + 16;     // 176: W / diff chunk [k][160 columns]
-// Epilogue tiles read by the MFMA fragment layout (row = 4·lg + q, column = 16·j + lr): the noise tile
-// and the p² partials.  A row pitch of BNT = 160 elements is ≡ 0 (mod 64) dwords for doubles, so the
-// lane groups lg = 0 / 1 of a half-wave hit the same banks; BNP ≡ 4 (mod 8) elements puts them 32
-// dwords apart (doubles) / 16 apart (floats).
+// k_bfwd's epilogue tile Zt (in the W chunk's LDS): thread (row il, chain cs) reads its chain's 10
+// classes as five ds_read_b128 at 20·cs dwords into row il.  A ds_read_b128 lane group mixes rows il and
+// il + 1 ({0-3, 12-15} of one row with {20-27} of the next, and so on), and the 16-byte starts 20·cs of one
+// row and 20·cs' + pitch of the next never share banks when the pitch is ≡ 0 (mod 64) dwords: 160
+// doubles.  (The chunk pitch 176, ≡ 32 dwords, put every chunk of the next row on a busy bank.)
+constexpr int ZTP = BNT;          // 160
+// Row pitch of the p² partials [row][BNP] (doubles, written by 16-lane rows: any pitch is conflict-free).
 constexpr int BNP = BNT + 4;      // 164
+// Row pitch of the friction-noise tile Nz, read in the MFMA fragment layout (hmcx_common.h): the lane
+// groups lg = 0 / 1 of a half-wave read rows 4 apart in f32 (row = 4·lg + q; ds_read_b32, banks mod 32:
+// pitch ≡ 4 (mod 8) puts them 16 banks apart) but ADJACENT rows in f64 (row = lg + 4·q; ds_read_b64,
+// banks mod 64: pitch ≡ 16 (mod 32) puts them 32 banks apart — the round-4 pitch 164 overlapped 24 of the
+// 32 banks, the k_bgradw bank conflicts of profiles/pmc_r04_batched_sq.json)
+template <typename T> constexpr int bnz() { return sizeof(T) == 8 ? BNT + 16 : BNT + 4; }
 
 // XCD-grouped tile order: the 1-D grid holds 8·nX·ceil(nCT/8) blocks; blocks b, b+8, b+16, ... share
 // one XCD (round-robin dispatch), so every x tile of chain tile ct lands on XCD ct mod 8 and the
@@ -281,7 +290,8 @@ __global__ __launch_bounds__(64 * NWV) void k_bfwd(BFwdArgs<T> a) {
   // ---- epilogue, 32 rows at a time through Zt: softmax.py:32-36 (clip, max, exp, normalise), :52
   const T hi = (T)CLIP_HI, lo = (T)CLIP_LO;
   const bool sghmc = a.mode == FWD_SGHMC;
-  T* Zt = Ws;                                          // [32][BWP] logits, then y − ŷ'
+  static_assert(32 * ZTP <= BCH * BWP, "k_bfwd: the epilogue tile must fit the W chunk's LDS");
+  T* Zt = Ws;                                          // [32][ZTP] logits, then y − ŷ'
   T cs_acc = T(0);                                     // thread t < 160: Σ_rows (y − ŷ') of column t
   for (int half = 0; half < MT; ++half) {
     __syncthreads();
@@ -294,7 +304,7 @@ __global__ __launch_bounds__(64 * NWV) void k_bfwd(BFwdArgs<T> a) {
       for (int j = 0; j < 5; ++j)
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-          Zt[((mtile & 1) * 16 + M::row(lane, q)) * BWP + (nh * 5 + j) * 16 + lr] = acc[i][j][q];
+          Zt[((mtile & 1) * 16 + M::row(lane, q)) * ZTP + (nh * 5 + j) * 16 + lr] = acc[i][j][q];
     }
     __syncthreads();
     for (int pr = tid; pr < 32 * BCT; pr += NTH) {
@@ -305,7 +315,7 @@ __global__ __launch_bounds__(64 * NWV) void k_bfwd(BFwdArgs<T> a) {
       T z[BKC], y[BKC];
 #pragma unroll
       for (int k = 0; k < BKC; ++k) {
-        z[k] = Zt[il * BWP + cs * BKC + k];
+        z[k] = Zt[il * ZTP + cs * BKC + k];
         y[k] = Ysh[i * BKC + k];
       }
       // variant 1: bias b (weights sub-step diff / LL mode)
@@ -340,7 +350,7 @@ __global__ __launch_bounds__(64 * NWV) void k_bfwd(BFwdArgs<T> a) {
 #pragma unroll
       for (int k = 0; k < BKC; ++k) { e[k] = exp(zc[k] - m2); s2 += e[k]; }
 #pragma unroll
-      for (int k = 0; k < BKC; ++k) Zt[il * BWP + cs * BKC + k] = y[k] - e[k] / s2;
+      for (int k = 0; k < BKC; ++k) Zt[il * ZTP + cs * BKC + k] = y[k] - e[k] / s2;
       double ll = 0.0;
       if (last) {
         const T lse = log(s2) + m2;
@@ -352,7 +362,7 @@ __global__ __launch_bounds__(64 * NWV) void k_bfwd(BFwdArgs<T> a) {
     __syncthreads();
     if (sghmc && tid < BNT) {
       const int nr = min(32, nrow - half * 32);
-      for (int il = 0; il < nr; ++il) cs_acc += Zt[il * BWP + tid];
+      for (int il = 0; il < nr; ++il) cs_acc += Zt[il * ZTP + tid];
     }
   }
   if (sghmc && tid < BNT) {                            // Σ_rows (y − ŷ') of this tile
@@ -399,8 +409,8 @@ __device__ inline void gen_tile_noise(const BGradArgs<T>& a, const int* chs, int
       if (ch < 0 || fi >= nfeat) continue;
       double z0, z1;
       philox_pair_d(a.seed, a.chain0 + ch, a.step, a.slot, (uint32_t)((d0 + fi) * NP + kk), z0, z1);
-      Nz[fl * BNP + cs * BKC + 2 * kk] = z0;
-      Nz[fl * BNP + cs * BKC + 2 * kk + 1] = z1;
+      Nz[fl * bnz<T>() + cs * BKC + 2 * kk] = z0;
+      Nz[fl * bnz<T>() + cs * BKC + 2 * kk + 1] = z1;
     }
   } else {                                        // nfl == tile width, fmap = identity
     const int e0 = d0 * BKC, ne = min(nfl, nfeat) * BKC;
@@ -413,7 +423,7 @@ __device__ inline void gen_tile_noise(const BGradArgs<T>& a, const int* chs, int
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int e = 4 * g + q - e0;
-        if (e >= 0 && e < ne) Nz[(e / BKC) * BNP + cs * BKC + (e % BKC)] = z4[q];
+        if (e >= 0 && e < ne) Nz[(e / BKC) * bnz<T>() + cs * BKC + (e % BKC)] = z4[q];
       }
     }
   }
@@ -520,7 +530,8 @@ __global__ __launch_bounds__(256) void k_bgrad(BGradArgs<T> a) {
     }
   }
   __syncthreads();
-  // friction noise of the tile into the diff chunk's space ([32 features][160], T)
+  // friction noise of the tile into the diff chunk's space ([32 features][bnz], T)
+  static_assert(BRW * bnz<T>() <= BCH * BWP, "k_bgrad: the noise tile must fit the diff chunk's LDS");
   T* Nz = Ds;
   if (a.noise_mode != HMCX_NOISE_BUFFER) {
     gen_tile_noise(a, chs, d0, nfeat, Nz, BRW, [](int fl) { return fl; });
@@ -569,7 +580,7 @@ __global__ __launch_bounds__(256) void k_bgrad(BGradArgs<T> a) {
       }
     } else {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) zv[q] = Nz[(mt * 16 + M::row(lane, q)) * BNP + col];
+      for (int q = 0; q < 4; ++q) zv[q] = Nz[(mt * 16 + M::row(lane, q)) * bnz<T>() + col];
     }
     double p2s = 0.0;
 #pragma unroll
@@ -617,7 +628,7 @@ template <typename T, int NW> struct BGW {
   static constexpr int NPASS = sizeof(T) == 8 ? 2 : 1;
   static constexpr int NZR = FT / NPASS;                               // noise rows per pass
   static constexpr int XSN = BCH * XP > 2 * NW * BNP * 8 / (int)sizeof(T) ? BCH * XP : 2 * NW * BNP * 8 / (int)sizeof(T);
-  static constexpr int DSN = BCH * BWP > NZR * BNP ? BCH * BWP : NZR * BNP;
+  static constexpr int DSN = BCH * BWP > NZR * bnz<T>() ? BCH * BWP : NZR * bnz<T>();
   static constexpr size_t lds() { return (size_t)(XSN + DSN + BNT) * sizeof(T) + BCT * sizeof(int); }
 };
 constexpr int BRW2 = 64;          // k_bgradw<T, 4> feature tile
@@ -792,7 +803,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
           for (int q = 0; q < 4; ++q) {
             const int fi = mt * 32 + (i0 + ii) * 16 + M::row(lane, q);
             const int nzr = G::NPASS == 2 ? mt * 16 + M::row(lane, q) : fi;
-            zv[ii * 4 + q] = Nz[nzr * BNP + col];
+            zv[ii * 4 + q] = Nz[nzr * bnz<T>() + col];
           }
       }
 #pragma unroll
