@@ -203,23 +203,27 @@ __device__ inline void load_step_rows(T* Xs, T* Yo, const T* Xg, const T* Yg, in
   if (tid < Ro * 16) Yo[tid] = y;
 }
 
-// C[16 x 16] += A[16 x 4·nk] · B[4·nk x 16] on one wave (v_mfma_*_16x16x4): A(i, kk) = a[i·as_i +
-// kk·as_k], B(kk, j) = b[kk·bs_k + j]; operands of 8 k-steps are loaded before their MFMAs, two
-// accumulators alternate.  Returns the D fragment (rows M::row(lane, q), column lane & 15).
+// C[16 x 16] += A[16 x 4·nk] · B[4·nk x 16] on one wave (v_mfma_*_16x16x4).  Lane group lg of k-step kk
+// holds A(i, ·) = a[i·as_i + lg·a_lg + kk·a_kk] and B(·, j) = b[lg·b_lg + kk·b_kk + j]: (a_lg, a_kk) =
+// (as_k, 4·as_k) walks k in order, (a_lg, a_kk) = (nk·as_k, as_k) lets the four lane groups of one
+// k-step read k values nk apart (the same 4·nk terms, summed in another grouping).  Operands of 8
+// k-steps are loaded before their MFMAs, two accumulators alternate.  Returns the D fragment (rows
+// M::row(lane, q), column lane & 15).
 template <typename T>
-__device__ inline typename mfma16<T>::acc_t mfma_tile(const T* a, int as_i, int as_k, const T* b, int bs_k, int nk) {
+__device__ inline typename mfma16<T>::acc_t mfma_tile(const T* a, int as_i, int a_lg, int a_kk, const T* b, int b_lg,
+                                                      int b_kk, int nk) {
   using M = mfma16<T>;
   const int lane = threadIdx.x & 63, lr = lane & 15, lg = lane >> 4;
-  const T* pa = a + lr * as_i + lg * as_k;
-  const T* pb = b + lg * bs_k + lr;
+  const T* pa = a + lr * as_i + lg * a_lg;
+  const T* pb = b + lg * b_lg + lr;
   typename M::acc_t c0 = M::zero(), c1 = M::zero();
   int kk = 0;
   for (; kk + 8 <= nk; kk += 8) {
     T av[8], bv[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      av[u] = pa[(kk + u) * 4 * as_k];
-      bv[u] = pb[(kk + u) * 4 * bs_k];
+      av[u] = pa[(kk + u) * a_kk];
+      bv[u] = pb[(kk + u) * b_kk];
     }
 #pragma unroll
     for (int u = 0; u < 8; u += 2) {
@@ -229,10 +233,10 @@ __device__ inline typename mfma16<T>::acc_t mfma_tile(const T* a, int as_i, int 
   }
   // tail: the two accumulators still alternate (two dependent MFMA chains, not one)
   for (; kk + 2 <= nk; kk += 2) {
-    c0 = M::fma(pa[kk * 4 * as_k], pb[kk * 4 * bs_k], c0);
-    c1 = M::fma(pa[(kk + 1) * 4 * as_k], pb[(kk + 1) * 4 * bs_k], c1);
+    c0 = M::fma(pa[kk * a_kk], pb[kk * b_kk], c0);
+    c1 = M::fma(pa[(kk + 1) * a_kk], pb[(kk + 1) * b_kk], c1);
   }
-  if (kk < nk) c0 = M::fma(pa[kk * 4 * as_k], pb[kk * 4 * bs_k], c0);
+  if (kk < nk) c0 = M::fma(pa[kk * a_kk], pb[kk * b_kk], c0);
   return c0 + c1;
 }
 
@@ -254,7 +258,7 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
   const int pbid = blockIdx.x;
   const int bid = xmap ? (pbid & 7) * (G >> 3) + (pbid >> 3) : pbid;
   const int r = bid / Gf, f = bid - (bid / Gf) * Gf;
-  const int Br = SP ? 64 : a.Br, Bf = SP ? 49 : a.Bf, BfP = SP ? 64 : a.BfP, BFP = SP ? 66 : a.BFP, Ro = SP ? 4 : a.Ro,
+  const int Br = SP ? 64 : a.Br, Bf = SP ? 49 : a.Bf, BfP = SP ? 64 : a.BfP, BFP = SP ? 65 : a.BFP, Ro = SP ? 4 : a.Ro,
             Fo = SP ? 7 : a.Fo;
   const int K = SP ? 10 : a.K, D = SP ? 784 : a.D, B = SP ? 500 : a.B;
   const int row0 = r * Br, feat0 = f * Bf;
@@ -360,8 +364,8 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
     const int nkp = SP ? 13 : WPA == 1 ? (nfeat + 3) / 4 : (BfP / 4) / WPA;
     for (int item = wave; item < MTA * WPA; item += QNW) {
       const int mt = item % MTA, part = item / MTA;
-      const typename M::acc_t c = mfma_tile<T>(Xs + mt * 16 * BFP + part * nkp * 4, BFP, 1,
-                                               Wf + part * nkp * 4 * 16, 16, nkp);
+      const typename M::acc_t c = mfma_tile<T>(Xs + mt * 16 * BFP + part * nkp * 4, BFP, 1, 4,
+                                               Wf + part * nkp * 4 * 16, 16, 64, nkp);
       if (WPA == 1) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -641,8 +645,8 @@ __global__ __launch_bounds__(QTH) void k_sghmc_p2(Q2Args a) {
         const int nkp = (Br / 4) / WPB;
         for (int item = wave; item < MTB * WPB; item += QNW) {
           const int mt = item % MTB, part = item / MTB;
-          const typename M::acc_t c = mfma_tile<T>(Xs + part * nkp * 4 * BFP + mt * 16, 1, BFP,
-                                                   Ds + part * nkp * 4 * 16, 16, nkp);
+          const typename M::acc_t c = mfma_tile<T>(Xs + part * nkp * 4 * BFP + mt * 16, 1, nkp * BFP, BFP,
+                                                   Ds + part * nkp * 4 * 16, nkp * 16, 16, nkp);
           if (WPB == 1) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -934,7 +938,10 @@ PersistPlan2 plan_p2(int B, int D, int K, size_t ts, int num_cus, size_t lds_max
       if (p.Br > QTH) continue;
       p.Bf = (D + Gf - 1) / Gf;
       p.BfP = (p.Bf + 15) / 16 * 16;
-      p.BFP = p.BfP + (ts == 8 ? 2 : 1);
+      // odd row pitch: the A-gemm's column reads (16 rows per ds_read2_b64 group) hit 16 distinct bank
+      // pairs; the B-gemm reads its k values Br/4 rows apart per lane group (mfma_tile), 2·BFP·16 ≡ 32
+      // dwords mod 64, so the two half-waves of its ds_read_b64 land on disjoint banks
+      p.BFP = p.BfP + 1;
       p.Ro = (p.Br + Gf - 1) / Gf;
       p.Fo = (p.Bf + Gr - 1) / Gr;
       if ((long)(Gr - 1) * rows >= B || (long)(Gf - 1) * p.Bf >= D) continue;  // no empty teams
@@ -1105,7 +1112,7 @@ int sghmc_p2_t(hmcx_ctx* ctx, const hmcx_sampler_args* s, const PersistPlan2& pl
   a.trace = dtrace;
   // the folded instantiation when the call is exactly BASELINE config 2's plan with default knobs
   const bool spec = sizeof(T) == 8 && KC == 10 && s->B == 500 && s->D == 784 && K == 10 && pl.Gr == 8 && pl.Gf == 16 &&
-                    pl.Br == 64 && pl.Bf == 49 && pl.BfP == 64 && pl.BFP == 66 && pl.Ro == 4 && pl.Fo == 7 &&
+                    pl.Br == 64 && pl.Bf == 49 && pl.BfP == 64 && pl.BFP == 65 && pl.Ro == 4 && pl.Fo == 7 &&
                     a.spread == 2 && a.pad == 1 && a.xmap == 0 && a.fl2 == 1 && a.al2 == 0 && a.prefetch == 1 &&
                     a.acc1 == 1 && a.zoff == 1 && a.bar == 1 && !a.trace;
   static const bool no_spec = getenv("HMCX_P2_SPEC") && getenv("HMCX_P2_SPEC")[0] == '0';
