@@ -1400,7 +1400,9 @@ int sghmc_batch_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
       f.nX = big ? nX64 : nRB; f.nCT = (c_act + BCT - 1) / BCT;
       // launches that leave CUs without a second workgroup: 32-row tiles (or the 8-wave 64-row kernel)
       static const bool bf8_off = getenv("HMCX_BFWD8") && getenv("HMCX_BFWD8")[0] == '0';
-      const bool tail = big && f.nX * f.nCT <= ctx->num_cus;
+      // HMCX_BTAIL_WG / HMCX_BGW_MIN: tile-height and feature-tile switch points (measurement knobs)
+      static const int tail_wg = getenv("HMCX_BTAIL_WG") ? atoi(getenv("HMCX_BTAIL_WG")) : ctx->num_cus;
+      const bool tail = big && f.nX * f.nCT <= tail_wg;
       if (tail && tail32) {
         f.nX = (B + 31) / 32;
         hipLaunchKernelGGL((k_bfwd<T, 1, 1>), dim3(xcd_grid(f.nX, f.nCT)), dim3(256), 0, st, f);
@@ -1413,7 +1415,8 @@ int sghmc_batch_t(hmcx_ctx* ctx, const hmcx_sampler_args* s) {
       // 64-feature tiles while they fill the chip's 2 workgroups per CU, 32-feature tiles after
       const int ctiles = (c_act + BCT - 1) / BCT;
       g.nCT = ctiles;
-      if (nDB2 * ctiles >= 2 * ctx->num_cus) {
+      static const int bgw_min = getenv("HMCX_BGW_MIN") ? atoi(getenv("HMCX_BGW_MIN")) : 2 * ctx->num_cus;
+      if (nDB2 * ctiles >= bgw_min) {
         g.nX = nDB2;
         static const bool tail_off = getenv("HMCX_BGW_TAIL") && getenv("HMCX_BGW_TAIL")[0] == '0';
         g.tail_last = !tail_off && nDB2 > 1 && D % BRW2 != 0 && D % BRW2 <= BRW2 / 2;
