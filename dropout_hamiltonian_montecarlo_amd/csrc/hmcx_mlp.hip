@@ -232,6 +232,7 @@ template <typename T> struct MMArgs {
   const T* H1;                       // MM_GA1: the gate from a stored h1 (no mask reads)
   int force_abort;                   // test knob (HMCX_MLP_FORCE_ABORT): raise the abort word, skip the publish
   unsigned long long* prof;          // HMCX_MLP_PROF: per-workgroup s_memrealtime stamps of the MM_L23 phases
+  int xmap;                          // plain launch: 1 = each XCD takes a contiguous y-major chunk of tiles (k_mm)
 };
 constexpr int L23_NPH = 12;          // stamps per workgroup and launch (prof)
 
@@ -857,8 +858,19 @@ __global__ __launch_bounds__(MM_NT) __attribute__((amdgpu_waves_per_eu(4))) void
   __shared__ double rowl[32];
   MMProbsN<T, 1> none;
   none.n = 0;
+  int x = blockIdx.x, y = blockIdx.y;
+  if (a.xmap && blockIdx.z == 0) {
+    // workgroups are dealt round-robin over the 8 XCDs in dispatch order (lin % 8); give XCD k the
+    // tiles [k·P/8, (k+1)·P/8) of the y-major order instead, so it pulls every A tile but only ≈ gy/8 B
+    // slices into its L2 (ga1ᵀ·X: 8 + 4 operand tiles per XCD instead of 1 + 25)
+    const int gx = gridDim.x, P = gx * gridDim.y, lin = y * gx + x;
+    const int xcd = lin & 7, q = P >> 3, rem = P & 7;
+    const int t = xcd * q + min(xcd, rem) + (lin >> 3);
+    x = t % gx;
+    y = t / gx;
+  }
   mm_body<T, EPI, AOP, BOP, TA, TB, AV, BV, MK>(
-      a, none, Blk{(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z, (int)gridDim.x, (int)gridDim.y}, red, rowl);
+      a, none, Blk{x, y, (int)blockIdx.z, (int)gridDim.x, (int)gridDim.y}, red, rowl);
 }
 template <typename T, int EPI, int AOP, int BOP, int TA, int TB, int AV, int BV, int MK>
 __global__ __launch_bounds__(MM_NT) __attribute__((amdgpu_waves_per_eu(4))) void k_mmb(MMArgs<T> a, MMProbs<T> pr) {
@@ -1177,6 +1189,16 @@ hipError_t mm(MlpNet<T>& net, MMArgs<T>& a, const MMProbs<T>* prp = nullptr) {
   // a batched launch: one plane per problem, plus one for the pending updates
   dim3 grid((a.M + 31) / 32, (a.N + 31) / 32, (pr.n > 0 ? pr.n : 1) + (a.pend.n > 0 ? 1 : 0)), blk(MM_NT);
   if (EPI == MM_L3CE) grid.y = (unsigned)std::max(1, std::min(8, a.n_mid / 32));   // n_mid column slices
+  // plain GEMM-only launches whose tiles share operands along y more than along x: XCD-contiguous
+  // chunks of the y-major tile order (k_mm; HMCX_MLP_XMAP=0 keeps the dispatch order).  Config 3's W1
+  // gradient: L2 hits 63 → 78 %, f32 14.91 k → 15.04 k leapfrog/s; f64 5.92 k → 5.90 k, so f32 only
+  // 
+  {
+    static const bool xmap_off = getenv("HMCX_MLP_XMAP") && getenv("HMCX_MLP_XMAP")[0] == '0';
+    const int gx = (int)grid.x, gy = (int)grid.y;
+    a.xmap = !xmap_off && sizeof(T) == 4 && pr.n == 0 && (EPI == MM_UPD || EPI == MM_STORE) && gx * gy >= 16 &&
+             gx + (gy + 7) / 8 + 1 < std::max(1, gx / 8) + gy;
+  }
   const bool h1ok = AOP != OP_H1 || net.vec_masks;
   const bool kvec = a.K % (int)(16 / sizeof(T)) == 0;       // vectors never straddle the K end
   bool aal = vec_ok(a.A, a.lda, sizeof(T)), bal = vec_ok(a.B, a.ldb, sizeof(T));
