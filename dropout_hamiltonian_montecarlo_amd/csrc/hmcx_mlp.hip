@@ -232,7 +232,8 @@ template <typename T> struct MMArgs {
   const T* H1;                       // MM_GA1: the gate from a stored h1 (no mask reads)
   int force_abort;                   // test knob (HMCX_MLP_FORCE_ABORT): raise the abort word, skip the publish
   unsigned long long* prof;          // HMCX_MLP_PROF: per-workgroup s_memrealtime stamps of the MM_L23 phases
-  int xmap;                          // plain launch: 1 = each XCD takes a contiguous y-major chunk of tiles (k_mm)
+  int xmap, xbx, xby;                // GEMM plane placement over the XCDs (xcd_place): 0 dispatch order, 1 y-major
+                                     // chunks, 2 xbx × xby tile blocks, one per XCD
 };
 constexpr int L23_NPH = 12;          // stamps per workgroup and launch (prof)
 
@@ -850,6 +851,31 @@ __device__ __forceinline__ void mm_body(const MMArgs<T>& a, const PR& pr, const 
 
 // amdgpu_waves_per_eu(4): two 8-wave workgroups per CU (≤ 128 registers): a batched fused launch
 // (MM_L23) needs all its problems' workgroups co-resident, and at 136 registers only one fit per CU.
+// Workgroups are dealt round-robin over the 8 XCDs in dispatch order (position lin of a launch plane
+// whose size is a multiple of 8: XCD = lin % 8), and every XCD pulls its tiles' operands into its own
+// L2.  xcd_place maps position (x, y) of a GX-wide plane to the tile it computes, or to none: xmap 1
+// gives XCD k the tiles [k·P/8, (k+1)·P/8) of the gx × gy tiles in y-major order, xmap 2 the k-th
+// xbx × xby block; both keep the tiles an XCD needs to few row tiles of A and few column slices of B
+// (A and B tiles are both 32 × K).  xmap 0: the dispatch order itself.
+template <typename T>
+__device__ inline bool xcd_place(const MMArgs<T>& a, int GX, int gx, int gy, int& x, int& y) {
+  if (!a.xmap) return x < gx && y < gy;
+  const int lin = y * GX + x, k = lin & 7, s = lin >> 3;
+  if (a.xmap == 1) {
+    const int P = gx * gy, q = P >> 3, rem = P & 7;
+    if (s >= q + (k < rem ? 1 : 0)) return false;
+    const int t = k * q + min(k, rem) + s;
+    x = t % gx;
+    y = t / gx;
+    return true;
+  }
+  if (s >= a.xbx * a.xby) return false;
+  const int nbx = gx / a.xbx;
+  x = (k % nbx) * a.xbx + s % a.xbx;
+  y = (k / nbx) * a.xby + s / a.xbx;
+  return true;
+}
+
 // A plain launch (k_mm) and a batched one (k_mmb, blockIdx.z = problem): the plain kernel keeps the
 // small argument block (no problem table).
 template <typename T, int EPI, int AOP, int BOP, int TA, int TB, int AV, int BV, int MK>
@@ -859,16 +885,7 @@ __global__ __launch_bounds__(MM_NT) __attribute__((amdgpu_waves_per_eu(4))) void
   MMProbsN<T, 1> none;
   none.n = 0;
   int x = blockIdx.x, y = blockIdx.y;
-  if (a.xmap && blockIdx.z == 0) {
-    // workgroups are dealt round-robin over the 8 XCDs in dispatch order (lin % 8); give XCD k the
-    // tiles [k·P/8, (k+1)·P/8) of the y-major order instead, so it pulls every A tile but only ≈ gy/8 B
-    // slices into its L2 (ga1ᵀ·X: 8 + 4 operand tiles per XCD instead of 1 + 25)
-    const int gx = gridDim.x, P = gx * gridDim.y, lin = y * gx + x;
-    const int xcd = lin & 7, q = P >> 3, rem = P & 7;
-    const int t = xcd * q + min(xcd, rem) + (lin >> 3);
-    x = t % gx;
-    y = t / gx;
-  }
+  if (a.xmap && blockIdx.z == 0 && !xcd_place(a, (int)gridDim.x, (int)gridDim.x, (int)gridDim.y, x, y)) return;
   mm_body<T, EPI, AOP, BOP, TA, TB, AV, BV, MK>(
       a, none, Blk{x, y, (int)blockIdx.z, (int)gridDim.x, (int)gridDim.y}, red, rowl);
 }
@@ -889,10 +906,14 @@ __global__ __launch_bounds__(MM_NT) __attribute__((amdgpu_waves_per_eu(4)))
 void k_mm2(MMArgs<T> a1, MMProbs3<T> p1, MMArgs<T> a2, int3 g1, int2 g2) {
   __shared__ T red[MM_NW][32][33];
   __shared__ double rowl[32];
-  const int x = blockIdx.x, y = blockIdx.y, z = blockIdx.z;
+  int x = blockIdx.x, y = blockIdx.y;
+  const int z = blockIdx.z, GX = gridDim.x;
   if (z < g1.z) {
-    if (x < g1.x && y < g1.y) mm_body<T, E1, A1, B1, TA1, TB1, AV1, BV1, MK>(a1, p1, Blk{x, y, z, g1.x, g1.y}, red, rowl);
-  } else if (x < g2.x && y < g2.y) {
+    // GEMM planes of grid 1 (not its pending plane) and grid 2's GEMM plane follow the XCD placement
+    const bool gemm = z < (p1.n > 0 ? p1.n : 1);
+    if (gemm ? xcd_place(a1, GX, g1.x, g1.y, x, y) : (x < g1.x && y < g1.y))
+      mm_body<T, E1, A1, B1, TA1, TB1, AV1, BV1, MK>(a1, p1, Blk{x, y, z, g1.x, g1.y}, red, rowl);
+  } else if (z == g1.z ? xcd_place(a2, GX, g2.x, g2.y, x, y) : (x < g2.x && y < g2.y)) {
     MMProbsN<T, 1> none;
     none.n = 0;
     mm_body<T, E2, A2, B2, TA2, TB2, AV2, BV2, MK>(a2, none, Blk{x, y, z - g1.z, g2.x, g2.y}, red, rowl);
@@ -1179,6 +1200,32 @@ void net_init(MlpNet<T>& net, int B, int n_in, int n_mid, int n_out, hipStream_t
 // Launch k_mm for a call site with compile-time operand layouts (TA: A stored [K][M], TB: B stored
 // [N][K]); k-contiguous operands take the 16-byte vector path when aligned.  Takes the pending update.
 // BAT: the call site passes a problem table (k_mmb); plain call sites instantiate k_mm only.
+// XCD placement of one GEMM plane (xcd_place): the candidate that leaves each XCD the fewest distinct
+// operand tiles (A row tiles + B column slices) — the dispatch order, y-major chunks, or one block of
+// tiles per XCD.  f32 only: config 3's W1 gradient (8 × 25 tiles; chunks: 8 + 4 tiles per XCD instead
+// of 1 + 25) went from 63 to 78 % L2 hits and 14.91 k to 15.04 k leapfrog/s, f64 measured 5.92 k → 5.90 k
+// (DESIGN §5.3 Round 5).  HMCX_MLP_XMAP=0 keeps the dispatch order everywhere.
+template <typename T>
+void xcd_choose(MMArgs<T>& a, int GX, int GY, int gx, int gy) {
+  static const bool off = getenv("HMCX_MLP_XMAP") && getenv("HMCX_MLP_XMAP")[0] == '0';
+  a.xmap = 0;
+  if (off || sizeof(T) != 4 || gx * gy < 16 || (GX * GY) % 8) return;
+  const int per = GX * GY / 8;                                   // positions per XCD in the plane
+  int best = GX % 8 == 0 ? (gx + 7) / 8 + gy : gx + gy;          // dispatch order
+  const int P = gx * gy, q = P / 8 + (P % 8 ? 1 : 0);
+  if (q <= per) {
+    const int c = std::min(gx, q) + (q + gx - 1) / gx + 1;
+    if (c < best) { best = c; a.xmap = 1; }
+  }
+  for (int bx = 1; bx <= gx; ++bx) {
+    if (gx % bx) continue;
+    for (int by = 1; by <= gy; ++by) {
+      if (gy % by || (gx / bx) * (gy / by) != 8 || bx * by > per) continue;
+      if (bx + by < best) { best = bx + by; a.xmap = 2; a.xbx = bx; a.xby = by; }
+    }
+  }
+}
+
 template <typename T, int EPI, int TA, int TB, int AOP = OP_PLAIN, int BOP = OP_PLAIN, bool BAT = false>
 hipError_t mm(MlpNet<T>& net, MMArgs<T>& a, const MMProbs<T>* prp = nullptr) {
   if (a.ta != TA || a.tb != TB || (prp && !BAT)) return hipErrorInvalidValue;
@@ -1189,16 +1236,7 @@ hipError_t mm(MlpNet<T>& net, MMArgs<T>& a, const MMProbs<T>* prp = nullptr) {
   // a batched launch: one plane per problem, plus one for the pending updates
   dim3 grid((a.M + 31) / 32, (a.N + 31) / 32, (pr.n > 0 ? pr.n : 1) + (a.pend.n > 0 ? 1 : 0)), blk(MM_NT);
   if (EPI == MM_L3CE) grid.y = (unsigned)std::max(1, std::min(8, a.n_mid / 32));   // n_mid column slices
-  // plain GEMM-only launches whose tiles share operands along y more than along x: XCD-contiguous
-  // chunks of the y-major tile order (k_mm; HMCX_MLP_XMAP=0 keeps the dispatch order).  Config 3's W1
-  // gradient: L2 hits 63 → 78 %, f32 14.91 k → 15.04 k leapfrog/s; f64 5.92 k → 5.90 k, so f32 only
-  // 
-  {
-    static const bool xmap_off = getenv("HMCX_MLP_XMAP") && getenv("HMCX_MLP_XMAP")[0] == '0';
-    const int gx = (int)grid.x, gy = (int)grid.y;
-    a.xmap = !xmap_off && sizeof(T) == 4 && pr.n == 0 && (EPI == MM_UPD || EPI == MM_STORE) && gx * gy >= 16 &&
-             gx + (gy + 7) / 8 + 1 < std::max(1, gx / 8) + gy;
-  }
+  if (pr.n == 0 && (EPI == MM_UPD || EPI == MM_STORE)) xcd_choose<T>(a, (int)grid.x, (int)grid.y, (int)grid.x, (int)grid.y);
   const bool h1ok = AOP != OP_H1 || net.vec_masks;
   const bool kvec = a.K % (int)(16 / sizeof(T)) == 0;       // vectors never straddle the K end
   bool aal = vec_ok(a.A, a.lda, sizeof(T)), bal = vec_ok(a.B, a.ldb, sizeof(T));
@@ -1566,6 +1604,8 @@ hipError_t mlp_l1_w2(MlpNet<T>& net, const T* W1, T* out, MlpNet<T>& w2n, const 
   const int3 g1 = make_int3((a1.M + 31) / 32, (a1.N + 31) / 32, 1);
   const int2 g2 = make_int2((a2.M + 31) / 32, (a2.N + 31) / 32);
   const dim3 grid((unsigned)std::max(g1.x, g2.x), (unsigned)std::max(g1.y, g2.y), 2u);
+  xcd_choose<T>(a1, (int)grid.x, (int)grid.y, g1.x, g1.y);     // layer 1: 4 × 4 tile blocks per XCD
+  xcd_choose<T>(a2, (int)grid.x, (int)grid.y, g2.x, g2.y);     // W2 gradient: 2 × 4
   hipStream_t st = net.st;
   if constexpr (sizeof(T) == 4) {
     auto go = [&](auto mkc) {
@@ -1593,6 +1633,8 @@ hipError_t mlp_w1_w2(MlpNet<T>& net, MlpNet<T>& w1n, const SubStep<T>& s1, const
   const int3 g1 = make_int3((a1.M + 31) / 32, (a1.N + 31) / 32, 1 + (a1.pend.n > 0 ? 1 : 0));
   const int2 g2 = make_int2((a2.M + 31) / 32, (a2.N + 31) / 32);
   const dim3 grid((unsigned)std::max(g1.x, g2.x), (unsigned)std::max(g1.y, g2.y), (unsigned)(g1.z + 1));
+  xcd_choose<T>(a1, (int)grid.x, (int)grid.y, g1.x, g1.y);     // W1 gradient: y-major chunks
+  xcd_choose<T>(a2, (int)grid.x, (int)grid.y, g2.x, g2.y);     // W2 gradient: 2 × 4 tile blocks
   hipStream_t st = net.st;
   if constexpr (sizeof(T) == 4) {                              // float32 only (quad_ok)
     auto go = [&](auto mkc) {

@@ -19,7 +19,7 @@ for xm in (0, 1):
         k = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("hmcx::", "")[:60]
         acc[k][r["Counter_Name"]] += float(r["Counter_Value"])
     for k, v in acc.items():
-        if k.startswith("k_mm<"):
+        if k.startswith("k_mm"):
             h, m = v["TCC_HIT_sum"], v["TCC_MISS_sum"]
             print("xmap=%d %-45s hit %.1f%% misses %.3g" % (xm, k, 100 * h / max(1, h + m), m))
 PY
