@@ -247,7 +247,10 @@ class Context:
 
     def recoveries(self):
         """Re-runs after timed-out exchanges since this context was created, by kind
-        (include/hmcx.h hmcx_get_recoveries): all zero unless a fallback path ran."""
+        (include/hmcx.h hmcx_get_recoveries): all zero unless a fallback path ran.  None when the
+        loaded library predates the counters (an older build loaded through HMCX_LIB for an A/B run)."""
+        if not hasattr(self.lib, "hmcx_get_recoveries"):
+            return None
         out = (ctypes.c_int64 * len(self.RECOVERY_KINDS))()
         self.check(self.lib.hmcx_get_recoveries(self.h, out), "hmcx_get_recoveries")
         return dict(zip(self.RECOVERY_KINDS, (int(v) for v in out)))
@@ -323,7 +326,7 @@ def recoveries_all():
     with _lock:
         ctxs = list(_ctxs.values())
     for c in ctxs:
-        for k, v in c.recoveries().items():
+        for k, v in (c.recoveries() or {}).items():
             tot[k] += v
     return tot
 

@@ -557,8 +557,7 @@ int hmcx_clear_abort(hmcx_ctx* ctx) {
             w[2], w[3]);
   }
   HMCX_HIP(ctx, hipMemsetAsync(ctx->abort_dev, 0, ABORT_WORDS * sizeof(int), ctx->stream));
-  ++ctx->recoveries[HMCX_RECOVERY_PERSISTENT];
-  return HMCX_OK;
+  return HMCX_OK;                                   // the re-runs themselves are counted by the caller
 }
 
 int hmcx_get_recoveries(const hmcx_ctx* ctx, int64_t* counts) {

@@ -134,7 +134,7 @@ extern "C" int hmcx_chain_diagnostics(hmcx_ctx* ctx, int C, int T, int P, const 
     ws.reset();
     sm = ws.take<double>((size_t)2 * C * P);
   } while (ws.retry());
-  if (ws.failed) return HMCX_ENOMEM;
+  if (ws.failed) return set_error(ctx, HMCX_ENOMEM, "chain diagnostics: workspace");
   DiagArgs a{C, T, P, trace, means, M2, n_moments, sm, out};
   hipLaunchKernelGGL(k_chain_diag, dim3((P + 255) / 256), dim3(256), 0, ctx->stream, a);
   HMCX_HIP(ctx, hipGetLastError());

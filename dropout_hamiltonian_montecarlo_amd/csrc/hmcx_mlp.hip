@@ -1824,7 +1824,9 @@ int mlp_leapfrog_t(hmcx_ctx* ctx, const hmcx_mlp_leapfrog_args* s) {
     return HMCX_OK;
   };
   const int* o = s->order;
-  if (int rc = grad(1u << o[0])) return rc;
+  // the last gradient call computes all six components, so g is the full gradient at the final
+  // position (as the header promises); every earlier call only the two the next kicks read
+  if (int rc = grad(s->n_iter > 0 ? 1u << o[0] : 63u)) return rc;
   for (int it = 0; it < s->n_iter; ++it)
     for (int i = 0; i < 6; ++i) {
       const int v = o[i];
@@ -1832,7 +1834,7 @@ int mlp_leapfrog_t(hmcx_ctx* ctx, const hmcx_mlp_leapfrog_args* s) {
       int rc = axpy_t<T>(ctx, 0, dim[v], 0.5 * s->eps, g[v], p[v]);                    // hmc.py:50
       if (!rc) rc = axpy_t<T>(ctx, 1, dim[v], s->eps, p[v], q[v]);                     // :51
       if (v == 0) net.xw_valid = false;
-      if (!rc) rc = grad((1u << v) | (tail ? 0u : 1u << o[(i + 1) % 6]));              // :52
+      if (!rc) rc = grad(tail ? 63u : (1u << v) | (1u << o[(i + 1) % 6]));            // :52
       if (!rc) rc = axpy_t<T>(ctx, 0, dim[v], s->eps, g[v], p[v]);                     // :53
       if (rc) return rc;
     }

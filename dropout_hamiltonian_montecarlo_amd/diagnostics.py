@@ -8,7 +8,7 @@ split-R̂ over chain halves, ESS with Geyer's initial monotone sequence.
 Two implementations of the same definitions: `device_diagnostics` runs them on the GPU where the RCCL
 all-gather leaves the chain summaries (libhmcx hmcx_chain_diagnostics, csrc/hmcx_diag.hip, one thread
 per parameter); the NumPy functions below are the host version used by CPU-only (gloo) runs and as the
-reference the device kernel is tested against (tests/test_gpu_rccl.py).
+reference the device kernel is tested against (tests/test_gpu_diagnostics.py).
 """
 import numpy as np
 

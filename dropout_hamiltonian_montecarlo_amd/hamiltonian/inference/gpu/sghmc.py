@@ -376,6 +376,7 @@ class sghmc(sgmcmc):
             a = x['args']
             a.out_abort = None
             ctx.check(ctx.lib.hmcx_sghmc_run(ctx.h, a), "hmcx_sghmc_run (recovery)")
+            ctx.note_recovery("persistent_sghmc")                  # one per re-run call (hmcx_get_recoveries)
             x['host'][:x['nbytes']].copy_(x['dev'][:x['nbytes']])
             x['host'][36 * x['n_steps'] * x['C']:x['nbytes']].zero_()
             x['recovered'] = True

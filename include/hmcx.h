@@ -212,7 +212,8 @@ int hmcx_clear_abort(hmcx_ctx* ctx);
 /* Fallback bookkeeping.  Every path that re-runs work after a timed-out cross-workgroup exchange
  * is counted per context, so a test suite, smoke check or benchmark can require that none happened
  * (a re-run gives the right result, which is exactly why it must not go unnoticed):
- *   HMCX_RECOVERY_PERSISTENT  hmcx_clear_abort calls: the caller re-runs persistent SGHMC calls
+ *   HMCX_RECOVERY_PERSISTENT  persistent SGHMC calls re-run after a timed-out launch (hmcx_clear_abort
+ *                             itself counts nothing; the host code that re-runs records each call)
  *   HMCX_RECOVERY_MLP_FUSED   hmcx_mlp_sghmc_run calls re-run unfused after their out_abort verdict
  *                             (the host code that re-runs records it: hmcx_note_recovery)
  *   HMCX_RECOVERY_WIDE_FUSED  hmcx_sgld_run calls whose fused forward + softmax timed out and that
@@ -394,8 +395,9 @@ int hmcx_mlp_sghmc_run(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* a);
  * gpu/hmc.py step with models/gpu/mlp.py grad).  With g = grad(q) first, per iteration and per
  * variable v in order[0..5]:  p_v −= ε/2·g_v;  q_v += ε·p_v;  g = grad(q);  p_v −= ε·g_v  (hmc.py:50-53),
  * then p = −p (hmc.py:55-56, as p − 2·p).  grad is hmcx_mlp_grad (∇ mean CE + ½·alpha·θ, all six
- * variables, 1 + 6·n_iter calls); the kicks and drifts are hmcx_axpy's — the same kernels in the same
- * order as the host loop, so the trajectory is bit-identical to it.  Masks per gradient call:
+ * variables, 1 + 6·n_iter calls; every call but the last computes only the one or two components the
+ * next kicks read, the last one all six); the kicks and drifts are hmcx_axpy's — the same kernels in
+ * the same order as the host loop, so the trajectory is bit-identical to it.  Masks per gradient call:
  *   HMCX_MLP_MASKS_NONE    no dropout;
  *   HMCX_MLP_MASKS_FIXED   masks [3][B][n_mid] (dtype) for every call;
  *   HMCX_MLP_MASKS_PHILOX  call k draws hmcx_mlp_masks(seed, chain, step, slot0 + k) into masks (scratch).

@@ -38,7 +38,7 @@ def _gpu_context_guard(request):
     before = {}
     if gpu:
         nat, ctxs = _contexts()
-        before = {id(c): c.recoveries() for c in ctxs if getattr(c, "h", None)}
+        before = {id(c): c.recoveries() for c in ctxs if getattr(c, "h", None)}   # None: a build without counters
     yield
     if not gpu:
         return
@@ -48,8 +48,8 @@ def _gpu_context_guard(request):
         if not getattr(c, "h", None):
             continue
         now = c.recoveries()
-        was = before.get(id(c), dict.fromkeys(now, 0))
-        d = {k: now[k] - was[k] for k in now if now[k] != was[k]}
+        was = before.get(id(c)) or dict.fromkeys(now or (), 0)
+        d = {k: now[k] - was[k] for k in now if now[k] != was[k]} if now is not None else {}
         if d:
             moved[str(c.device)] = d
         c.set_sghmc_path(0)

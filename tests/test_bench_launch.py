@@ -19,7 +19,7 @@ def _env(**kw):
     return env
 
 
-@pytest.mark.parametrize("n", [2, 3])
+@pytest.mark.parametrize("n", [2, 3, 8])   # 8: the driver's 8-GPU node, rehearsed over gloo
 def test_bench_spawns_n_ranks_dry_run(n):
     r = subprocess.run([sys.executable, "bench.py", "--gpus", str(n), "--steps", "7", "--warmup", "1", "--dry-run"],
                        cwd=REPO, env=_env(CUDA_VISIBLE_DEVICES=""), capture_output=True, text=True, timeout=300)

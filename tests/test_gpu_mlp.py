@@ -298,12 +298,14 @@ def test_mlp_fused_timeout_is_recovered_in_process(monkeypatch, capfd):
     undisturbed run's — bit-exact path lengths / accept flags, states within rel 1e-10 (the fused and
     unfused launches differ only in the summation order of the logits)."""
     ref_post, ref_logp, ref_tr, m = _mlp_f64_run()
+    before = m.ctx.recoveries()["mlp_fused"]
     try:
         post, logp, tr, m = _mlp_f64_run(monkeypatch, force=3)
         err = capfd.readouterr().err
         assert "re-running the call unfused" in err
         assert not m.ctx.mlp_fuse
-        assert m.ctx.recoveries()["mlp_fused"] >= 1                   # counted (hmcx_get_recoveries)
+        # exactly the forced call is re-run (the context stays unfused after it): counted once
+        assert m.ctx.recoveries()["mlp_fused"] == before + 1
         assert [t["L"] for t in tr] == [t["L"] for t in ref_tr]
         assert [t["accepted"] for t in tr] == [t["accepted"] for t in ref_tr]
         for k in ref_post:
@@ -549,3 +551,24 @@ def test_hmc_mlp_device_leapfrog_equals_host_loop(monkeypatch, dtype, masks):
     np.testing.assert_array_equal(loss_d, loss_h)
     for k in start:
         np.testing.assert_array_equal(np.asarray(post_d[k]), np.asarray(post_h[k]))
+
+
+@pytest.mark.parametrize("n_iter", [0, 1, 3])
+@pytest.mark.parametrize("masks", ["off", "fixed"])
+def test_hmc_mlp_leapfrog_returns_full_gradient_at_final_position(n_iter, masks):
+    """hmcx_mlp_hmc_leapfrog's contract (include/hmcx.h): on return g holds the gradient of all six
+    variables at the final position — also with n_iter = 0 — as one hmcx_mlp_grad call at that q
+    with the same masks gives it (hmc.py:52 is the gradient the trajectory ends on)."""
+    mlp, _ = _mlp_cls()
+    n_in, n_mid, n_out, B = 24, 20, 5, 40
+    par, X, y, mk = _problem(31, B, n_in, n_mid, n_out)
+    m = mlp({"alpha": 0.01}, n_in, n_mid, n_out, dtype=torch.float64, device="cuda:0", seed=5)
+    keys = ['/l2/W', '/l1/b', '/l3/b', '/l1/W', '/l3/W', '/l2/b']
+    rs = np.random.RandomState(2)
+    q = {k: torch.as_tensor(par[k], device="cuda:0").contiguous() for k in keys}
+    p = {k: torch.as_tensor(rs.normal(size=par[k].shape), device="cuda:0").contiguous() for k in keys}
+    margs = "off" if masks == "off" else [mk[0], mk[1], mk[2]]
+    g = m.leapfrog_device(q, p, n_iter, 0.005, keys, masks=margs, X_train=X, y_train=y)
+    ref = m.grad({k: q[k] for k in keys}, masks=margs, X_train=X, y_train=y)
+    for k in keys:
+        _close(g[k].cpu().numpy(), ref[k].cpu().numpy(), 1e-12)

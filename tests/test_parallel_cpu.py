@@ -143,3 +143,63 @@ def test_gloo_world2_gather():
     for p, (o, e) in zip(procs, outs):
         assert p.returncode == 0, e[-2000:]
         assert "ok" in o.split()
+
+
+WORKER8 = r"""
+import os, sys
+sys.path.insert(0, os.environ["REPO"])
+import numpy as np
+from dropout_hamiltonian_montecarlo_amd import parallel
+rank, world, local = parallel.init("gloo")
+assert world == 8
+P, T, THIN = 7850, 240, 4                 # the bench's sizes: config 2 (P = 7,850), 240 diagnostics draws, every 4th kept
+def draws(r):                             # rank r's one chain (BASELINE config 4: one chain per GPU)
+    rs = np.random.RandomState(500 + r)
+    return (np.cumsum(rs.normal(size=(1, T, P)), axis=1) * 0.05 + 0.01 * r)
+mine = draws(rank)
+c0, c = parallel.chain_block(8, rank, world)
+assert (c0, c) == (rank, 1)
+w = parallel.Welford((1, P)).update(mine)
+n, means, M2, tr = parallel.gather_summaries(w, mine[:, ::THIN], device=None)
+assert n == T and means.shape == (8, P) and M2.shape == (8, P) and tr.shape == (8, T // THIN, P)
+if rank == 0:
+    allx = np.concatenate([draws(r) for r in range(world)])            # [8, T, P], rank order
+    np.testing.assert_allclose(means, allx.mean(axis=1), rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(M2, ((allx - allx.mean(axis=1, keepdims=True)) ** 2).sum(axis=1), rtol=1e-10)
+    np.testing.assert_array_equal(tr, allx[:, ::THIN])
+    s = parallel.summary_diagnostics(n, means, M2, tr)
+    assert s["chains"] == 8 and s["params"] == P and s["trace_draws_per_chain"] == 60 and s["draws_per_chain"] == T
+    ref_sr = parallel.diagnostics.split_rhat(allx[:, ::THIN])
+    assert abs(s["split_rhat"]["median"] - float(np.median(ref_sr))) < 1e-12
+    assert s["rhat"]["min"] > 1.0 and s["ess"]["min"] > 0
+# the N = 8 line: both aggregates over the gathered per-rank numbers (bench.aggregate_ranks)
+import bench
+lf = 182.0 + 7 * rank
+per = parallel.gather_objects({"leapfrogs": lf, "seconds": 1.7e-3 * lf / 182.0})
+agg = bench.aggregate_ranks(per, P_dim=P)
+tot = sum(182.0 + 7 * r for r in range(world))
+assert abs(agg["value_makespan"] - tot / (1.7e-3 * (182.0 + 49) / 182.0) * P) < 1e-6 * agg["value_makespan"]
+assert abs(agg["value_chain_throughput"] - world * 182.0 / 1.7e-3 * P) < 1e-6 * agg["value_chain_throughput"]
+parallel.barrier()
+parallel.finalize()
+print("ok", rank)
+"""
+
+
+def test_gloo_world8_gather_at_bench_sizes():
+    """World-8 rehearsal of the driver's 8-GPU run (configs 4 and 5: one chain per rank, reference
+    sghmc_multicore.py:81-99 concatenates the workers' posteriors): the per-chain summaries at the
+    bench's real sizes (P = 7,850, 240 draws, 60 thinned) in one all-gather over gloo, R̂ / split-R̂ /
+    ESS on rank 0 against the same statistics of the concatenated draws, and both aggregates of the
+    N = 8 line."""
+    port = _free_port()
+    procs = []
+    for r in range(8):
+        env = dict(os.environ, REPO=REPO, RANK=str(r), WORLD_SIZE="8", LOCAL_RANK=str(r), OMP_NUM_THREADS="1",
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), CUDA_VISIBLE_DEVICES="")
+        procs.append(subprocess.Popen([sys.executable, "-c", WORKER8], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    outs = [p.communicate(timeout=400) for p in procs]
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0, e[-2000:]
+        assert "ok" in o.split()
