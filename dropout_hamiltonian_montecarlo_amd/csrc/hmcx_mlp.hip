@@ -955,6 +955,285 @@ __global__ __launch_bounds__(MM_NT) void k_l3_wide(MMArgs<T> a, const T* z) {
   l3_backward<T, MK>(a, zt, zs, m0, blockIdx.x, scr, MM_NT, 0, a.n_mid, true);
 }
 
+// ------------------------------------------------------------------ forwards by row block (k_fwdr)
+// The forwards of a batched iteration (mlp.py:30-31 + the loss of :52 and its layer-3 backward), one
+// workgroup per (16-row block, problem), holding ALL n_mid columns of its rows: layer 3 contracts over
+// those columns, so the logits, the cross-entropy and the layer-3 backward of the block need no other
+// workgroup — no cross-workgroup exchange, no co-residency requirement, and all six forwards of an
+// iteration (plus the energy forwards that ride along) fit one launch.  Measured on the layer-2 GEMM
+// alone (tools/microbench_fwdr.hip): 9.5 µs for six problems, flat in the problem count, against
+// 8.3 µs for k_mm's 32 × 32 tiles before their exchange.
+//   * h1 = max((xw + b1)·m0, 0) of the 16 rows is built once into LDS (A);
+//   * wave w computes h2ᵀ for the columns n ∈ [32w, 32w + 32) over all of K = n_mid: A = W2 rows
+//     (16-byte loads along k, three chunks in flight), B = h1ᵀ from LDS.  The accumulator layout (rows
+//     n, columns r = lane & 15) is the B-operand layout of the layer-3 MFMA, so d3 never leaves the
+//     registers: zᵀ[o][r] = Σ_n W3[o][n]·d3[r][n] is 8 more MFMAs per wave, then a fixed-order sum over
+//     the waves in LDS;
+//   * cross-entropy with 16 lanes per row (ce_rows_lanes' formula), then the layer-3 backward as MFMAs
+//     in the same layout: ga2ᵀ = W3ᵀ·gzᵀ, the W3 partial (gzᵀ·d3)ᵀ from the d3 tile in LDS, the b2 / b3
+//     partials as fixed-order sums over the block's rows.
+// Partials are per 16-row block (nparts = ⌈B/16⌉).  Float32 results differ from the k_mm path by
+// summation order only (K in one MFMA chain instead of split over the waves; slice partials of the
+// logits summed in T instead of double).
+constexpr int FR_ROWS = 16;
+constexpr int FR_NW = 8;                 // waves per workgroup: n_mid ≤ 32·FR_NW
+constexpr int FR_NMAX = 32 * FR_NW;
+constexpr int FR_MAXP = 8;               // problems per launch: six sub-steps + E_new + E_current
+template <typename T> struct RbFwdProb {
+  const T* xw; const T* b1; const T* W2; const T* b2; const T* W3; const T* b3;
+  MaskSrc<T> ms;
+  T* ga2; T* pb2; T* pb3; T* pw3;        // outputs, null when not wanted; partials [⌈B/16⌉][…]
+  double* lpart;                         // loss partial of each 16-row block (null: none)
+};
+template <typename T> struct RbFwdArgs {
+  int M, n_mid, n_out, np;
+  const int32_t* y;
+  RbFwdProb<T> p[FR_MAXP];
+  PendSet<T> pend;                       // pending updates: run by the extra plane blockIdx.y == np
+};
+
+template <typename T, int MK>
+__global__ __launch_bounds__(FR_NW * 64) void k_fwdr(RbFwdArgs<T> a) {
+  using Mf = mfma16<T>;
+  constexpr int AP = FR_NMAX + 16 / (int)sizeof(T);               // pitch ≡ 4 dwords (mod 64): conflict-free
+  __shared__ T At[FR_ROWS][AP];                                   // h1 tile, then the d3 tile
+  __shared__ T w3s[16][FR_NMAX];                                  // W3 (rows ≥ n_out zero)
+  __shared__ T zr[FR_NW][16][17];                                 // per-wave logit partials zᵀ[o][r]
+  __shared__ T gzs[16][17];                                       // gz[r][o]
+  __shared__ double rowl[FR_ROWS];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lg = lane >> 4;
+  if ((int)blockIdx.y == a.np) {                                  // the pending updates' plane
+    run_pendset(a.pend, (int)blockIdx.x, (int)gridDim.x);
+    return;
+  }
+  const RbFwdProb<T>& P = a.p[blockIdx.y];
+  const int rb = blockIdx.x, m0 = rb * FR_ROWS, nm = a.n_mid, No = a.n_out, M = a.M;
+  const int nwv = (nm + 31) / 32;                                  // waves with columns
+  const int n0 = 32 * wave;
+  const bool wact = wave < nwv;
+  constexpr int V = 16 / sizeof(T);
+  // labels of the cross-entropy rows, b3, and W3 into LDS: before anything waits on memory
+  const int32_t yv = a.y[min(m0 + (tid >> 4), M - 1)];
+  const T b3v = P.b3[min(tid & 15, No - 1)];
+  for (int e = tid; e < 16 * FR_NMAX; e += FR_NW * 64) {
+    const int o = e / FR_NMAX, n = e % FR_NMAX;
+    const bool ok = o < No && n < nm;
+    const T w = P.W3[ok ? (size_t)o * nm + n : 0];
+    w3s[o][n] = ok ? w : T(0);
+  }
+  // h1 = max((xw + b1)·m0, 0) of the 16 rows (rows past M: 0)
+  for (int e = tid; e < FR_ROWS * nm / V; e += FR_NW * 64) {
+    const int r = e / (nm / V), c = (e % (nm / V)) * V, m = m0 + r;
+    const bool ok = m < M;
+    const size_t base = ok ? (size_t)m * nm + c : 0;
+    T x[V], bb[V], mk[V];
+    if constexpr (V == 4) {
+      const float4 w = *reinterpret_cast<const float4*>(P.xw + base);
+      x[0] = w.x; x[1] = w.y; x[2] = w.z; x[3] = w.w;
+    } else {
+      const double2 w = *reinterpret_cast<const double2*>(P.xw + base);
+      x[0] = w.x; x[1] = w.y;
+    }
+#pragma unroll
+    for (int q = 0; q < V; ++q) bb[q] = P.b1[c + q];
+    mvals<T, V, MK>(P.ms, 0, base, mk);
+#pragma unroll
+    for (int q = 0; q < V; ++q) At[r][c + q] = ok ? op_apply<T, OP_H1>(x[q], mk[q], bb[q]) : T(0);
+  }
+  // epilogue operands of this lane's 8 elements (r = lr, n = n0 + 16j + row(q)): b2 and the m1 / m2 masks
+  const int r = lr, m = m0 + r;
+  const bool rok = m < M;
+  T b2v[2][4];
+  MRaw<T> m1r[2][4], m2r[2][4];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int n = n0 + 16 * j + Mf::row(lane, q);
+      const bool ok = rok && n < nm;
+      const size_t i = ok ? (size_t)m * nm + n : 0;
+      b2v[j][q] = P.b2[ok ? n : 0];
+      m1r[j][q] = mraw<T, MK>(P.ms, 1, i);
+      m2r[j][q] = mraw<T, MK>(P.ms, 2, i);
+    }
+  __syncthreads();
+  // layer 2, transposed: acc[j] = h2ᵀ[n0 + 16j + row][r] over all of K = n_mid
+  typename Mf::acc_t acc[2] = {Mf::zero(), Mf::zero()};
+  if (wact) {
+    T bv[3][4][2];
+    auto load = [&](int s, int k0) {
+      load_chunk<T, OP_PLAIN, 0, 1, MK_NONE>(bv[s], P.W2, nm, n0, nm, k0, nm, lr, lg, P.ms, nullptr);
+    };
+    auto mf = [&](int s, int k0) {
+      T hv[4];                                                     // h1[lr][k0 + kmap(u, lg)]: 16-byte LDS reads
+      if constexpr (sizeof(T) == 4) {
+        const float4 w = *reinterpret_cast<const float4*>(&At[lr][k0 + 4 * lg]);
+        hv[0] = w.x; hv[1] = w.y; hv[2] = w.z; hv[3] = w.w;
+      } else {
+        const double2 w0 = *reinterpret_cast<const double2*>(&At[lr][k0 + 2 * lg]);
+        const double2 w1 = *reinterpret_cast<const double2*>(&At[lr][k0 + 8 + 2 * lg]);
+        hv[0] = w0.x; hv[1] = w0.y; hv[2] = w1.x; hv[3] = w1.y;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[j] = Mf::fma(bv[s][u][j], hv[u], acc[j]);
+    };
+    load(0, 0);
+    if (16 < nm) load(1, 16);
+    if (32 < nm) load(2, 32);
+    for (int k0 = 0; k0 < nm; k0 += 48) {
+      mf(0, k0);
+      if (k0 + 48 < nm) load(0, k0 + 48);
+      if (k0 + 16 < nm) {
+        mf(1, k0 + 16);
+        if (k0 + 64 < nm) load(1, k0 + 64);
+      }
+      if (k0 + 32 < nm) {
+        mf(2, k0 + 32);
+        if (k0 + 80 < nm) load(2, k0 + 80);
+      }
+    }
+  }
+  // h2 = max((z2 + b2)·m1, 0), d3 = h2·m2 (mlp.py:30-31), kept in registers
+  T dv[2][4], hp[2][4], m1v[2][4], m2v[2][4];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      mpin<T, MK>(m1r[j][q]);
+      mpin<T, MK>(m2r[j][q]);
+      const int n = n0 + 16 * j + Mf::row(lane, q);
+      const bool ok = rok && n < nm;
+      m1v[j][q] = mfin<T, MK>(P.ms, m1r[j][q]);
+      m2v[j][q] = mfin<T, MK>(P.ms, m2r[j][q]);
+      const T t = (acc[j][q] + b2v[j][q]) * m1v[j][q];
+      const T h = t > T(0) ? t : T(0);
+      hp[j][q] = h > T(0) ? T(1) : T(0);
+      dv[j][q] = ok ? h * m2v[j][q] : T(0);
+    }
+  __syncthreads();                                                 // every wave is done with the h1 tile
+  // layer 3: zᵀ[o][r] = Σ_n W3[o][n]·d3[r][n] over this wave's columns (k index n = n0 + 16j + row(u))
+  {
+    typename Mf::acc_t za = Mf::zero();
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int n = n0 + 16 * j + Mf::row(lane, u);
+        za = Mf::fma(w3s[lr][min(n, FR_NMAX - 1)], dv[j][u], za);
+        At[r][min(n, FR_NMAX - 1)] = dv[j][u];                     // the d3 tile, for the W3 partial
+      }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) zr[wave][Mf::row(lane, q)][lr] = za[q];
+  }
+  __syncthreads();
+  // cross-entropy of the block's rows, 16 lanes per row (F.softmax_cross_entropy, mean over M)
+  if (tid < 256) {
+    const int rr = tid >> 4, k = tid & 15, mm = m0 + rr;
+    const bool kin = k < No;
+    T z = zr[0][k][rr];
+    for (int w = 1; w < nwv; ++w) z += zr[w][k][rr];
+    z = kin ? z + b3v : T(0);
+    T mx = kin ? z : -INFINITY;
+#pragma unroll
+    for (int w = 8; w >= 1; w >>= 1) {                               // NaN propagates as in np.max
+      const T o = __shfl_xor(mx, w, 16);
+      mx = (o > mx || o != o) ? o : mx;
+    }
+    T e = kin ? exp(z - mx) : T(0);
+#pragma unroll
+    for (int w = 8; w >= 1; w >>= 1) e += __shfl_xor(e, w, 16);
+    const T ls = log(e);
+    double l = (kin && k == yv && mm < M) ? -(double)((z - mx) - ls) : 0.0;
+    T g = T(0);
+    if (kin && mm < M) {
+      g = exp((z - mx) - ls);
+      if (k == yv) g -= T(1);
+      g = g / (T)M;
+    }
+    gzs[rr][k] = g;
+#pragma unroll
+    for (int w = 8; w >= 1; w >>= 1) l += __shfl_xor(l, w, 16);
+    if (k == 0) rowl[rr] = l;
+  }
+  __syncthreads();
+  if (tid == 0 && P.lpart) {
+    double s = 0.0;
+    for (int q = 0; q < FR_ROWS; ++q) s += rowl[q];
+    P.lpart[rb] = s;
+  }
+  if (P.pb3 && tid < No) {                                           // b3 partial: Σ_rows gz
+    T cs = T(0);
+    for (int q = 0; q < FR_ROWS; ++q) cs += gzs[q][tid];
+    P.pb3[(size_t)rb * No + tid] = cs;
+  }
+  if (!wact) return;
+  // layer-3 backward (k index o = 4·lg + u < 16): ga2ᵀ[n][r] = Σ_o W3[o][n]·gz[r][o], then
+  // ga2 = ((·)·m2)·[h2 > 0]·m1 in the layer-2 accumulator layout
+  if (P.ga2 || P.pb2) {
+    typename Mf::acc_t ga[2] = {Mf::zero(), Mf::zero()};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int o = 4 * lg + u;
+      const T gzv = gzs[lr][o];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) ga[j] = Mf::fma(w3s[o][min(n0 + 16 * j + lr, FR_NMAX - 1)], gzv, ga[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      T gv[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        T t = ga[j][q] * m2v[j][q];
+        t = t * hp[j][q];
+        t = t * m1v[j][q];
+        const int n = n0 + 16 * j + Mf::row(lane, q);
+        gv[q] = (rok && n < nm) ? t : T(0);
+      }
+      if (P.ga2 && rok) {
+        if constexpr (sizeof(T) == 4) {                              // rows 4·lg … 4·lg + 3: one float4
+          const int n = n0 + 16 * j + 4 * lg;
+          if (n < nm) *reinterpret_cast<float4*>(P.ga2 + (size_t)m * nm + n) = make_float4(gv[0], gv[1], gv[2], gv[3]);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int n = n0 + 16 * j + Mf::row(lane, q);
+            if (n < nm) P.ga2[(size_t)m * nm + n] = gv[q];
+          }
+        }
+      }
+      if (P.pb2) {                                                   // b2 partial: Σ over the block's rows
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          T s = gv[q];
+#pragma unroll
+          for (int w = 1; w < 16; w <<= 1) s += __shfl_xor(s, w, 16);
+          const int n = n0 + 16 * j + Mf::row(lane, q);
+          if (lr == 0 && n < nm) P.pb2[(size_t)rb * nm + n] = s;
+        }
+      }
+    }
+  }
+  // W3 partial: pw3ᵀ[n][o] = Σ_r d3[r][n]·gz[r][o] over the block's rows (k index r = 4·lg + u)
+  if (P.pw3) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      typename Mf::acc_t pw = Mf::zero();
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int rk = 4 * lg + u;
+        pw = Mf::fma(At[rk][min(n0 + 16 * j + lr, FR_NMAX - 1)], gzs[rk][lr], pw);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int n = n0 + 16 * j + Mf::row(lane, q);
+        if (lr < No && n < nm) P.pw3[(size_t)rb * No * nm + (size_t)lr * nm + n] = pw[q];
+      }
+    }
+  }
+}
+
 // Keep flags of forward f, one bit per element (bit e % 32 of word e / 32; forward f's words start at
 // f·⌈n3/32⌉).  Thread g draws Philox block g (flags 4g … 4g + 3, flag e = keep_flag(word e % 4)); eight
 // neighbouring lanes OR their nibbles into one word, which the first of them stores.
@@ -1092,8 +1371,8 @@ __global__ __launch_bounds__(256) void k_sumsq12(VarTab vt, double* part) {
 // MH accept (hmc.py:67-79): E = nlp + ½Σp², nlp = loss + log_prior, log_prior = −Σ_v ½α·Σθ²/dim.
 struct MlpAccept {
   const double* part_cur; const double* part_new;   // [2][6][NPART]
-  const double* lp_cur; const double* lp_new;       // loss partials [nlb]
-  int nlb, B;
+  const double* lp_cur; const double* lp_new;       // loss partials [nlb_cur] / [nlb_new]
+  int nlb_cur, nlb_new, B;
   int dim[6];
   double alpha, u;
   double* out_A; int32_t* out_acc; double* out_loss; double* out_nlp; double* out_E;
@@ -1111,7 +1390,8 @@ static __global__ __launch_bounds__(1024) void k_mlp_accept(MlpAccept a) {
     for (int q = 0; q < NPART / 32; ++q) x += pp[q * 32 + j];
   } else if (g < 26) {
     const double* lp = g == 24 ? a.lp_cur : a.lp_new;
-    for (int b = j; b < a.nlb; b += 32) x += lp[b];
+    const int nb = g == 24 ? a.nlb_cur : a.nlb_new;
+    for (int b = j; b < nb; b += 32) x += lp[b];
   }
   if (g < 26) sh[g][j] = x;
   __syncthreads();
@@ -1171,6 +1451,8 @@ struct MlpNet {
   T *xw, *h2, *d3, *z, *gz, *ga2, *ga1;
   T* h1 = nullptr; bool h1_valid = false;   // h1 of the last fused forward (when its sub-step needs it)
   T *pb1, *pb2, *pb3, *pw3;              // gradient partials of b1, b2, b3, W3 ([nlb][...])
+  T *fpb2 = nullptr, *fpb3 = nullptr, *fpw3 = nullptr;   // the same partials per 16-row block (k_fwdr, [nrb][...])
+  int nrb = 0;                           // 16-row blocks: ⌈B/16⌉
   hipStream_t st;
   bool xw_valid = false;
   bool vec_masks = true;                 // masks may be read as 4-/2-element vectors
@@ -1194,6 +1476,7 @@ struct MlpNet {
 template <typename T>
 void net_init(MlpNet<T>& net, int B, int n_in, int n_mid, int n_out, hipStream_t st) {
   net.B = B; net.n_in = n_in; net.n_mid = n_mid; net.n_out = n_out; net.nlb = (B + 31) / 32; net.st = st;
+  net.nrb = (B + FR_ROWS - 1) / FR_ROWS;
   net.vec_masks = n_mid % 4 == 0;
 }
 
@@ -1583,6 +1866,66 @@ hipError_t mlp_l23_ga1(MlpNet<T>& net, const SubStep<T>* const* fw, int nf, cons
   return hipErrorInvalidValue;
 }
 
+// k_fwdr in the batched sampler: float32 (the bench's dtype; float64 keeps the k_mm forwards), n_mid a
+// multiple of 32 up to 256, n_out ≤ 16, keep-flag or buffer masks, 16-byte aligned xw / W2 rows and
+// masks.  HMCX_MLP_FWDR=0 (read per call) keeps the k_mm fused forwards (MM_L23) — whose results the
+// one-sub-step-at-a-time order reproduces bit for bit.
+template <typename T>
+bool fwdr_ok(const MlpNet<T>& net, const SubStep<T>* ss, int n) {
+  const char* env = getenv("HMCX_MLP_FWDR");
+  if ((env && env[0] == '0') || sizeof(T) != 4) return false;
+  if (net.n_mid % 32 || net.n_mid > FR_NMAX || net.n_out > 16 || !net.vec_masks || !net.fpb2) return false;
+  const int mk = mask_kind(ss[0].ms);
+  if (mk != MK_KEEP && mk != MK_VALS) return false;
+  for (int i = 0; i < n; ++i) {
+    const T* xw = ss[i].xw ? ss[i].xw : net.xw;
+    if (!vec_ok(xw, net.n_mid, sizeof(T)) || !vec_ok(ss[i].q[2], net.n_mid, sizeof(T)) || mask_kind(ss[i].ms) != mk)
+      return false;
+  }
+  return true;
+}
+
+// The forwards of np problems (sub-steps and energy forwards) in one k_fwdr launch: sub-step v writes
+// ga2 when a backward reads it (W1, b1: the layer-1 backward; W2: its gradient) and the 16-row-block
+// partials of its own bias / W3 gradient into its net's fpb2 / fpw3 / fpb3; energy forwards (v < 0)
+// only their loss partials.  net's pending updates run in the extra plane.
+template <typename T>
+hipError_t mlp_fwdr(MlpNet<T>& net, const SubStep<T>* const* ss, int np) {
+  if (np < 1 || np > FR_MAXP) return hipErrorInvalidValue;
+  RbFwdArgs<T> a{};
+  a.M = net.B; a.n_mid = net.n_mid; a.n_out = net.n_out; a.np = np; a.y = net.y;
+  for (int p = 0; p < np; ++p) {
+    const SubStep<T>& x = *ss[p];
+    RbFwdProb<T>& q = a.p[p];
+    q.xw = x.xw ? x.xw : net.xw;
+    q.b1 = x.q[1]; q.W2 = x.q[2]; q.b2 = x.q[3]; q.W3 = x.q[4]; q.b3 = x.q[5];
+    q.ms = x.ms;
+    q.ga2 = (x.v >= 0 && x.v <= 2) ? x.scr->ga2 : nullptr;
+    q.pb2 = x.w.pb2 ? x.scr->fpb2 : nullptr;
+    q.pw3 = x.w.pw3 ? x.scr->fpw3 : nullptr;
+    q.pb3 = x.w.pb3 ? x.scr->fpb3 : nullptr;
+    q.lpart = x.v < 0 ? x.lpart : nullptr;
+  }
+  a.pend = net.pend;
+  net.pend.n = 0;
+  const dim3 grid((unsigned)net.nrb, (unsigned)(np + (a.pend.n > 0 ? 1 : 0)));
+  if constexpr (sizeof(T) == 4) {                              // float32 only (fwdr_ok)
+    if (mask_kind(a.p[0].ms) == MK_KEEP) hipLaunchKernelGGL((k_fwdr<T, MK_KEEP>), grid, dim3(FR_NW * 64), 0, net.st, a);
+    else hipLaunchKernelGGL((k_fwdr<T, MK_VALS>), grid, dim3(FR_NW * 64), 0, net.st, a);
+    return hipGetLastError();
+  }
+  return hipErrorInvalidValue;
+}
+
+// The layer-1 backwards of np sub-steps (W1, b1) in one batched launch.
+template <typename T>
+hipError_t mlp_ga1_batch(MlpNet<T>& net, const SubStep<T>* const* ss, int np) {
+  MMArgs<T> a;
+  MMProbs<T> pr{};
+  ga1_build(net, ss, np, a, pr);
+  return mm<T, MM_GA1, 0, 0, OP_PLAIN, OP_PLAIN, true>(net, a, &pr);
+}
+
 // Layer 1 of the next iteration (xw = X·W1ᵀ into `out`, net's X) and the W2 gradient of sub-step net
 // `w2n` in one launch (k_mm2): the W2 gradient reads the CURRENT iteration's xw (another buffer) and
 // writes only W2's momentum and next position; layer 1 reads only X and W1.  False: the operands are
@@ -1661,6 +2004,14 @@ void set_pending(MlpNet<T>& net, int v, int mode, const Upd<T>& u, const MlpNet<
     case 4: p.part = src->pw3; p.n = net.n_out * net.n_mid; break;
     default: p.part = src->pb3; p.n = net.n_out; break;
   }
+}
+
+// The same from explicit partials [nparts][n] (k_fwdr's per-16-row-block partials).
+template <typename T>
+void set_pending_part(MlpNet<T>& net, int v, int mode, const Upd<T>& u, const T* part, int nparts) {
+  Pending<T>& p = net.pend.p[net.pend.n++];
+  p.mode = mode; p.u = u; p.nparts = nparts; p.part = part;
+  p.n = v == 4 ? net.n_out * net.n_mid : (v == 5 ? net.n_out : net.n_mid);
 }
 
 template <typename T>
@@ -1945,7 +2296,11 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
       net_init(pn[i], s->B, s->n_in, s->n_mid, s->n_out, ctx->stream);
       mlp_workspace<T>(ws, pn[i]);
       pn[i].lpart_scr = ws.take<double>(net.nlb);
+      pn[i].fpb2 = ws.take<T>((size_t)net.nrb * s->n_mid);       // k_fwdr's 16-row-block partials
+      pn[i].fpw3 = ws.take<T>((size_t)net.nrb * s->n_out * s->n_mid);
+      pn[i].fpb3 = ws.take<T>((size_t)net.nrb * s->n_out);
     }
+    net.fpb2 = batch ? pn[0].fpb2 : nullptr;                       // marks the buffers as present (fwdr_ok)
     net.prof = prof_cap ? ws.take<unsigned long long>((size_t)prof_cap * net.nlb * ((net.n_mid + 31) / 32) * L23_NPH)
                         : nullptr;
     net.prof_cap = prof_cap;
@@ -1960,8 +2315,8 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
     }
     part_cur = ws.take<double>(12 * NPART);
     part_new = ws.take<double>(12 * NPART);
-    lp_cur = ws.take<double>(net.nlb);
-    lp_new = ws.take<double>(net.nlb);
+    lp_cur = ws.take<double>(std::max(net.nlb, net.nrb));        // 32-row (k_mm) or 16-row (k_fwdr) partials
+    lp_new = ws.take<double>(std::max(net.nlb, net.nrb));
     lp_scr = ws.take<double>(net.nlb);
     if (keep_arr) keep = ws.take<uint32_t>((size_t)maxF * kw);
     accf = ws.take<int32_t>(1);
@@ -2017,6 +2372,7 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
     T* cur[6];
     for (int v = 0; v < 6; ++v) cur[v] = par[v];
     int fwd = 0;
+    bool e_fr[2] = {false, false};                            // E_new / E_current by k_fwdr (16-row partials)
     auto upd_for = [&](int it, int v, T* W, T* Qn) {
       Upd<T> u{};
       u.W = W; u.P = pv[v]; u.Qn = Qn;
@@ -2091,6 +2447,39 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
         }
         int i2 = 0;                                              // position of the W2 sub-step
         while (s->order[i2] != 2) ++i2;
+        {
+          // 4 launches: every forward of the iteration and the energy forwards due, in ONE k_fwdr launch
+          // | the W1 / b1 layer-1 backwards | the W1 gradient + every pending update | the next
+          // iteration's layer 1 beside this iteration's W2 gradient
+          const SubStep<T>* fa[FR_MAXP];
+          SubStep<T> chk[FR_MAXP];
+          int na = 0;
+          for (int i = 0; i < 6; ++i) fa[na++] = &ss[i];
+          if (it == n - 1) fa[na++] = &es[0];
+          if (it == 0) fa[na++] = &es[1];
+          for (int q = 0; q < na; ++q) chk[q] = *fa[q];
+          if (fwdr_ok(net, chk, na)) {
+            if (it == n - 1) e_done[0] = e_fr[0] = true;
+            if (it == 0) e_done[1] = e_fr[1] = true;
+            HMCX_HIP(ctx, mlp_fwdr<T>(net, fa, na));
+            HMCX_HIP(ctx, mlp_ga1_batch<T>(net, ga, nga));
+            for (int i = 0; i < 6; ++i) {
+              const int v = s->order[i];
+              if (v == 0 || v == 2) continue;
+              const Upd<T> u = upd_for(it, v, Xit[v], it + 1 < n ? Xnx[v] : nullptr);
+              if (v == 1) set_pending(pn[0], v, UPD_SGHMC, u, &pn[i]);   // b1: the layer-1 backward's 32-row partials
+              else set_pending_part(pn[0], v, UPD_SGHMC, u, v == 3 ? pn[i].fpb2 : v == 4 ? pn[i].fpw3 : pn[i].fpb3,
+                                    net.nrb);
+            }
+            HMCX_HIP(ctx, mlp_wgrad<T>(pn[0], ss[0].q, ss[0].ms, 0, UPD_SGHMC,
+                                       upd_for(it, 0, Xit[0], it + 1 < n ? Xnx[0] : nullptr)));
+            const Upd<T> u2 = upd_for(it, 2, Xit[2], it + 1 < n ? Xnx[2] : nullptr);
+            if (it + 1 < n) HMCX_HIP(ctx, mlp_l1_w2<T>(net, Xnx[0], xwb[(it + 1) & 1], pn[i2], ss[i2], u2, &l1_done));
+            if (!l1_done) HMCX_HIP(ctx, mlp_wgrad<T>(pn[i2], ss[i2].q, ss[i2].ms, 2, UPD_SGHMC, u2));
+            fwd += 6;
+            continue;
+          }
+        }
         if (quad_ok(net, ss)) {
           // 4 launches: forwards of W1, b1, W2 (+ one more) | the other two forwards + the W1 / b1
           // layer-1 backwards | the W1 and W2 gradients + every pending update | layer 1
@@ -2178,7 +2567,9 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
     hipLaunchKernelGGL(k_sumsq12<T>, dim3(NPART, 6), dim3(256), 0, st, ve, part_new);
     MlpAccept ac{};
     ac.part_cur = part_cur; ac.part_new = part_new; ac.lp_cur = lp_cur; ac.lp_new = lp_new;
-    ac.nlb = net.nlb; ac.B = s->B;
+    ac.nlb_new = e_fr[0] ? net.nrb : net.nlb;
+    ac.nlb_cur = e_fr[1] ? net.nrb : net.nlb;
+    ac.B = s->B;
     for (int i = 0; i < 6; ++i) ac.dim[i] = dim[s->order[i]];
     ac.alpha = s->alpha; ac.u = s->u_accept[si];
     ac.out_A = s->out_A + si; ac.out_acc = s->out_accepted + si; ac.out_loss = s->out_loss + si;

@@ -250,6 +250,47 @@ def test_sghmc_mlp_config3_f64_trajectory_matches_oracle():
         np.testing.assert_allclose(post_g[k], post_r[k], rtol=1e-8, atol=1e-10)
 
 
+@pytest.mark.parametrize("fwdr", ["1", "0"])
+def test_sghmc_mlp_config3_f32_trajectory_matches_oracle(fwdr, monkeypatch):
+    """Config 3 in float32 — the bench's dtype — through the path the bench times: the batched
+    iterations with every forward of an iteration in one k_fwdr launch (HMCX_MLP_FWDR=1, default) or
+    the k_mm fused forwards (=0), buffer masks injected (MK_VALS, the keep-flag kernels' twin), against
+    the NumPy restatement in float64 at the float32-rounded inputs: 4 steps of 1-3 leapfrog
+    iterations (iterations 0 and n−1 carry the energy forwards), path lengths and accept flags
+    bit-exact, acceptance probabilities within 1e-3, the state within 2e-5 of its largest entry
+    (float32 rounding through the trajectory; the kernels differ from the oracle in summation order)."""
+    mlp, sghmc = _mlp_cls()
+    monkeypatch.setenv("HMCX_MLP_FWDR", fwdr)
+    n_in, n_mid, n_out, N, B = 784, 256, 10, 1000, 500
+    rs = np.random.RandomState(11)
+    X = rs.rand(N, n_in).astype(np.float32).astype(np.float64)
+    y = rs.randint(0, n_out, N)
+    start = {k: rs.normal(0, 0.05, s).astype(np.float32).astype(np.float64)
+             for k, s in om.mlp_param_shapes(n_in, n_mid, n_out).items()}
+    get, one = _mask_stream(B, n_mid)
+    kw = dict(path_length=3e-3, step_size=1e-3, verbose=True)
+
+    o = _OracleSghmc(_MaskedOracleMLP(om.mlp({"alpha": 0.01}, n_in, n_mid, n_out), one), start, **kw)
+    o.trace, o.out = [], io.StringIO()
+    np.random.seed(21)
+    post_r, _ = o.sample(epochs=1, burnin=1, batch_size=B, rng=np.random.RandomState(22), X_train=X, y_train=y)
+
+    m = mlp({"alpha": 0.01}, n_in, n_mid, n_out, dtype=torch.float32, device="cuda:0")
+    s = sghmc(m, start, noise='numpy', **kw)
+    s.mask_provider = get
+    s.trace, s.out = [], io.StringIO()
+    np.random.seed(21)
+    post_g, _ = s.sample(epochs=1, burnin=1, batch_size=B, rng=np.random.RandomState(22), X_train=X, y_train=y)
+
+    assert len(s.trace) == len(o.trace) == 4
+    assert [t["L"] for t in s.trace] == [t["L"] for t in o.trace]
+    assert max(t["L"] for t in o.trace) >= 3                       # at least one multi-iteration trajectory
+    assert [t["accepted"] for t in s.trace] == [t["accepted"] for t in o.trace]
+    np.testing.assert_allclose([t["A"] for t in s.trace], [t["A"] for t in o.trace], rtol=0, atol=1e-3)
+    for k in start:
+        _close(post_g[k], post_r[k], 2e-5)
+
+
 @pytest.mark.parametrize("dtype,rtol", [(torch.float64, 1e-13), (torch.float32, 1e-6)])
 def test_mlp_log_prior_device_reduction(dtype, rtol):
     """mlp.log_prior (mlp.py:40-45, −Σ_var ½·alpha·Σθ²/dim) with Σθ² from hmcx_sumsq against the
@@ -332,8 +373,10 @@ def test_mlp_timeout_leaves_softmax_persistent_path_alone(monkeypatch):
 
 
 def test_mlp_timeout_reported_through_c_abi_without_out_abort(monkeypatch):
-    """Plain C callers (out_abort = NULL) get an error from the call itself."""
+    """Plain C callers (out_abort = NULL) get an error from the call itself.  The k_mm fused forwards
+    (HMCX_MLP_FWDR=0) are the launches with an exchange that can time out; k_fwdr has none."""
     from dropout_hamiltonian_montecarlo_amd import _native as nat
+    monkeypatch.setenv("HMCX_MLP_FWDR", "0")
     mlp, _ = _mlp_cls()
     n_in, n_mid, n_out, B = 784, 256, 10, 500
     m = mlp({"alpha": 0.01}, n_in, n_mid, n_out, dtype=torch.float32, device="cuda:0")
@@ -427,6 +470,9 @@ def test_batched_iterations_equal_one_at_a_time(dtype, order, monkeypatch):
         keys = list(start)
         start = {k: start[k] for k in [keys[0], keys[4], keys[2], keys[5], keys[1], keys[3]]}
     kw = dict(path_length=4e-3, step_size=1e-3, verbose=False, noise='philox', seed=7, chain=1)
+    # the k_mm fused forwards: the one-at-a-time order runs the same kernels (k_fwdr sums in another
+    # order: test_batched_fwdr_close_to_one_at_a_time)
+    monkeypatch.setenv("HMCX_MLP_FWDR", "0")
     runs = []
     for batch in ("1", "0"):
         monkeypatch.setenv("HMCX_MLP_BATCH", batch)
@@ -440,6 +486,33 @@ def test_batched_iterations_equal_one_at_a_time(dtype, order, monkeypatch):
     for k in p1:
         np.testing.assert_array_equal(p1[k], p2[k])
     np.testing.assert_array_equal(l1, l2)
+
+
+def test_batched_fwdr_close_to_one_at_a_time(monkeypatch):
+    """float32 batched iterations with k_fwdr (the default: all forwards of an iteration in one launch,
+    per-16-row-block partials) against the one-sub-step-at-a-time order on the same Philox noise and
+    masks: the same path lengths and accept flags, states within float32 summation-order differences."""
+    mlp, sghmc = _mlp_cls()
+    n_in, n_mid, n_out, N, B = 784, 256, 10, 1000, 500
+    rs = np.random.RandomState(9)
+    X = rs.rand(N, n_in)
+    y = rs.randint(0, n_out, N)
+    m = mlp({"alpha": 0.01}, n_in, n_mid, n_out, dtype=torch.float32, device="cuda:0")
+    start = m.init_params(6)
+    kw = dict(path_length=4e-3, step_size=1e-3, verbose=False, noise='philox', seed=7, chain=1)
+    monkeypatch.setenv("HMCX_MLP_FWDR", "1")
+    runs = []
+    for batch in ("1", "0"):
+        monkeypatch.setenv("HMCX_MLP_BATCH", batch)
+        s = sghmc(m, start, **kw)
+        s.trace, s.out = [], io.StringIO()
+        post, logp = s.sample(epochs=2, burnin=1, batch_size=B, X_train=X, y_train=y)
+        runs.append((post, logp, [t["L"] for t in s.trace], [t["accepted"] for t in s.trace]))
+    (p1, l1, L1, a1), (p2, l2, L2, a2) = runs
+    assert L1 == L2 and a1 == a2 and max(L1) >= 3
+    for k in p1:
+        _close(p1[k], p2[k], 2e-5)
+    np.testing.assert_allclose(l1, l2, rtol=1e-4)
 
 
 # ----------------------------------------------------------------------------- full-batch HMC (generic loop)

@@ -1,5 +1,5 @@
 """Timing probe: config 3 (MNIST MLP 784-256-256-10, B = 500) SGHMC through hmcx_mlp_sghmc_run,
-Philox noise and masks.  Usage: python tools/probe_mlp.py [f64] [steps]"""
+Philox noise and masks.  Usage: python tools/probe_mlp.py [f64] [steps] [lam=<path length>] [reps=<n>]"""
 import sys
 import time
 
@@ -22,7 +22,9 @@ P = sum(int(np.prod(s)) for s in shapes)
 ctx = nat.context(0)
 if 'graph' in sys.argv:
     ctx.set_graph_mode(True)
-eps, lam = 1e-3, 5e-3
+eps = 1e-3
+lam = next((float(a[4:]) for a in sys.argv[1:] if a.startswith('lam=')), 5e-3)
+reps = next((int(a[5:]) for a in sys.argv[1:] if a.startswith('reps=')), 1)
 L = np.ceil(2 * rs.rand(steps) * lam / eps)
 n_iter = np.maximum(0, np.ceil(L - 1)).astype(np.int32)
 u = rs.rand(steps)
@@ -53,12 +55,13 @@ ctx.check(ctx.lib.hmcx_mlp_sghmc_run(ctx.h, a), "warmup")
 torch.cuda.synchronize()
 ctx.set_timing(True)
 t0 = time.perf_counter()
-ctx.check(ctx.lib.hmcx_mlp_sghmc_run(ctx.h, a), "run")
+for _ in range(reps):
+    ctx.check(ctx.lib.hmcx_mlp_sghmc_run(ctx.h, a), "run")
 torch.cuda.synchronize()
 dt = time.perf_counter() - t0
 kms, _ = ctx.get_timing()
 ctx.set_timing(False)
-lf = float(n_iter.sum())
+lf = float(n_iter.sum()) * reps
 # FLOP per leapfrog iteration (6 sub-steps, minimal recompute): forwards + backward parts
 f_l1 = 2.0 * B * n_in * n_mid
 f_l2 = 2.0 * B * n_mid * n_mid
@@ -69,6 +72,7 @@ per_iter = (2 * fwd_full + 4 * (f_l2 + f_l3)            # sub-steps W1, b1: full
             + (f_l3 + f_l2 + f_l2)                      # b2
             + 2 * (f_l2 + f_l3 + f_l3)                  # W3, b3
             + 2 * (f_l2 + f_l1))                        # W1/b1 backward: ga1 + gW1
+print("lam %g E[L-1] %.1f " % (lam, lf / steps / reps), end="")
 print("MLP %s%s steps %d lf %.0f wall %.4f s kern %.4f s  lf/s %.1f  lf/s*P %.3e  ~GFLOP/s %.1f  acc %.3f  loss %.4f"
       % ('f64' if dtype == torch.float64 else 'f32', ' graph' if 'graph' in sys.argv else '', steps, lf, dt, kms / 1e3, lf / (kms / 1e3),
          lf / (kms / 1e3) * P, per_iter * lf / (kms / 1e3) / 1e9, out_acc.float().mean().item(),
