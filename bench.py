@@ -333,6 +333,7 @@ def batched_chains(model, X, Y, data, C, n_steps, rank):
 MLP_SHAPE = (784, 256, 10)                   # MyNetwork(784, 256, 10): two hidden layers (mlp.py:24-26)
 MLP_P = 256 * 784 + 256 + 256 * 256 + 256 + 10 * 256 + 10          # 269,322
 MLP_FLOP_PER_LEAPFROG = 1.0193e9             # SURVEY §8d "M": minimal-recompute schedule, B = 500
+MLP_LAMBDA = 2e-2                            # path length: E[L] = λ/ε + ½ ≈ 20.5, inside SURVEY §8d's 10–50
 
 
 def mlp_measure(X, lab, n_steps, rank, dtype="f32"):
@@ -344,7 +345,7 @@ def mlp_measure(X, lab, n_steps, rank, dtype="f32"):
     from dropout_hamiltonian_montecarlo_amd.hamiltonian.inference.gpu.sghmc import sghmc
     tdt = torch.float32 if dtype == "f32" else torch.float64
     m = mlp({"alpha": ALPHA}, *MLP_SHAPE, dtype=tdt)
-    s = sghmc(m, m.init_params(1), path_length=5e-3, step_size=EPS, noise="philox", seed=11, chain=rank)
+    s = sghmc(m, m.init_params(1), path_length=MLP_LAMBDA, step_size=EPS, noise="philox", seed=11, chain=rank)
     s.out = io.StringIO()
     state = s._init_state()
     Xd = torch.as_tensor(X).to(m.device, tdt).contiguous()
@@ -365,7 +366,8 @@ def mlp_measure(X, lab, n_steps, rank, dtype="f32"):
     lf = float(sum(max(0.0, t["L"] - 1) for t in s.trace))
     achieved = MLP_FLOP_PER_LEAPFROG * lf / (kms * 1e-3) / 1e12
     out = {"workload": "MNIST MLP 784-256-256-10 SGHMC, batch 500, 1 chain (BASELINE config 3)",
-           "dtype": dtype, "param_dim": MLP_P, "steps": n_steps, "leapfrogs": lf,
+           "dtype": dtype, "param_dim": MLP_P, "steps": n_steps, "leapfrogs": lf, "path_length": MLP_LAMBDA,
+           "mean_L": float(np.mean([t["L"] for t in s.trace])),
            "leapfrogs_per_s": lf / dt, "value": lf / dt * MLP_P, "unit": "leapfrog-steps/s x param-dim",
            "accept_rate": float(np.mean(res.accepted)),
            "roofline": {"bound": "mfma", "achieved": achieved, "peak": MFMA_PEAK_TFLOPS[dtype], "unit": "TFLOP/s",

@@ -990,7 +990,9 @@ template <typename T> struct RbFwdArgs {
   const int32_t* y;
   RbFwdProb<T> p[FR_MAXP];
   PendSet<T> pend;                       // pending updates: run by the extra plane blockIdx.y == np
+  unsigned long long* prof;              // HMCX_FWDR_PROF: FR_NPH s_memrealtime stamps per workgroup
 };
+constexpr int FR_NPH = 8;
 
 template <typename T, int MK>
 __global__ __launch_bounds__(FR_NW * 64) void k_fwdr(RbFwdArgs<T> a) {
@@ -1006,82 +1008,124 @@ __global__ __launch_bounds__(FR_NW * 64) void k_fwdr(RbFwdArgs<T> a) {
     run_pendset(a.pend, (int)blockIdx.x, (int)gridDim.x);
     return;
   }
-  const RbFwdProb<T>& P = a.p[blockIdx.y];
+  // this workgroup's problem, read through the kernel-argument segment pointer (address space 4) at a
+  // uniform offset: scalar loads of ITS fields only (a.p[blockIdx.y] on the by-value argument made the
+  // compiler load every problem's fields and select among them — 500+ spilled SGPRs)
+  typedef __attribute__((address_space(4))) const RbFwdArgs<T> KArgs;
+  KArgs* ka = (KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+  const int pb = (int)blockIdx.y;
+  struct {
+    const T *xw, *b1, *W2, *b2, *W3, *b3;
+    const uint32_t* keep; const T* vals; T scale; int mn;
+    T *ga2, *pb2, *pb3, *pw3; double* lpart;
+  } P = {ka->p[pb].xw, ka->p[pb].b1, ka->p[pb].W2, ka->p[pb].b2, ka->p[pb].W3, ka->p[pb].b3,
+         ka->p[pb].ms.keep, ka->p[pb].ms.vals, ka->p[pb].ms.scale, ka->p[pb].ms.mn,
+         ka->p[pb].ga2, ka->p[pb].pb2, ka->p[pb].pb3, ka->p[pb].pw3, ka->p[pb].lpart};
+  const MaskSrc<T> nomask{};
   const int rb = blockIdx.x, m0 = rb * FR_ROWS, nm = a.n_mid, No = a.n_out, M = a.M;
+  auto stamp = [&](int ph) {
+    if (a.prof && tid == 0) a.prof[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * FR_NPH + ph] = __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
+  static_assert(sizeof(T) == 4, "k_fwdr is the float32 kernel (fwdr_ok)");
   const int nwv = (nm + 31) / 32;                                  // waves with columns
   const int n0 = 32 * wave;
   const bool wact = wave < nwv;
-  constexpr int V = 16 / sizeof(T);
-  // labels of the cross-entropy rows, b3, and W3 into LDS: before anything waits on memory
-  const int32_t yv = a.y[min(m0 + (tid >> 4), M - 1)];
-  const T b3v = P.b3[min(tid & 15, No - 1)];
-  for (int e = tid; e < 16 * FR_NMAX; e += FR_NW * 64) {
-    const int o = e / FR_NMAX, n = e % FR_NMAX;
-    const bool ok = o < No && n < nm;
-    const T w = P.W3[ok ? (size_t)o * nm + n : 0];
-    w3s[o][n] = ok ? w : T(0);
-  }
-  // h1 = max((xw + b1)·m0, 0) of the 16 rows (rows past M: 0)
-  for (int e = tid; e < FR_ROWS * nm / V; e += FR_NW * 64) {
-    const int r = e / (nm / V), c = (e % (nm / V)) * V, m = m0 + r;
-    const bool ok = m < M;
-    const size_t base = ok ? (size_t)m * nm + c : 0;
-    T x[V], bb[V], mk[V];
-    if constexpr (V == 4) {
-      const float4 w = *reinterpret_cast<const float4*>(P.xw + base);
-      x[0] = w.x; x[1] = w.y; x[2] = w.z; x[3] = w.w;
-    } else {
-      const double2 w = *reinterpret_cast<const double2*>(P.xw + base);
-      x[0] = w.x; x[1] = w.y;
-    }
-#pragma unroll
-    for (int q = 0; q < V; ++q) bb[q] = P.b1[c + q];
-    mvals<T, V, MK>(P.ms, 0, base, mk);
-#pragma unroll
-    for (int q = 0; q < V; ++q) At[r][c + q] = ok ? op_apply<T, OP_H1>(x[q], mk[q], bb[q]) : T(0);
-  }
-  // epilogue operands of this lane's 8 elements (r = lr, n = n0 + 16j + row(q)): b2 and the m1 / m2 masks
   const int r = lr, m = m0 + r;
   const bool rok = m < M;
-  T b2v[2][4];
-  MRaw<T> m1r[2][4], m2r[2][4];
+  const int mn = P.mn;
+  // Every load of the prologue goes out before the first use (one memory round trip, not four):
+  // 1. the first three 16-k chunks of this wave's W2 rows — the operand the launch waits on longest
+  T bv[3][4][2];
+  auto load = [&](int s, int k0) {
+    load_chunk<T, OP_PLAIN, 0, 1, MK_NONE>(bv[s], P.W2, nm, n0, nm, k0, nm, lr, lg, nomask, nullptr);
+  };
+  load(0, 0);
+  if (16 < nm) load(1, 16);
+  if (32 < nm) load(2, 32);
+  // 2. h1's inputs, two 4-element pieces per thread of the 16 × n_mid tile: xw, b1, the m0 mask
+  constexpr int HP = FR_ROWS * FR_NMAX / 4 / (FR_NW * 64);
+  float4 hx[HP], hb[HP], hv4[HP];
+  uint32_t hk[HP];
+  size_t hbase[HP];
 #pragma unroll
-  for (int j = 0; j < 2; ++j)
+  for (int h = 0; h < HP; ++h) {
+    const int e = tid + h * FR_NW * 64, rr = e / (nm / 4), c = (e % (nm / 4)) * 4, mm = m0 + rr;
+    const bool ok = e < FR_ROWS * nm / 4 && mm < M;
+    const size_t base = ok ? (size_t)mm * nm + c : 0;
+    hbase[h] = base;
+    hx[h] = *reinterpret_cast<const float4*>(P.xw + base);
+    hb[h] = *reinterpret_cast<const float4*>(P.b1 + (ok ? c : 0));
+    if constexpr (MK == MK_KEEP) hk[h] = P.keep[base >> 5];
+    if constexpr (MK == MK_VALS) hv4[h] = *reinterpret_cast<const float4*>(P.vals + base);
+  }
+  // 3. W3, two 4-column pieces per thread (rows o ≥ n_out: zero)
+  float4 w3v[HP];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int n = n0 + 16 * j + Mf::row(lane, q);
-      const bool ok = rok && n < nm;
-      const size_t i = ok ? (size_t)m * nm + n : 0;
-      b2v[j][q] = P.b2[ok ? n : 0];
-      m1r[j][q] = mraw<T, MK>(P.ms, 1, i);
-      m2r[j][q] = mraw<T, MK>(P.ms, 2, i);
+  for (int h = 0; h < HP; ++h) {
+    const int e = tid + h * FR_NW * 64, o = e / (FR_NMAX / 4), c = (e % (FR_NMAX / 4)) * 4;
+    const bool ok = o < No && c < nm;
+    w3v[h] = *reinterpret_cast<const float4*>(P.W3 + (ok ? (size_t)o * nm + c : 0));
+  }
+  // 4. the epilogue's operands for this lane's 8 elements (r = lr, n = n0 + 16j + 4·lg + q): b2, the
+  //    m1 / m2 masks (one keep word or one 16-byte vector each); the labels and b3 of the cross-entropy
+  float4 b2v[2], m1v4[2], m2v4[2];
+  uint32_t k1[2], k2[2];
+  size_t ebase[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = n0 + 16 * j + 4 * lg;
+    const bool ok = rok && n < nm;
+    const size_t e = ok ? (size_t)m * nm + n : 0;
+    ebase[j] = e;
+    b2v[j] = *reinterpret_cast<const float4*>(P.b2 + (ok ? n : 0));
+    if constexpr (MK == MK_KEEP) {
+      k1[j] = P.keep[((size_t)mn + e) >> 5];
+      k2[j] = P.keep[((size_t)2 * mn + e) >> 5];
     }
+    if constexpr (MK == MK_VALS) {
+      m1v4[j] = *reinterpret_cast<const float4*>(P.vals + (size_t)mn + e);
+      m2v4[j] = *reinterpret_cast<const float4*>(P.vals + (size_t)2 * mn + e);
+    }
+  }
+  const int32_t yv = a.y[min(m0 + (tid >> 4), M - 1)];
+  const T b3v = P.b3[min(tid & 15, No - 1)];
+  // h1 = max((xw + b1)·m0, 0) (mlp.py:30) and W3 into LDS
+  auto mbit = [&](uint32_t w, size_t e, int q) { return ((w >> ((e & 31) + q)) & 1u) ? P.scale : T(0); };
+#pragma unroll
+  for (int h = 0; h < HP; ++h) {
+    const int e = tid + h * FR_NW * 64, rr = e / (nm / 4), c = (e % (nm / 4)) * 4;
+    if (e < FR_ROWS * nm / 4) {
+      const bool ok = m0 + rr < M;
+      const T x[4] = {hx[h].x, hx[h].y, hx[h].z, hx[h].w}, bb[4] = {hb[h].x, hb[h].y, hb[h].z, hb[h].w};
+      const T vv[4] = {hv4[h].x, hv4[h].y, hv4[h].z, hv4[h].w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        T mk = T(1);
+        if constexpr (MK == MK_KEEP) mk = mbit(hk[h], hbase[h], q);
+        if constexpr (MK == MK_VALS) mk = vv[q];
+        At[rr][c + q] = ok ? op_apply<T, OP_H1>(x[q], mk, bb[q]) : T(0);
+      }
+    }
+    const int o = e / (FR_NMAX / 4), c3 = (e % (FR_NMAX / 4)) * 4;
+    const bool ok3 = o < No && c3 < nm;
+    *reinterpret_cast<float4*>(&w3s[o][c3]) = ok3 ? w3v[h] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  stamp(1);
   __syncthreads();
-  // layer 2, transposed: acc[j] = h2ᵀ[n0 + 16j + row][r] over all of K = n_mid
+  stamp(2);
+  // layer 2, transposed: acc[j] = h2ᵀ[n0 + 16j + row][r] over all of K = n_mid; A = W2 rows (the ring),
+  // B = h1ᵀ from LDS (16-byte reads)
   typename Mf::acc_t acc[2] = {Mf::zero(), Mf::zero()};
   if (wact) {
-    T bv[3][4][2];
-    auto load = [&](int s, int k0) {
-      load_chunk<T, OP_PLAIN, 0, 1, MK_NONE>(bv[s], P.W2, nm, n0, nm, k0, nm, lr, lg, P.ms, nullptr);
-    };
     auto mf = [&](int s, int k0) {
-      T hv[4];                                                     // h1[lr][k0 + kmap(u, lg)]: 16-byte LDS reads
-      if constexpr (sizeof(T) == 4) {
-        const float4 w = *reinterpret_cast<const float4*>(&At[lr][k0 + 4 * lg]);
-        hv[0] = w.x; hv[1] = w.y; hv[2] = w.z; hv[3] = w.w;
-      } else {
-        const double2 w0 = *reinterpret_cast<const double2*>(&At[lr][k0 + 2 * lg]);
-        const double2 w1 = *reinterpret_cast<const double2*>(&At[lr][k0 + 8 + 2 * lg]);
-        hv[0] = w0.x; hv[1] = w0.y; hv[2] = w1.x; hv[3] = w1.y;
-      }
+      const float4 w = *reinterpret_cast<const float4*>(&At[lr][k0 + 4 * lg]);
+      const T hv[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
       for (int u = 0; u < 4; ++u)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[j] = Mf::fma(bv[s][u][j], hv[u], acc[j]);
     };
-    load(0, 0);
-    if (16 < nm) load(1, 16);
-    if (32 < nm) load(2, 32);
     for (int k0 = 0; k0 < nm; k0 += 48) {
       mf(0, k0);
       if (k0 + 48 < nm) load(0, k0 + 48);
@@ -1095,24 +1139,34 @@ __global__ __launch_bounds__(FR_NW * 64) void k_fwdr(RbFwdArgs<T> a) {
       }
     }
   }
+  stamp(3);
   // h2 = max((z2 + b2)·m1, 0), d3 = h2·m2 (mlp.py:30-31), kept in registers
   T dv[2][4], hp[2][4], m1v[2][4], m2v[2][4];
 #pragma unroll
-  for (int j = 0; j < 2; ++j)
+  for (int j = 0; j < 2; ++j) {
+    const T b2q[4] = {b2v[j].x, b2v[j].y, b2v[j].z, b2v[j].w};
+    const T v1[4] = {m1v4[j].x, m1v4[j].y, m1v4[j].z, m1v4[j].w}, v2[4] = {m2v4[j].x, m2v4[j].y, m2v4[j].z, m2v4[j].w};
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      mpin<T, MK>(m1r[j][q]);
-      mpin<T, MK>(m2r[j][q]);
       const int n = n0 + 16 * j + Mf::row(lane, q);
       const bool ok = rok && n < nm;
-      m1v[j][q] = mfin<T, MK>(P.ms, m1r[j][q]);
-      m2v[j][q] = mfin<T, MK>(P.ms, m2r[j][q]);
-      const T t = (acc[j][q] + b2v[j][q]) * m1v[j][q];
+      m1v[j][q] = m2v[j][q] = T(1);
+      if constexpr (MK == MK_KEEP) {
+        m1v[j][q] = mbit(k1[j], (size_t)mn + ebase[j], q);
+        m2v[j][q] = mbit(k2[j], (size_t)2 * mn + ebase[j], q);
+      }
+      if constexpr (MK == MK_VALS) {
+        m1v[j][q] = v1[q];
+        m2v[j][q] = v2[q];
+      }
+      const T t = (acc[j][q] + b2q[q]) * m1v[j][q];
       const T h = t > T(0) ? t : T(0);
       hp[j][q] = h > T(0) ? T(1) : T(0);
       dv[j][q] = ok ? h * m2v[j][q] : T(0);
     }
+  }
   __syncthreads();                                                 // every wave is done with the h1 tile
+  stamp(4);
   // layer 3: zᵀ[o][r] = Σ_n W3[o][n]·d3[r][n] over this wave's columns (k index n = n0 + 16j + row(u))
   {
     typename Mf::acc_t za = Mf::zero();
@@ -1128,6 +1182,7 @@ __global__ __launch_bounds__(FR_NW * 64) void k_fwdr(RbFwdArgs<T> a) {
     for (int q = 0; q < 4; ++q) zr[wave][Mf::row(lane, q)][lr] = za[q];
   }
   __syncthreads();
+  stamp(5);
   // cross-entropy of the block's rows, 16 lanes per row (F.softmax_cross_entropy, mean over M)
   if (tid < 256) {
     const int rr = tid >> 4, k = tid & 15, mm = m0 + rr;
@@ -1158,6 +1213,7 @@ __global__ __launch_bounds__(FR_NW * 64) void k_fwdr(RbFwdArgs<T> a) {
     if (k == 0) rowl[rr] = l;
   }
   __syncthreads();
+  stamp(6);
   if (tid == 0 && P.lpart) {
     double s = 0.0;
     for (int q = 0; q < FR_ROWS; ++q) s += rowl[q];
@@ -1232,6 +1288,7 @@ __global__ __launch_bounds__(FR_NW * 64) void k_fwdr(RbFwdArgs<T> a) {
       }
     }
   }
+  stamp(7);
 }
 
 // Keep flags of forward f, one bit per element (bit e % 32 of word e / 32; forward f's words start at
@@ -1452,6 +1509,9 @@ struct MlpNet {
   T* h1 = nullptr; bool h1_valid = false;   // h1 of the last fused forward (when its sub-step needs it)
   T *pb1, *pb2, *pb3, *pw3;              // gradient partials of b1, b2, b3, W3 ([nlb][...])
   T *fpb2 = nullptr, *fpb3 = nullptr, *fpw3 = nullptr;   // the same partials per 16-row block (k_fwdr, [nrb][...])
+  unsigned long long* fr_prof = nullptr;  // HMCX_FWDR_PROF: stamps of the call's k_fwdr launches
+  int fr_prof_cap = 0, fr_prof_n = 0;
+  std::vector<int> fr_prof_np;
   int nrb = 0;                           // 16-row blocks: ⌈B/16⌉
   hipStream_t st;
   bool xw_valid = false;
@@ -1881,6 +1941,8 @@ bool fwdr_ok(const MlpNet<T>& net, const SubStep<T>* ss, int n) {
     const T* xw = ss[i].xw ? ss[i].xw : net.xw;
     if (!vec_ok(xw, net.n_mid, sizeof(T)) || !vec_ok(ss[i].q[2], net.n_mid, sizeof(T)) || mask_kind(ss[i].ms) != mk)
       return false;
+    if (!vec_ok(ss[i].q[1], 4, 4) || !vec_ok(ss[i].q[3], 4, 4) || !vec_ok(ss[i].q[4], net.n_mid, sizeof(T))) return false;
+    if (mk == MK_VALS && !vec_ok(ss[i].ms.vals, 4, 4)) return false;
   }
   return true;
 }
@@ -1893,6 +1955,10 @@ template <typename T>
 hipError_t mlp_fwdr(MlpNet<T>& net, const SubStep<T>* const* ss, int np) {
   if (np < 1 || np > FR_MAXP) return hipErrorInvalidValue;
   RbFwdArgs<T> a{};
+  if (net.fr_prof && net.fr_prof_n < net.fr_prof_cap) {          // HMCX_FWDR_PROF: this launch's stamps
+    a.prof = net.fr_prof + (size_t)net.fr_prof_n * net.nrb * FR_MAXP * FR_NPH;
+    net.fr_prof_np[net.fr_prof_n++] = np;
+  }
   a.M = net.B; a.n_mid = net.n_mid; a.n_out = net.n_out; a.np = np; a.y = net.y;
   for (int p = 0; p < np; ++p) {
     const SubStep<T>& x = *ss[p];
@@ -2288,6 +2354,7 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
   const int kw = (n3 + 31) / 32;                              // words per forward
   int32_t* accf;
   static const char* prof_path = getenv("HMCX_MLP_PROF");
+  static const char* fr_prof_path = getenv("HMCX_FWDR_PROF");
   const int prof_cap = prof_path && net.fuse ? 8192 : 0;
   do {
     ws.reset();
@@ -2303,6 +2370,9 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
     net.fpb2 = batch ? pn[0].fpb2 : nullptr;                       // marks the buffers as present (fwdr_ok)
     net.prof = prof_cap ? ws.take<unsigned long long>((size_t)prof_cap * net.nlb * ((net.n_mid + 31) / 32) * L23_NPH)
                         : nullptr;
+    net.fr_prof_cap = fr_prof_path ? 512 : 0;
+    net.fr_prof_np.assign(net.fr_prof_cap, 0);
+    net.fr_prof = fr_prof_path ? ws.take<unsigned long long>((size_t)512 * net.nrb * FR_MAXP * FR_NPH) : nullptr;
     net.prof_cap = prof_cap;
     for (int v = 0; v < 6; ++v) {
       pv[v] = ws.take<T>(dim[v]); qa[v] = ws.take<T>(dim[v]); qb[v] = ws.take<T>(dim[v]);
@@ -2589,6 +2659,20 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
   }
   if ((rc = gs.finish())) return rc;
   if ((rc = timing_end(ctx, ctx->stream))) return rc;
+  if (net.fr_prof && net.fr_prof_n) {                        // HMCX_FWDR_PROF=<file>: append per launch
+    HMCX_HIP(ctx, hipStreamSynchronize(st));                  // {np, nrb, FR_NPH} + stamps [np][nrb][FR_NPH]
+    const size_t per = (size_t)net.nrb * FR_MAXP * FR_NPH;
+    std::vector<unsigned long long> h(per * net.fr_prof_n);
+    HMCX_HIP(ctx, hipMemcpy(h.data(), net.fr_prof, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    if (FILE* f = fopen(fr_prof_path, "ab")) {
+      for (int l = 0; l < net.fr_prof_n; ++l) {
+        const int hdr[3] = {net.fr_prof_np[l], net.nrb, FR_NPH};
+        fwrite(hdr, sizeof(int), 3, f);
+        fwrite(h.data() + l * per, sizeof(unsigned long long), (size_t)net.fr_prof_np[l] * net.nrb * FR_NPH, f);
+      }
+      fclose(f);
+    }
+  }
   if (net.prof) {                                            // HMCX_MLP_PROF=<file>: append the stamps
     HMCX_HIP(ctx, hipStreamSynchronize(st));
     const size_t n = (size_t)std::min(net.l23_count, net.prof_cap) * net.nlb * ((net.n_mid + 31) / 32) * L23_NPH;

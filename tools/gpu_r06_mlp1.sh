@@ -14,3 +14,6 @@ timeout -k 10 180 rocprofv3 --kernel-trace --output-format csv -d $O/trace -o ru
 f=$(find $O/trace -name '*kernel_trace.csv' | head -1)
 python tools/kernel_timeline.py $f hmcx 150 30 > $O/timeline.txt 2>&1
 tail -14 $O/timeline.txt
+rm -f $O/fwdr.prof
+HMCX_FWDR_PROF=$O/fwdr.prof timeout -k 10 120 python tools/probe_mlp.py 12 lam=2e-2 > $O/probe_prof.txt 2>&1 || exit 1
+python tools/fwdr_prof_summary.py $O/fwdr.prof | tee $O/stamps.txt
