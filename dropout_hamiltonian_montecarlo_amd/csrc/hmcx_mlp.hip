@@ -161,6 +161,14 @@ __device__ inline void run_pending(const Pending<T>& pd, int bid, int nb) {
     // all loads of a batch go out before the (in-order) sum: one memory round trip per 16
     // partials instead of one per partial
     T s = T(0);
+    if (pd.nparts == 4) {                                      // a split-K weight gradient (W2): 4 partials
+      T v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = pd.part[(size_t)q * pd.n + i];
+      s = ((v[0] + v[1]) + v[2]) + v[3];
+      apply_upd(pd.u, pd.mode, i, s);
+      continue;
+    }
     for (int b0 = 0; b0 < pd.nparts; b0 += PB) {
       T v[PB];
 #pragma unroll
@@ -254,7 +262,7 @@ template <typename T, int NP> struct MMProbsN {
   int n;                             // 0: a plain launch
 };
 template <typename T> using MMProbs = MMProbsN<T, MAXPROB>;
-template <typename T> using MMProbs3 = MMProbsN<T, 3>;   // the sub-grids of a dual launch
+template <typename T> using MMProbs3 = MMProbsN<T, 4>;   // the sub-grids of a dual launch (up to 4 problems)
 
 template <typename T, int OP>
 __device__ inline T op_apply(T x, T mask, T bias) {
@@ -980,7 +988,9 @@ constexpr int FR_NW = 8;                 // waves per workgroup: n_mid ≤ 32·F
 constexpr int FR_NMAX = 32 * FR_NW;
 constexpr int FR_MAXP = 8;               // problems per launch: six sub-steps + E_new + E_current
 template <typename T> struct RbFwdProb {
-  const T* xw; const T* b1; const T* W2; const T* b2; const T* W3; const T* b3;
+  const T* xw; const T* xw2;             // layer 1 as split-K planes: xw + xw2 (xw2 null: one plane)
+  T* xwout;                              // the summed xw of the block's rows is stored here (null: not)
+  const T* b1; const T* W2; const T* b2; const T* W3; const T* b3;
   MaskSrc<T> ms;
   T* ga2; T* pb2; T* pb3; T* pw3;        // outputs, null when not wanted; partials [⌈B/16⌉][…]
   double* lpart;                         // loss partial of each 16-row block (null: none)
@@ -1015,10 +1025,10 @@ __global__ __launch_bounds__(FR_NW * 64) void k_fwdr(RbFwdArgs<T> a) {
   KArgs* ka = (KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
   const int pb = (int)blockIdx.y;
   struct {
-    const T *xw, *b1, *W2, *b2, *W3, *b3;
+    const T *xw, *xw2; T* xwout; const T *b1, *W2, *b2, *W3, *b3;
     const uint32_t* keep; const T* vals; T scale; int mn;
     T *ga2, *pb2, *pb3, *pw3; double* lpart;
-  } P = {ka->p[pb].xw, ka->p[pb].b1, ka->p[pb].W2, ka->p[pb].b2, ka->p[pb].W3, ka->p[pb].b3,
+  } P = {ka->p[pb].xw, ka->p[pb].xw2, ka->p[pb].xwout, ka->p[pb].b1, ka->p[pb].W2, ka->p[pb].b2, ka->p[pb].W3, ka->p[pb].b3,
          ka->p[pb].ms.keep, ka->p[pb].ms.vals, ka->p[pb].ms.scale, ka->p[pb].ms.mn,
          ka->p[pb].ga2, ka->p[pb].pb2, ka->p[pb].pb3, ka->p[pb].pw3, ka->p[pb].lpart};
   const MaskSrc<T> nomask{};
@@ -1045,7 +1055,7 @@ __global__ __launch_bounds__(FR_NW * 64) void k_fwdr(RbFwdArgs<T> a) {
   if (32 < nm) load(2, 32);
   // 2. h1's inputs, two 4-element pieces per thread of the 16 × n_mid tile: xw, b1, the m0 mask
   constexpr int HP = FR_ROWS * FR_NMAX / 4 / (FR_NW * 64);
-  float4 hx[HP], hb[HP], hv4[HP];
+  float4 hx[HP], hx2[HP], hb[HP], hv4[HP];
   uint32_t hk[HP];
   size_t hbase[HP];
 #pragma unroll
@@ -1055,6 +1065,7 @@ __global__ __launch_bounds__(FR_NW * 64) void k_fwdr(RbFwdArgs<T> a) {
     const size_t base = ok ? (size_t)mm * nm + c : 0;
     hbase[h] = base;
     hx[h] = *reinterpret_cast<const float4*>(P.xw + base);
+    hx2[h] = *reinterpret_cast<const float4*>((P.xw2 ? P.xw2 : P.xw) + base);
     hb[h] = *reinterpret_cast<const float4*>(P.b1 + (ok ? c : 0));
     if constexpr (MK == MK_KEEP) hk[h] = P.keep[base >> 5];
     if constexpr (MK == MK_VALS) hv4[h] = *reinterpret_cast<const float4*>(P.vals + base);
@@ -1097,6 +1108,10 @@ __global__ __launch_bounds__(FR_NW * 64) void k_fwdr(RbFwdArgs<T> a) {
     const int e = tid + h * FR_NW * 64, rr = e / (nm / 4), c = (e % (nm / 4)) * 4;
     if (e < FR_ROWS * nm / 4) {
       const bool ok = m0 + rr < M;
+      if (P.xw2) {                                             // the two split-K planes, in plane order
+        hx[h].x += hx2[h].x; hx[h].y += hx2[h].y; hx[h].z += hx2[h].z; hx[h].w += hx2[h].w;
+        if (P.xwout && ok) *reinterpret_cast<float4*>(P.xwout + hbase[h]) = hx[h];
+      }
       const T x[4] = {hx[h].x, hx[h].y, hx[h].z, hx[h].w}, bb[4] = {hb[h].x, hb[h].y, hb[h].z, hb[h].w};
       const T vv[4] = {hv4[h].x, hv4[h].y, hv4[h].z, hv4[h].w};
 #pragma unroll
@@ -1753,6 +1768,8 @@ hipError_t mlp_layer1_batch(MlpNet<T>& net, const T* const* W1, T* const* out, i
 // gradient partials), loss partials and what its layer-3 backward must produce.
 template <typename T> struct SubStep {
   const T* xw;                       // layer-1 output of its W1 (null: net's)
+  const T* xw2 = nullptr;            // k_fwdr: the second split-K plane of layer 1 (xw = xw + xw2)
+  T* xwout = nullptr;                // k_fwdr: store the summed xw here
   T* q[6];
   MaskSrc<T> ms;
   MlpNet<T>* scr;
@@ -1935,6 +1952,9 @@ bool fwdr_ok(const MlpNet<T>& net, const SubStep<T>* ss, int n) {
   const char* env = getenv("HMCX_MLP_FWDR");
   if ((env && env[0] == '0') || sizeof(T) != 4) return false;
   if (net.n_mid % 32 || net.n_mid > FR_NMAX || net.n_out > 16 || !net.vec_masks || !net.fpb2) return false;
+  // layer 1 in two 16-byte-aligned split-K halves; the W2 gradient in 4 row quarters whose m0 masks start
+  // on a keep word
+  if (net.n_in % 8 || net.B % 4 || ((size_t)(net.B / 4) * net.n_mid) % 32) return false;
   const int mk = mask_kind(ss[0].ms);
   if (mk != MK_KEEP && mk != MK_VALS) return false;
   for (int i = 0; i < n; ++i) {
@@ -1964,6 +1984,8 @@ hipError_t mlp_fwdr(MlpNet<T>& net, const SubStep<T>* const* ss, int np) {
     const SubStep<T>& x = *ss[p];
     RbFwdProb<T>& q = a.p[p];
     q.xw = x.xw ? x.xw : net.xw;
+    q.xw2 = x.xw2;
+    q.xwout = x.xwout;
     q.b1 = x.q[1]; q.W2 = x.q[2]; q.b2 = x.q[3]; q.W3 = x.q[4]; q.b3 = x.q[5];
     q.ms = x.ms;
     q.ga2 = (x.v >= 0 && x.v <= 2) ? x.scr->ga2 : nullptr;
@@ -1978,6 +2000,68 @@ hipError_t mlp_fwdr(MlpNet<T>& net, const SubStep<T>* const* ss, int np) {
   if constexpr (sizeof(T) == 4) {                              // float32 only (fwdr_ok)
     if (mask_kind(a.p[0].ms) == MK_KEEP) hipLaunchKernelGGL((k_fwdr<T, MK_KEEP>), grid, dim3(FR_NW * 64), 0, net.st, a);
     else hipLaunchKernelGGL((k_fwdr<T, MK_VALS>), grid, dim3(FR_NW * 64), 0, net.st, a);
+    return hipGetLastError();
+  }
+  return hipErrorInvalidValue;
+}
+
+// Layer 1 as two split-K planes (k_fwdr sums them, plane 0 + plane 1): out[w][h] = X[:, K_h]·W1_w[:, K_h]ᵀ
+// over the h-th half of n_in, for nw W1s in one batched launch — twice the workgroups of the plain
+// layer 1 (config 3: 256 instead of 128, each half the 784-deep dot products); net's pending updates run
+// in the extra plane.  Needs n_in % 8 == 0 (16-byte vectors in both halves).
+template <typename T>
+hipError_t mlp_layer1_split(MlpNet<T>& net, const T* const* W1, T* const (*out)[2], int nw) {
+  const int Kh = net.n_in / 2;
+  MMArgs<T> a{};
+  MMProbs<T> pr{};
+  pr.n = 2 * nw;
+  for (int w = 0; w < nw; ++w)
+    for (int h = 0; h < 2; ++h) {
+      MMProb<T>& q = pr.p[2 * w + h];
+      q.A = net.X + (size_t)h * Kh; q.B = W1[w] + (size_t)h * Kh; q.C = out[w][h];
+    }
+  mm_set<T>(a, net.B, net.n_mid, Kh, pr.p[0].A, net.n_in, 0, pr.p[0].B, net.n_in, 1, pr.p[0].C, net.n_mid);
+  return mm<T, MM_STORE, 0, 1, OP_PLAIN, OP_PLAIN, true>(net, a, &pr);
+}
+
+// The W1 gradient (SGHMC epilogue; pn's pending bias / W3 updates in its extra plane) and the W2 gradient
+// of sub-step net `w2n` as 4 split-K partial planes wp[4][n_mid][n_mid] over the minibatch rows, in ONE
+// launch (k_mm2b): the W2 update itself runs as a pending update (4 partials, summed in plane order) in
+// the NEXT launch.  200 + 256 workgroups at config 3 instead of 200 and a separate 64-workgroup W2 launch.
+template <typename T>
+hipError_t mlp_w1_w2split(MlpNet<T>& pn0, const SubStep<T>& s1, const Upd<T>& u1, MlpNet<T>& w2n, const SubStep<T>& s2,
+                          T* wp) {
+  MMArgs<T> a1, a2;
+  MMProbs3<T> p1{}, p2{};
+  wgrad_build(pn0, s1, 0, u1, a1);
+  a1.pend = pn0.pend;
+  pn0.pend.n = 0;
+  wgrad_build(w2n, s2, 2, Upd<T>{}, a2);
+  a2.upd_mode = UPD_NONE;
+  a2.pend.n = 0;
+  const int nm = w2n.n_mid, Kq = w2n.B / 4;
+  a2.K = Kq;
+  p2.n = 4;
+  for (int q = 0; q < 4; ++q) {
+    MMProb<T>& x = p2.p[q];
+    const size_t r0 = (size_t)q * Kq * nm;                       // rows q·Kq … of ga2 and xw (and the m0 mask)
+    x.A = a2.A + r0; x.B = a2.B + r0; x.C = wp + (size_t)q * nm * nm; x.b1 = a2.b1;
+    x.ms = a2.ms;
+    if (x.ms.keep) x.ms.keep += r0 / 32;
+    if (x.ms.vals) x.ms.vals += r0;
+  }
+  a2.C = p2.p[0].C; a2.ldc = nm;
+  const int3 g1 = make_int3((a1.M + 31) / 32, (a1.N + 31) / 32, 1 + (a1.pend.n > 0 ? 1 : 0));
+  const int3 g2 = make_int3((nm + 31) / 32, (nm + 31) / 32, 4);
+  const dim3 grid((unsigned)std::max(g1.x, g2.x), (unsigned)std::max(g1.y, g2.y), (unsigned)(g1.z + g2.z));
+  if constexpr (sizeof(T) == 4) {                              // float32 only (the k_fwdr path)
+    auto go = [&](auto mkc) {
+      constexpr int MK = decltype(mkc)::value;                 // the W1 gradient reads no masks
+      hipLaunchKernelGGL((k_mm2b<T, MM_UPD, OP_PLAIN, OP_PLAIN, 1, 0, 0, 0, MM_STORE, OP_PLAIN, OP_H1, 1, 0, 0, 0, MK>),
+                         grid, dim3(MM_NT), 0, pn0.st, a1, p1, a2, p2, g1, g2);
+    };
+    if (mask_kind(a2.ms) == MK_KEEP) go(std::integral_constant<int, MK_KEEP>{});
+    else go(std::integral_constant<int, MK_VALS>{});
     return hipGetLastError();
   }
   return hipErrorInvalidValue;
@@ -2077,7 +2161,7 @@ template <typename T>
 void set_pending_part(MlpNet<T>& net, int v, int mode, const Upd<T>& u, const T* part, int nparts) {
   Pending<T>& p = net.pend.p[net.pend.n++];
   p.mode = mode; p.u = u; p.nparts = nparts; p.part = part;
-  p.n = v == 4 ? net.n_out * net.n_mid : (v == 5 ? net.n_out : net.n_mid);
+  p.n = net.nvar(v);
 }
 
 template <typename T>
@@ -2349,6 +2433,7 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
   }
   Workspace ws(ctx);
   T *pv[6], *qa[6], *qb[6], *qc[6], *xw_par = nullptr, *xw_b1 = nullptr;
+  T *xwp[2] = {}, *xpar[2] = {}, *w2part = nullptr;           // k_fwdr path: layer-1 split-K planes, W2 partials
   double *part_cur, *part_new, *lp_cur, *lp_new, *lp_scr;
   uint32_t* keep = nullptr;                                  // keep flags of the step: one bit per element
   const int kw = (n3 + 31) / 32;                              // words per forward
@@ -2381,6 +2466,8 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
     if (batch) {
       xw_par = ws.take<T>((size_t)mn);
       xw_b1 = ws.take<T>((size_t)mn);
+      for (int h = 0; h < 2; ++h) { xwp[h] = ws.take<T>((size_t)mn); xpar[h] = ws.take<T>((size_t)mn); }
+      w2part = ws.take<T>((size_t)4 * s->n_mid * s->n_mid);
       for (auto& e : en) e.gz = ws.take<T>((size_t)s->B * s->n_out);
     }
     part_cur = ws.take<double>(12 * NPART);
@@ -2486,20 +2573,13 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
         x.w = L3Want{false, false, false, false, false};
         x.v = -1;
       }
+      bool use_fr = false;                                     // the k_fwdr path (decided in iteration 0)
       for (int it = 0; it < n; ++it) {
         T* const* Xit = q3[it % 3];                              // positions of iteration it
         T* const* Xpr = it == 0 ? par : q3[(it + 2) % 3];        // of iteration it − 1
         T* const* Xnx = q3[(it + 1) % 3];                        // the next iteration's (written here)
         net.xw = xwb[it & 1];
         for (int i = 0; i < 6; ++i) pn[i].xw = net.xw;
-        if (it == 0) {                                           // xw(0) and the start state's xw (E_current)
-          const T* w1[2] = {qa[0], par[0]};
-          T* out[2] = {net.xw, xw_par};
-          HMCX_HIP(ctx, mlp_layer1_batch<T>(net, w1, out, 2));
-        } else if (!l1_done) {
-          HMCX_HIP(ctx, mlp_layer1<T>(net, Xit[0]));
-        }
-        l1_done = false;
         SubStep<T> ss[6];
         const SubStep<T>* ga[6];
         int nga = 0;
@@ -2517,39 +2597,76 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
         }
         int i2 = 0;                                              // position of the W2 sub-step
         while (s->order[i2] != 2) ++i2;
-        {
-          // 4 launches: every forward of the iteration and the energy forwards due, in ONE k_fwdr launch
-          // | the W1 / b1 layer-1 backwards | the W1 gradient + every pending update | the next
-          // iteration's layer 1 beside this iteration's W2 gradient
-          const SubStep<T>* fa[FR_MAXP];
-          SubStep<T> chk[FR_MAXP];
-          int na = 0;
-          for (int i = 0; i < 6; ++i) fa[na++] = &ss[i];
-          if (it == n - 1) fa[na++] = &es[0];
-          if (it == 0) fa[na++] = &es[1];
-          for (int q = 0; q < na; ++q) chk[q] = *fa[q];
-          if (fwdr_ok(net, chk, na)) {
-            if (it == n - 1) e_done[0] = e_fr[0] = true;
-            if (it == 0) e_done[1] = e_fr[1] = true;
-            HMCX_HIP(ctx, mlp_fwdr<T>(net, fa, na));
-            HMCX_HIP(ctx, mlp_ga1_batch<T>(net, ga, nga));
-            for (int i = 0; i < 6; ++i) {
-              const int v = s->order[i];
-              if (v == 0 || v == 2) continue;
-              const Upd<T> u = upd_for(it, v, Xit[v], it + 1 < n ? Xnx[v] : nullptr);
-              if (v == 1) set_pending(pn[0], v, UPD_SGHMC, u, &pn[i]);   // b1: the layer-1 backward's 32-row partials
-              else set_pending_part(pn[0], v, UPD_SGHMC, u, v == 3 ? pn[i].fpb2 : v == 4 ? pn[i].fpw3 : pn[i].fpb3,
-                                    net.nrb);
-            }
-            HMCX_HIP(ctx, mlp_wgrad<T>(pn[0], ss[0].q, ss[0].ms, 0, UPD_SGHMC,
-                                       upd_for(it, 0, Xit[0], it + 1 < n ? Xnx[0] : nullptr)));
-            const Upd<T> u2 = upd_for(it, 2, Xit[2], it + 1 < n ? Xnx[2] : nullptr);
-            if (it + 1 < n) HMCX_HIP(ctx, mlp_l1_w2<T>(net, Xnx[0], xwb[(it + 1) & 1], pn[i2], ss[i2], u2, &l1_done));
-            if (!l1_done) HMCX_HIP(ctx, mlp_wgrad<T>(pn[i2], ss[i2].q, ss[i2].ms, 2, UPD_SGHMC, u2));
-            fwd += 6;
-            continue;
-          }
+        if (it == 0) {
+          SubStep<T> chk[8];
+          for (int i = 0; i < 6; ++i) chk[i] = ss[i];
+          chk[6] = es[0];
+          chk[7] = es[1];
+          use_fr = fwdr_ok(net, chk, 8);
         }
+        if (use_fr) {
+          // 4 launches per iteration, the layer-1 GEMM and the W2 gradient as split-K partials:
+          //  A  k_fwdr: every forward of the iteration (and the energy forwards due) — h1 from the two
+          //     layer-1 planes, whose sum problem 0 stores as the iteration's xw;
+          //  B  the W1 / b1 layer-1 backwards;
+          //  C  the W1 gradient (SGHMC epilogue) + the W2 gradient as 4 row-quarter partials, the pending
+          //     bias / W3 updates in the extra plane;
+          //  D  the next iteration's layer 1 (two split-K planes) with the W2 update from its 4 partials in
+          //     the extra plane (after the last iteration: flushed before the kinetic energies).
+          if (it == 0) {                                          // layer 1 of iteration 0 and of the start state
+            const T* w1[2] = {qa[0], par[0]};
+            T* const out[2][2] = {{xwp[0], xwp[1]}, {xpar[0], xpar[1]}};
+            HMCX_HIP(ctx, mlp_layer1_split<T>(net, w1, out, 2));
+          }
+          const SubStep<T>* fa[FR_MAXP];
+          int na = 0;
+          for (int i = 0; i < 6; ++i) {
+            ss[i].xw = xwp[0];
+            ss[i].xw2 = xwp[1];
+            fa[na++] = &ss[i];
+          }
+          ss[0].xwout = net.xw;
+          if (it == n - 1) {
+            es[0].xw = xwp[0];
+            es[0].xw2 = xwp[1];
+            fa[na++] = &es[0];
+            e_done[0] = e_fr[0] = true;
+          }
+          if (it == 0) {
+            es[1].xw = xpar[0];
+            es[1].xw2 = xpar[1];
+            fa[na++] = &es[1];
+            e_done[1] = e_fr[1] = true;
+          }
+          HMCX_HIP(ctx, mlp_fwdr<T>(net, fa, na));
+          HMCX_HIP(ctx, mlp_ga1_batch<T>(net, ga, nga));
+          for (int i = 0; i < 6; ++i) {
+            const int v = s->order[i];
+            if (v == 0 || v == 2) continue;
+            const Upd<T> u = upd_for(it, v, Xit[v], it + 1 < n ? Xnx[v] : nullptr);
+            if (v == 1) set_pending(pn[0], v, UPD_SGHMC, u, &pn[i]);   // b1: the layer-1 backward's 32-row partials
+            else set_pending_part(pn[0], v, UPD_SGHMC, u, v == 3 ? pn[i].fpb2 : v == 4 ? pn[i].fpw3 : pn[i].fpb3,
+                                  net.nrb);
+          }
+          HMCX_HIP(ctx, mlp_w1_w2split<T>(pn[0], ss[0], upd_for(it, 0, Xit[0], it + 1 < n ? Xnx[0] : nullptr),
+                                          pn[i2], ss[i2], w2part));
+          set_pending_part(net, 2, UPD_SGHMC, upd_for(it, 2, Xit[2], it + 1 < n ? Xnx[2] : nullptr), w2part, 4);
+          if (it + 1 < n) {
+            const T* w1[1] = {Xnx[0]};
+            T* const out[1][2] = {{xwp[0], xwp[1]}};
+            HMCX_HIP(ctx, mlp_layer1_split<T>(net, w1, out, 1));
+          }
+          fwd += 6;
+          continue;
+        }
+        if (it == 0) {                                           // xw(0) and the start state's xw (E_current)
+          const T* w1[2] = {qa[0], par[0]};
+          T* out[2] = {net.xw, xw_par};
+          HMCX_HIP(ctx, mlp_layer1_batch<T>(net, w1, out, 2));
+        } else if (!l1_done) {
+          HMCX_HIP(ctx, mlp_layer1<T>(net, Xit[0]));
+        }
+        l1_done = false;
         if (quad_ok(net, ss)) {
           // 4 launches: forwards of W1, b1, W2 (+ one more) | the other two forwards + the W1 / b1
           // layer-1 backwards | the W1 and W2 gradients + every pending update | layer 1
