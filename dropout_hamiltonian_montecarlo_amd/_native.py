@@ -105,7 +105,7 @@ EXPORTS = ("hmcx_version", "hmcx_create", "hmcx_destroy", "hmcx_last_error", "hm
            "hmcx_sgld_run", "hmcx_hmc_mvn_run", "hmcx_mlp_masks", "hmcx_mlp_grad", "hmcx_mlp_loss",
            "hmcx_mlp_sghmc_run", "hmcx_mlp_hmc_leapfrog", "hmcx_logistic_grad", "hmcx_logistic_loglik", "hmcx_logistic_predict",
            "hmcx_sumsq", "hmcx_sgd_run", "hmcx_hmc_run", "hmcx_axpy", "hmcx_mvn_eval",
-           "hmcx_clear_abort", "hmcx_get_recoveries", "hmcx_note_recovery", "hmcx_philox_schedule", "hmcx_host_wait", "hmcx_set_mlp_fuse",
+           "hmcx_clear_abort", "hmcx_get_recoveries", "hmcx_note_recovery", "hmcx_set_sgld_fuse", "hmcx_philox_schedule", "hmcx_host_wait", "hmcx_set_mlp_fuse",
            "hmcx_comm_unique_id", "hmcx_comm_init", "hmcx_comm_destroy", "hmcx_allgather_chain_stats",
            "hmcx_allreduce_f64", "hmcx_chain_diagnostics")
 
@@ -174,6 +174,8 @@ def load_library():
             lib.hmcx_mlp_hmc_leapfrog.argtypes = [c_void_p, ctypes.POINTER(MlpLeapfrogArgs)]
         if hasattr(lib, "hmcx_set_mlp_fuse"):          # absent in older builds loaded for A/B runs
             lib.hmcx_set_mlp_fuse.argtypes = [c_void_p, c_int]
+        if hasattr(lib, "hmcx_set_sgld_fuse"):
+            lib.hmcx_set_sgld_fuse.argtypes = [c_void_p, c_int]
         if hasattr(lib, "hmcx_comm_init"):
             lib.hmcx_comm_unique_id.argtypes = [c_void_p]
             lib.hmcx_comm_init.argtypes = [c_void_p, c_int, c_int, c_void_p, ctypes.POINTER(c_void_p)]
@@ -260,6 +262,10 @@ class Context:
         self.check(self.lib.hmcx_note_recovery(self.h, self.RECOVERY_KINDS.index(kind)), "hmcx_note_recovery")
 
     mlp_fuse = True
+
+    def set_sgld_fuse(self, on):
+        """Fused forward + softmax of the wide SGLD path (include/hmcx.h hmcx_set_sgld_fuse)."""
+        self.check(self.lib.hmcx_set_sgld_fuse(self.h, 1 if on else 0), "hmcx_set_sgld_fuse")
 
     def set_mlp_fuse(self, on):
         """Fused layer-2/3 MLP launches in the sampler (include/hmcx.h hmcx_set_mlp_fuse)."""

@@ -587,6 +587,12 @@ int hmcx_set_mlp_fuse(hmcx_ctx* ctx, int on) {
   return HMCX_OK;
 }
 
+int hmcx_set_sgld_fuse(hmcx_ctx* ctx, int on) {
+  HMCX_GUARD_CTX(ctx);
+  ctx->wide_nofuse = on ? 0 : 1;
+  return HMCX_OK;
+}
+
 int hmcx_set_graph_mode(hmcx_ctx* ctx, int enabled) {
   HMCX_GUARD_CTX(ctx);
   ctx->graph_mode = enabled ? 1 : 0;

@@ -62,6 +62,7 @@ struct hmcx_ctx {
   // fused MLP launches (hmcx_mlp.hip MM_L23): their own abort word, reported per call (out_abort)
   int* mlp_abort_dev = nullptr;
   int mlp_nofuse = 0;                  // hmcx_set_mlp_fuse(ctx, 0): the sampler runs unfused
+  int wide_nofuse = 0;                 // hmcx_set_sgld_fuse(ctx, 0): wide SGLD on the three launches
   // fused wide-SGLD forward + softmax (hmcx_wide.hip k_wfwd_sm): its own abort word, never the
   // persistent SGHMC kernels' sticky one — read and lowered only by the wide call that raised it
   int* wide_abort_dev = nullptr;

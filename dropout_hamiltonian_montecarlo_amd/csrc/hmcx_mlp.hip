@@ -256,6 +256,7 @@ template <typename T> struct MMProb {
   MaskSrc<T> ms;
   T* ga2; T* pb2; T* pb3; T* pw3; T* gz; double* lpart; T* colpart;
   char* gx;                          // MM_L23: the problem's own region of the granule arena
+  const T* H1;                       // MM_GA1: the gate from this problem's stored h1 (null: from xw, b1, m0)
 };
 template <typename T, int NP> struct MMProbsN {
   MMProb<T> p[NP];
@@ -591,6 +592,7 @@ __device__ __forceinline__ void mm_body(const MMArgs<T>& a, const PR& pr, const 
   const T* const oB = pp ? pp->B : a.B;
   T* const oC = pp ? pp->C : a.C;
   const T* const ob1 = pp ? pp->b1 : a.b1;
+  const T* const oH1 = pp ? pp->H1 : a.H1;
   const T* const obias = pp ? pp->bias : a.bias;
   const T* const oW3 = pp ? pp->W3 : a.W3;
   const T* const obias3 = pp ? pp->bias3 : a.bias3;
@@ -710,10 +712,10 @@ __device__ __forceinline__ void mm_body(const MMArgs<T>& a, const PR& pr, const 
       T g = T(0);
       if (m < a.M && n < a.N) {
         const size_t i = (size_t)m * a.ldc + n;
-        if (a.H1) {
+        if (oH1) {
           // (xw + b1)·m0 > 0 ⟺ h1 > 0, and then m0 = scale; where h1 = 0 the product is ±0 either way
           // (the sign of v·0), so this is the reference's value without reading m0 again
-          const bool pos = a.H1[i] > T(0);
+          const bool pos = oH1[i] > T(0);
           g = (v * (pos ? T(1) : T(0))) * (pos ? oms.scale : T(0));
         } else {
           const T m0v = mval<T, MK>(oms, 0, i);
@@ -990,6 +992,7 @@ constexpr int FR_MAXP = 8;               // problems per launch: six sub-steps +
 template <typename T> struct RbFwdProb {
   const T* xw; const T* xw2;             // layer 1 as split-K planes: xw + xw2 (xw2 null: one plane)
   T* xwout;                              // the summed xw of the block's rows is stored here (null: not)
+  T* h1out;                              // h1 of the block's rows is stored here (null: not)
   const T* b1; const T* W2; const T* b2; const T* W3; const T* b3;
   MaskSrc<T> ms;
   T* ga2; T* pb2; T* pb3; T* pw3;        // outputs, null when not wanted; partials [⌈B/16⌉][…]
@@ -1025,12 +1028,26 @@ __global__ __launch_bounds__(FR_NW * 64) void k_fwdr(RbFwdArgs<T> a) {
   KArgs* ka = (KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
   const int pb = (int)blockIdx.y;
   struct {
-    const T *xw, *xw2; T* xwout; const T *b1, *W2, *b2, *W3, *b3;
+    const T *xw, *xw2; T *xwout, *h1out; const T *b1, *W2, *b2, *W3, *b3;
     const uint32_t* keep; const T* vals; T scale; int mn;
     T *ga2, *pb2, *pb3, *pw3; double* lpart;
-  } P = {ka->p[pb].xw, ka->p[pb].xw2, ka->p[pb].xwout, ka->p[pb].b1, ka->p[pb].W2, ka->p[pb].b2, ka->p[pb].W3, ka->p[pb].b3,
-         ka->p[pb].ms.keep, ka->p[pb].ms.vals, ka->p[pb].ms.scale, ka->p[pb].ms.mn,
+  } P = {ka->p[pb].xw, ka->p[pb].xw2, ka->p[pb].xwout, ka->p[pb].h1out, ka->p[pb].b1, ka->p[pb].W2, ka->p[pb].b2,
+         ka->p[pb].W3, ka->p[pb].b3, ka->p[pb].ms.keep, ka->p[pb].ms.vals, ka->p[pb].ms.scale, ka->p[pb].ms.mn,
          ka->p[pb].ga2, ka->p[pb].pb2, ka->p[pb].pb3, ka->p[pb].pw3, ka->p[pb].lpart};
+  // MK_PHILOX: the masks are drawn here, as the sampler's keep flags would hold them (mask_words: flag e of
+  // forward f = keep_flag(word e % 4 of Philox4x32-10({e / 4, slot, step, chain}, seed)))
+  MaskSrc<T> pms{};
+  if constexpr (MK == MK_PHILOX) {
+    pms.mn = P.mn; pms.seed = ka->p[pb].ms.seed; pms.chain = ka->p[pb].ms.chain; pms.step = ka->p[pb].ms.step;
+    pms.slot = ka->p[pb].ms.slot;
+  }
+  auto pflags = [&](size_t e) {                               // flags e … e + 3 (e % 4 == 0) as 4 bits
+    const u32x4 w = mask_words(pms, e);
+    uint32_t b = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) b |= keep_flag(w.v[q]) ? 1u << q : 0u;
+    return b;
+  };
   const MaskSrc<T> nomask{};
   const int rb = blockIdx.x, m0 = rb * FR_ROWS, nm = a.n_mid, No = a.n_out, M = a.M;
   auto stamp = [&](int ph) {
@@ -1099,10 +1116,29 @@ __global__ __launch_bounds__(FR_NW * 64) void k_fwdr(RbFwdArgs<T> a) {
       m2v4[j] = *reinterpret_cast<const float4*>(P.vals + (size_t)2 * mn + e);
     }
   }
+  if constexpr (MK == MK_PHILOX) {                            // drawn while the loads above are in flight
+#pragma unroll
+    for (int h = 0; h < HP; ++h) hk[h] = pflags(hbase[h]);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      k1[j] = pflags((size_t)mn + ebase[j]);
+      k2[j] = pflags((size_t)2 * mn + ebase[j]);
+    }
+    // pinned here, so the draws overlap the loads in flight instead of sinking into the epilogue
+#pragma unroll
+    for (int h = 0; h < HP; ++h) asm volatile("" : "+v"(hk[h]));
+#pragma unroll
+    for (int j = 0; j < 2; ++j) asm volatile("" : "+v"(k1[j]), "+v"(k2[j]));
+  }
   const int32_t yv = a.y[min(m0 + (tid >> 4), M - 1)];
   const T b3v = P.b3[min(tid & 15, No - 1)];
   // h1 = max((xw + b1)·m0, 0) (mlp.py:30) and W3 into LDS
-  auto mbit = [&](uint32_t w, size_t e, int q) { return ((w >> ((e & 31) + q)) & 1u) ? P.scale : T(0); };
+  // the mask value of flag q of a 4-element piece at element e: one bit of a keep word (bit e % 32 + q), or
+  // bit q of the drawn flags
+  auto mbit = [&](uint32_t w, size_t e, int q) {
+    const uint32_t sh = MK == MK_PHILOX ? (uint32_t)q : (uint32_t)((e & 31) + q);
+    return ((w >> sh) & 1u) ? P.scale : T(0);
+  };
 #pragma unroll
   for (int h = 0; h < HP; ++h) {
     const int e = tid + h * FR_NW * 64, rr = e / (nm / 4), c = (e % (nm / 4)) * 4;
@@ -1117,10 +1153,12 @@ __global__ __launch_bounds__(FR_NW * 64) void k_fwdr(RbFwdArgs<T> a) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         T mk = T(1);
-        if constexpr (MK == MK_KEEP) mk = mbit(hk[h], hbase[h], q);
+        if constexpr (MK == MK_KEEP || MK == MK_PHILOX) mk = mbit(hk[h], hbase[h], q);
         if constexpr (MK == MK_VALS) mk = vv[q];
         At[rr][c + q] = ok ? op_apply<T, OP_H1>(x[q], mk, bb[q]) : T(0);
       }
+      if (P.h1out && ok)                                       // for the layer-1 backward's gate / the W2 gradient
+        *reinterpret_cast<float4*>(P.h1out + hbase[h]) = *reinterpret_cast<const float4*>(&At[rr][c]);
     }
     const int o = e / (FR_NMAX / 4), c3 = (e % (FR_NMAX / 4)) * 4;
     const bool ok3 = o < No && c3 < nm;
@@ -1166,7 +1204,7 @@ __global__ __launch_bounds__(FR_NW * 64) void k_fwdr(RbFwdArgs<T> a) {
       const int n = n0 + 16 * j + Mf::row(lane, q);
       const bool ok = rok && n < nm;
       m1v[j][q] = m2v[j][q] = T(1);
-      if constexpr (MK == MK_KEEP) {
+      if constexpr (MK == MK_KEEP || MK == MK_PHILOX) {
         m1v[j][q] = mbit(k1[j], (size_t)mn + ebase[j], q);
         m2v[j][q] = mbit(k2[j], (size_t)2 * mn + ebase[j], q);
       }
@@ -1825,6 +1863,7 @@ void ga1_build(MlpNet<T>& net, const SubStep<T>* const* ss, int np, MMArgs<T>& a
     q = MMProb<T>{};
     q.A = s.scr->ga2; q.B = s.q[2]; q.C = s.scr->ga1;
     q.b1 = s.q[1]; q.ms = s.ms;
+    q.H1 = s.w.h1 ? s.scr->h1 : nullptr;                        // k_fwdr stored h1: the gate reads it alone
     q.colpart = s.v == 1 ? s.scr->pb1 : nullptr;
   }
   const MMProb<T>& q0 = pr.p[0];
@@ -1956,7 +1995,7 @@ bool fwdr_ok(const MlpNet<T>& net, const SubStep<T>* ss, int n) {
   // on a keep word
   if (net.n_in % 8 || net.B % 4 || ((size_t)(net.B / 4) * net.n_mid) % 32) return false;
   const int mk = mask_kind(ss[0].ms);
-  if (mk != MK_KEEP && mk != MK_VALS) return false;
+  if (mk != MK_KEEP && mk != MK_VALS && mk != MK_PHILOX) return false;
   for (int i = 0; i < n; ++i) {
     const T* xw = ss[i].xw ? ss[i].xw : net.xw;
     if (!vec_ok(xw, net.n_mid, sizeof(T)) || !vec_ok(ss[i].q[2], net.n_mid, sizeof(T)) || mask_kind(ss[i].ms) != mk)
@@ -1986,6 +2025,7 @@ hipError_t mlp_fwdr(MlpNet<T>& net, const SubStep<T>* const* ss, int np) {
     q.xw = x.xw ? x.xw : net.xw;
     q.xw2 = x.xw2;
     q.xwout = x.xwout;
+    q.h1out = x.w.h1 ? x.scr->h1 : nullptr;
     q.b1 = x.q[1]; q.W2 = x.q[2]; q.b2 = x.q[3]; q.W3 = x.q[4]; q.b3 = x.q[5];
     q.ms = x.ms;
     q.ga2 = (x.v >= 0 && x.v <= 2) ? x.scr->ga2 : nullptr;
@@ -1998,7 +2038,9 @@ hipError_t mlp_fwdr(MlpNet<T>& net, const SubStep<T>* const* ss, int np) {
   net.pend.n = 0;
   const dim3 grid((unsigned)net.nrb, (unsigned)(np + (a.pend.n > 0 ? 1 : 0)));
   if constexpr (sizeof(T) == 4) {                              // float32 only (fwdr_ok)
-    if (mask_kind(a.p[0].ms) == MK_KEEP) hipLaunchKernelGGL((k_fwdr<T, MK_KEEP>), grid, dim3(FR_NW * 64), 0, net.st, a);
+    const int mk = mask_kind(a.p[0].ms);
+    if (mk == MK_PHILOX) hipLaunchKernelGGL((k_fwdr<T, MK_PHILOX>), grid, dim3(FR_NW * 64), 0, net.st, a);
+    else if (mk == MK_KEEP) hipLaunchKernelGGL((k_fwdr<T, MK_KEEP>), grid, dim3(FR_NW * 64), 0, net.st, a);
     else hipLaunchKernelGGL((k_fwdr<T, MK_VALS>), grid, dim3(FR_NW * 64), 0, net.st, a);
     return hipGetLastError();
   }
@@ -2039,6 +2081,8 @@ hipError_t mlp_w1_w2split(MlpNet<T>& pn0, const SubStep<T>& s1, const Upd<T>& u1
   wgrad_build(w2n, s2, 2, Upd<T>{}, a2);
   a2.upd_mode = UPD_NONE;
   a2.pend.n = 0;
+  const bool h1 = s2.w.h1;                                     // B = the stored h1 (no xw / b1 / mask reads)
+  if (h1) a2.B = w2n.h1;
   const int nm = w2n.n_mid, Kq = w2n.B / 4;
   a2.K = Kq;
   p2.n = 4;
@@ -2049,6 +2093,7 @@ hipError_t mlp_w1_w2split(MlpNet<T>& pn0, const SubStep<T>& s1, const Upd<T>& u1
     x.ms = a2.ms;
     if (x.ms.keep) x.ms.keep += r0 / 32;
     if (x.ms.vals) x.ms.vals += r0;
+    if (h1) x.ms = MaskSrc<T>{};
   }
   a2.C = p2.p[0].C; a2.ldc = nm;
   const int3 g1 = make_int3((a1.M + 31) / 32, (a1.N + 31) / 32, 1 + (a1.pend.n > 0 ? 1 : 0));
@@ -2060,6 +2105,11 @@ hipError_t mlp_w1_w2split(MlpNet<T>& pn0, const SubStep<T>& s1, const Upd<T>& u1
       hipLaunchKernelGGL((k_mm2b<T, MM_UPD, OP_PLAIN, OP_PLAIN, 1, 0, 0, 0, MM_STORE, OP_PLAIN, OP_H1, 1, 0, 0, 0, MK>),
                          grid, dim3(MM_NT), 0, pn0.st, a1, p1, a2, p2, g1, g2);
     };
+    if (h1) {
+      hipLaunchKernelGGL((k_mm2b<T, MM_UPD, OP_PLAIN, OP_PLAIN, 1, 0, 0, 0, MM_STORE, OP_PLAIN, OP_PLAIN, 1, 0, 0, 0, MK_NONE>),
+                         grid, dim3(MM_NT), 0, pn0.st, a1, p1, a2, p2, g1, g2);
+      return hipGetLastError();
+    }
     if (mask_kind(a2.ms) == MK_KEEP) go(std::integral_constant<int, MK_KEEP>{});
     else go(std::integral_constant<int, MK_VALS>{});
     return hipGetLastError();
@@ -2500,7 +2550,24 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
     const int n = s->n_iter[si], F = 6 * n + 2;
     const uint32_t step_id = s->step_base + (uint32_t)si;
     const double* nz = s->noise_mode == HMCX_NOISE_BUFFER ? s->noise + s->noise_off[si] : nullptr;
-    const bool fused_start = philox_masks && keep_arr;       // keep flags in the momentum launch
+    // the k_fwdr path for this step's iterations (decided before the momentum launch: with Philox masks
+    // k_fwdr draws every mask itself, so the step's keep flags are not drawn at all)
+    bool fr_step = false;
+    if (batch && n > 0) {
+      SubStep<T> chk[6];
+      for (int i = 0; i < 6; ++i) {
+        for (int j = 0; j < 6; ++j) chk[i].q[s->order[j]] = j <= i ? qa[s->order[j]] : par[s->order[j]];
+        chk[i].xw = xw_par;
+        chk[i].ms = !philox_masks ? MaskSrc<T>{(const T*)s->masks + s->mask_off[si], nullptr, scale, mn, 0, 0, 0, 0}
+                    : keep_arr ? MaskSrc<T>{nullptr, keep, scale, mn, 0, 0, 0, 0}
+                               : MaskSrc<T>{nullptr, nullptr, scale, mn, s->seed, s->chain, step_id, MASK_SLOT0};
+      }
+      fr_step = fwdr_ok(net, chk, 6);
+    }
+    // keep flags of every forward of the step in the momentum launch (compute-bound Philox draws: drawn
+    // instead beside each iteration's last launch, in an extra plane, they lengthened that launch by as
+    // much as they took off this one — 21.46 k vs 22.2 k leapfrog/s at config 3)
+    const bool fused_start = philox_masks && keep_arr;
     auto masks_for = [&](int f) -> MaskSrc<T> {
       // PHILOX: the kernels draw the flags they read (MK_PHILOX, slot MASK_SLOT0 + f); with
       // HMCX_MLP_MASKS=keep, k_mlp_keep stores the same flags once per step and the kernels load them
@@ -2602,7 +2669,7 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
           for (int i = 0; i < 6; ++i) chk[i] = ss[i];
           chk[6] = es[0];
           chk[7] = es[1];
-          use_fr = fwdr_ok(net, chk, 8);
+          use_fr = fr_step && fwdr_ok(net, chk, 8);
         }
         if (use_fr) {
           // 4 launches per iteration, the layer-1 GEMM and the W2 gradient as split-K partials:
@@ -2623,6 +2690,9 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
           for (int i = 0; i < 6; ++i) {
             ss[i].xw = xwp[0];
             ss[i].xw2 = xwp[1];
+            // masks drawn inside k_fwdr (HMCX_MLP_MASKS=philox) live only there: it stores h1 for the W1 / b1
+            // gates and the W2 gradient
+            ss[i].w.h1 = philox_masks && !keep_arr && ss[i].v <= 2;
             fa[na++] = &ss[i];
           }
           ss[0].xwout = net.xw;

@@ -635,7 +635,10 @@ static int sgld_wide_impl(hmcx_ctx* ctx, const hmcx_sampler_args* s, bool allow_
   // the whole forward grid is co-resident and a workgroup's gathered partials fit its LDS stage;
   // HMCX_WIDE_FUSE=0 keeps the three launches
   const int fuse_env = getenv("HMCX_WIDE_FUSE") ? atoi(getenv("HMCX_WIDE_FUSE")) : 1;     // read per call (tests)
-  bool fuse = allow_fuse && fuse_env != 0 && S * ((WRB + S - 1) / S) * K <= WSM_STAGE;
+  bool fuse = allow_fuse && !ctx->wide_nofuse && fuse_env != 0 && S * ((WRB + S - 1) / S) * K <= WSM_STAGE;
+  // out_abort set: the call's verdict is stream-ordered into it and the caller, which keeps the start
+  // state, re-runs a timed-out call itself — no snapshot here and no wait for the stream
+  const bool defer = s->out_abort != nullptr;
   if (fuse) {
     int per_cu = 0, rc0 = kernel_occupancy(ctx, fwd_sm_fn<T>(KP), WTH, 0, &per_cu);
     if (rc0) return rc0;
@@ -660,7 +663,7 @@ static int sgld_wide_impl(hmcx_ctx* ctx, const hmcx_sampler_args* s, bool allow_
     slab = fuse ? nullptr : ws.take<T>((size_t)S * C * B * KP);
     diff = ws.take<T>((size_t)C * B * KP);
     llp = ws.take<double>((size_t)C * std::max(nSB, nRB * S));
-    if (fuse) {                        // the call's start state, for the unfused re-run after a timeout
+    if (fuse && !defer) {              // the call's start state, for the unfused re-run after a timeout
       snapW = ws.take<T>(nW);
       snapb = ws.take<T>(nb);
       if (s->pW) { snappW = ws.take<T>(nW); snappb = ws.take<T>(nb); }
@@ -683,7 +686,7 @@ static int sgld_wide_impl(hmcx_ctx* ctx, const hmcx_sampler_args* s, bool allow_
   }
   begin_call(ctx);
   if (buf && (rc = upload(ctx, d_noff, s->noise_off, nsc * sizeof(int64_t)))) return rc;
-  if (fuse) {
+  if (fuse && !defer) {
     HMCX_HIP(ctx, hipMemcpyAsync(snapW, s->W, nW * sizeof(T), hipMemcpyDeviceToDevice, ctx->stream));
     HMCX_HIP(ctx, hipMemcpyAsync(snapb, s->b, nb * sizeof(T), hipMemcpyDeviceToDevice, ctx->stream));
     if (snappW) {
@@ -762,7 +765,16 @@ static int sgld_wide_impl(hmcx_ctx* ctx, const hmcx_sampler_args* s, bool allow_
   }
   if ((rc = gs.finish())) return rc;
   if ((rc = timing_end(ctx, ctx->stream))) return rc;
-  if (fuse) {
+  if (defer) {
+    // the verdict (1: a team round timed out, W / b are invalid) into the caller's slot and the word
+    // lowered, both stream-ordered: the call returns without waiting for its kernels
+    if (fuse) {
+      HMCX_HIP(ctx, hipMemcpyAsync(s->out_abort, ctx->wide_abort_dev, sizeof(int), hipMemcpyDeviceToDevice, ctx->stream));
+      HMCX_HIP(ctx, hipMemsetAsync(ctx->wide_abort_dev, 0, sizeof(int), ctx->stream));
+    } else {
+      HMCX_HIP(ctx, hipMemsetAsync(s->out_abort, 0, sizeof(int32_t), ctx->stream));
+    }
+  } else if (fuse) {
     // a timed-out team round raised the wide abort word (the launch's workgroups then stopped early): put
     // the call's start state back, lower the word and run the call again on the three-launch path — same
     // operands, same noise, so the result is the one the fused call would have given.  The check waits

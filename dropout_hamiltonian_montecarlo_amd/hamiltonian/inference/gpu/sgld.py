@@ -88,9 +88,28 @@ class sgld(sgmcmc):
             out_steps = torch.empty((n_steps, C, P), dtype=self.model.dtype, device=dev)
             a.out_trace = ptr(out_steps)
         ctx = nat.context(dev)
+        # the call's verdict (include/hmcx.h out_abort): a fused wide-SGLD call that timed out in a team
+        # round leaves W / b invalid; the start state is kept here and the call re-run on the three
+        # launches — same noise, same result — so the call itself never waits for its stream
+        out_abort = torch.zeros(1, dtype=torch.int32, device=dev)
+        a.out_abort = ptr(out_abort)
+        saved = [t.clone() for t in ((W, b) if self.variant != 'gpu' else (W, b, mom['weights'], mom['bias']))]
         ctx.check(ctx.lib.hmcx_sgld_run(ctx.h, a), "hmcx_sgld_run")
-        self.global_step += n_steps
         ll = out_ll.cpu().numpy()
+        if int(out_abort.item()):
+            import sys
+            print("[hmcx] wide SGLD: a team round timed out; call re-run on the three-launch path", file=sys.stderr)
+            for t, s0 in zip((W, b) if self.variant != 'gpu' else (W, b, mom['weights'], mom['bias']), saved):
+                t.copy_(s0)
+            ctx.set_sgld_fuse(False)
+            try:
+                ctx.check(ctx.lib.hmcx_sgld_run(ctx.h, a), "hmcx_sgld_run (unfused re-run)")
+            finally:
+                ctx.set_sgld_fuse(True)
+            ctx.note_recovery("sgld_wide_fused")
+            ll = out_ll.cpu().numpy()
+        del saved
+        self.global_step += n_steps
         if C > 1:
             ll = ll.reshape(n_steps, C)
         if self.trace is not None:

@@ -177,6 +177,9 @@ typedef struct hmcx_sampler_args {
                            /* timed out in a hand-off (or followed one that did) and left */
                            /* W/b untouched — see hmcx_clear_abort.  NULL: the check is    */
                            /* deferred to the next call / hmcx_synchronize instead.       */
+                           /* SGLD (wide path): 1 when a fused team round timed out; W/b  */
+                           /* are then invalid (hmcx_set_sgld_fuse).  NULL: the call re-runs */
+                           /* itself and waits for its stream.                            */
   double path_length;      /* SGHMC, PHILOX mode with n_iter == u_accept == NULL: the call */
   double* out_L;           /* draws its own schedule (hmcx_philox_schedule, this path     */
                            /* length); out_L (host [n_steps*C] or NULL) receives the L's  */
@@ -423,6 +426,13 @@ int hmcx_mlp_hmc_leapfrog(hmcx_ctx* ctx, const hmcx_mlp_leapfrog_args* a);
 /* on = 0: hmcx_mlp_sghmc_run stops fusing layer 2 and layer 3 into one launch (no cross-workgroup
  * exchange; one more launch per forward) — the recovery path after out_abort; on = 1 restores it. */
 int hmcx_set_mlp_fuse(hmcx_ctx* ctx, int on);
+/* Wide SGLD (config 5, hmcx_sgld_run with K ≤ 64 or several chains): fused forward + softmax (1, the
+ * default) or the three-launch form (0).  A fused call given out_abort stores its verdict there
+ * (stream-ordered, no host wait): 1 means a team round timed out and W / b (pW / pb) are invalid —
+ * restore the start state and re-run the call with hmcx_set_sgld_fuse(ctx, 0).  Without out_abort the
+ * call restores and re-runs itself and waits for its stream (hmcx_get_recoveries counts either re-run
+ * once the caller reports its own with hmcx_note_recovery). */
+int hmcx_set_sgld_fuse(hmcx_ctx* ctx, int on);
 
 /* ------------------------------------------------------------------ cross-rank gather (RCCL)
  * Replaces the reference's multi-chain result collection (hamiltonian/inference/cpu/
