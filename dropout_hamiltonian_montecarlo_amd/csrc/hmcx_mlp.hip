@@ -54,17 +54,65 @@ template <typename T> struct MaskSrc {
                           // neither vals nor keep: no dropout or MK_PHILOX
   T scale;
   int mn;
-  // MK_PHILOX: the keep flags are drawn where they are used — element e = which·mn + i is word e % 4
-  // of Philox4x32-10({e / 4, slot, step, chain}, seed), the values k_mlp_keep and hmcx_mlp_masks give
+  // MK_PHILOX: the keep flags are drawn where they are used — element e = which·mn + i is bit e % 64 of
+  // keep_group(e / 64) under (seed, slot, step, chain), the values k_mlp_start and hmcx_mlp_masks give
   uint64_t seed; uint32_t chain, step, slot;
 };
 
-__device__ inline bool keep_flag(uint32_t w) {                // Chainer dropout: keep iff u >= ratio
-  return (float)(w >> 8) * 5.9604644775390625e-08f >= 0.1f;
+// Dropout keep flags (Chainer, mlp.py:30-31: keep iff u >= ratio 0.1, u a 24-bit float32 uniform — keep iff
+// x >= 0x19999A for x uniform on [0, 2^24)), 64 elements per group G of one forward's flag space: element
+// 64G + p is bit p of {lo, hi} (bit p % 32 of word p / 32: the keep-word layout).  Its x takes its top byte
+// from byte p / 8 % 4 of word 8·(p / 32) + p % 8 of blocks 4G … 4G + 3 = Philox4x32-10({4G + k, slot, step,
+// chain}, seed) (word k·4 + q of the group = word q of block k): a byte below 0x19 drops, above keeps;
+// a byte equal to 0x19 (p = 1/256) takes x's low 16 bits from the fallback blocks Philox({0x80000000 |
+// 8G + j, slot, step, chain}) — the a-th such element of the group (ascending p) reads 16-bit half a % 8
+// (low half first) of block j = a / 8 — and keeps iff they are >= 0x999A.  Exactly the 24-bit law, at 16
+// flags per Philox block plus about one fallback block per group (the round-5 form drew 4 per block).
+// Host twin: tests/test_gpu_mlp.py::_keep_group_host.
+__host__ __device__ inline uint32_t bytes_gt19(uint32_t w) {       // bit 8b + 7: byte b > 0x19
+  return (((w & 0x7F7F7F7Fu) + 0x66666666u) | w) & 0x80808080u;
 }
-template <typename T> __device__ inline u32x4 mask_words(const MaskSrc<T>& s, size_t e) {
-  u32x4 c = {{(uint32_t)(e >> 2), s.slot, s.step, s.chain}};
-  return philox4x32_10(c, (uint32_t)s.seed, (uint32_t)(s.seed >> 32));
+__host__ __device__ inline uint32_t bytes_eq19(uint32_t w) {       // bit 8b + 7: byte b == 0x19
+  const uint32_t z = w ^ 0x19191919u;
+  return ~(((z & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | z) & 0x80808080u;
+}
+struct KeepGroup { uint32_t lo, hi; };
+__host__ __device__ inline KeepGroup keep_group(uint64_t seed, uint32_t G, uint32_t slot, uint32_t step,
+                                                uint32_t chain) {
+  const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+  uint32_t f0 = 0, f1 = 0, a0 = 0, a1 = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const u32x4 r = philox4x32_10(u32x4{{4u * G + (uint32_t)k, slot, step, chain}}, k0, k1);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int j = (k & 1) * 4 + q;                           // word of the half: bits 8b + j
+      const uint32_t gt = bytes_gt19(r.v[q]) >> (7 - j), eq = bytes_eq19(r.v[q]) >> (7 - j);
+      if (k < 2) { f0 |= gt; a0 |= eq; } else { f1 |= gt; a1 |= eq; }
+    }
+  }
+  for (uint32_t j = 0; (a0 | a1) != 0u; ++j) {                 // at most 8 blocks (64 ambiguous bytes)
+    const u32x4 r = philox4x32_10(u32x4{{0x80000000u | (G << 3) | j, slot, step, chain}}, k0, k1);
+#pragma unroll
+    for (int h = 0; h < 8; ++h) {
+      const bool keep = ((r.v[h >> 1] >> (16 * (h & 1))) & 0xFFFFu) >= 0x999Au;
+      if (a0) {
+        const uint32_t low = a0 & (0u - a0);
+        if (keep) f0 |= low;
+        a0 ^= low;
+      } else if (a1) {
+        const uint32_t low = a1 & (0u - a1);
+        if (keep) f1 |= low;
+        a1 ^= low;
+      }
+    }
+  }
+  return KeepGroup{f0, f1};
+}
+// the keep word (32 flags) holding element e of a MK_PHILOX source: bit e % 32
+template <typename T> __device__ inline uint32_t philox_keep_word(const MaskSrc<T>& s, size_t e) {
+  const KeepGroup g = keep_group(s.seed, (uint32_t)(e >> 6), s.slot, s.step, s.chain);
+  return (e & 32) ? g.hi : g.lo;
 }
 
 // Where the masks come from is a compile-time parameter (MK) of every kernel that reads them, so a
@@ -78,7 +126,7 @@ template <typename T, int MK> __device__ inline MRaw<T> mraw(const MaskSrc<T>& s
   const size_t e = (size_t)which * s.mn + i;
   if constexpr (MK == MK_KEEP) r.k = (s.keep[e >> 5] >> (e & 31)) & 1u;
   if constexpr (MK == MK_VALS) r.v = s.vals[e];
-  if constexpr (MK == MK_PHILOX) r.k = keep_flag(mask_words(s, e).v[e & 3]) ? 1u : 0u;
+  if constexpr (MK == MK_PHILOX) r.k = (philox_keep_word(s, e) >> (e & 31)) & 1u;
   return r;
 }
 template <typename T, int MK> __device__ inline void mpin(MRaw<T>& r) {
@@ -112,10 +160,10 @@ template <typename T, int V, int MK> __device__ inline void mvals(const MaskSrc<
     k >>= (e & 31);
 #pragma unroll
     for (int q = 0; q < V; ++q) m[q] = ((k >> q) & 1u) ? s.scale : T(0);
-  } else if constexpr (MK == MK_PHILOX) {                        // e % V == 0: one Philox block
-    const u32x4 w = mask_words(s, e);
+  } else if constexpr (MK == MK_PHILOX) {                        // e % V == 0: V bits of one keep word
+    const uint32_t k = philox_keep_word(s, e) >> (e & 31);
 #pragma unroll
-    for (int q = 0; q < V; ++q) m[q] = keep_flag(w.v[(e & 3) + q]) ? s.scale : T(0);
+    for (int q = 0; q < V; ++q) m[q] = ((k >> q) & 1u) ? s.scale : T(0);
   } else {
 #pragma unroll
     for (int q = 0; q < V; ++q) m[q] = T(1);
@@ -1034,19 +1082,15 @@ __global__ __launch_bounds__(FR_NW * 64) void k_fwdr(RbFwdArgs<T> a) {
   } P = {ka->p[pb].xw, ka->p[pb].xw2, ka->p[pb].xwout, ka->p[pb].h1out, ka->p[pb].b1, ka->p[pb].W2, ka->p[pb].b2,
          ka->p[pb].W3, ka->p[pb].b3, ka->p[pb].ms.keep, ka->p[pb].ms.vals, ka->p[pb].ms.scale, ka->p[pb].ms.mn,
          ka->p[pb].ga2, ka->p[pb].pb2, ka->p[pb].pb3, ka->p[pb].pw3, ka->p[pb].lpart};
-  // MK_PHILOX: the masks are drawn here, as the sampler's keep flags would hold them (mask_words: flag e of
-  // forward f = keep_flag(word e % 4 of Philox4x32-10({e / 4, slot, step, chain}, seed)))
+  // MK_PHILOX: the masks are drawn here, as the sampler's keep flags would hold them (flag e of forward f =
+  // bit e % 64 of keep_group(e / 64) under slot MASK_SLOT0 + f)
   MaskSrc<T> pms{};
   if constexpr (MK == MK_PHILOX) {
     pms.mn = P.mn; pms.seed = ka->p[pb].ms.seed; pms.chain = ka->p[pb].ms.chain; pms.step = ka->p[pb].ms.step;
     pms.slot = ka->p[pb].ms.slot;
   }
   auto pflags = [&](size_t e) {                               // flags e … e + 3 (e % 4 == 0) as 4 bits
-    const u32x4 w = mask_words(pms, e);
-    uint32_t b = 0;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) b |= keep_flag(w.v[q]) ? 1u << q : 0u;
-    return b;
+    return (philox_keep_word(pms, e) >> (e & 31)) & 0xFu;
   };
   const MaskSrc<T> nomask{};
   const int rb = blockIdx.x, m0 = rb * FR_ROWS, nm = a.n_mid, No = a.n_out, M = a.M;
@@ -1344,35 +1388,46 @@ __global__ __launch_bounds__(FR_NW * 64) void k_fwdr(RbFwdArgs<T> a) {
   stamp(7);
 }
 
-// Keep flags of forward f, one bit per element (bit e % 32 of word e / 32; forward f's words start at
-// f·⌈n3/32⌉).  Thread g draws Philox block g (flags 4g … 4g + 3, flag e = keep_flag(word e % 4)); eight
-// neighbouring lanes OR their nibbles into one word, which the first of them stores.
-__device__ inline void keep_flags(uint32_t* keep, int n3, uint64_t seed, uint32_t chain, uint32_t step, int g, int f) {
-  const int W = (n3 + 31) / 32;
-  u32x4 c = {{(uint32_t)g, MASK_SLOT0 + (uint32_t)f, step, chain}};
-  const u32x4 r = philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
-  uint32_t w = 0;
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-    if (4 * g + q < n3 && keep_flag(r.v[q])) w |= 1u << q;
-  w <<= 4 * (g & 7);
-  w |= __shfl_xor(w, 1, 8);                                   // every lane of the group takes part
-  w |= __shfl_xor(w, 2, 8);
-  w |= __shfl_xor(w, 4, 8);
-  if ((g & 7) == 0 && (g >> 3) < W) keep[(size_t)f * W + (g >> 3)] = w;
+// Keep flags of a step's forwards, one bit per element (bit e % 32 of word e / 32; forward f's words start
+// at f·⌈n3/32⌉): work item gi = f·⌈n3/64⌉ + G draws keep_group(G) of forward f (slot MASK_SLOT0 + f) and
+// stores its two words (flags past n3 zero).
+__device__ inline void keep_flags(uint32_t* keep, int n3, int nf, uint64_t seed, uint32_t chain, uint32_t step,
+                                  size_t gi) {
+  const int W = (n3 + 31) / 32, ng = (n3 + 63) / 64;
+  if (gi >= (size_t)nf * ng) return;
+  const int f = (int)(gi / (size_t)ng), G = (int)(gi - (size_t)f * ng);
+  const KeepGroup k = keep_group(seed, (uint32_t)G, MASK_SLOT0 + (uint32_t)f, step, chain);
+  const int e0 = 64 * G;
+  const uint32_t lo = n3 - e0 >= 32 ? k.lo : k.lo & ((1u << (n3 - e0)) - 1u);
+  const uint32_t hi = n3 - e0 >= 64 ? k.hi : n3 - e0 > 32 ? k.hi & ((1u << (n3 - e0 - 32)) - 1u) : 0u;
+  uint32_t* dst = keep + (size_t)f * W + 2 * G;
+  dst[0] = lo;
+  if (2 * G + 1 < W) dst[1] = hi;
 }
 
-// Mask values of one forward (the API twin of k_mlp_keep: same counters, value = keep·(1/0.9)).
+// Mask values of one forward (the API twin of the sampler's keep flags: same groups, value = keep·(1/0.9)).
+// Thread g: group g (64 elements), written as 16-byte vectors.
 template <typename T>
 __global__ void k_mlp_masks(T* masks, int n3, uint64_t seed, uint32_t chain, uint32_t step, uint32_t slot) {
   const int g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (4 * g >= n3) return;
-  u32x4 c = {{(uint32_t)g, slot, step, chain}};
-  const u32x4 r = philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+  if (64 * g >= n3) return;
+  const KeepGroup k = keep_group(seed, (uint32_t)g, slot, step, chain);
   const T scale = (T)(1.0 / 0.9);
+  constexpr int V = 16 / sizeof(T);
+  typedef T tv __attribute__((ext_vector_type(V)));
+  const int e0 = 64 * g, n = min(64, n3 - e0);
+  for (int p = 0; p < 64; p += V) {
+    tv v;
 #pragma unroll
-  for (int q = 0; q < 4; ++q)
-    if (4 * g + q < n3) masks[4 * g + q] = keep_flag(r.v[q]) ? scale : T(0);
+    for (int q = 0; q < V; ++q) v[q] = (((p + q < 32 ? k.lo >> (p + q) : k.hi >> (p + q - 32)) & 1u) ? scale : T(0));
+    if (p + V <= n && (reinterpret_cast<uintptr_t>(masks + e0 + p) & 15) == 0) {
+      *reinterpret_cast<tv*>(masks + e0 + p) = v;
+    } else {
+#pragma unroll
+      for (int q = 0; q < V; ++q)
+        if (p + q < n) masks[e0 + p + q] = v[q];
+    }
+  }
 }
 
 template <typename T>
@@ -1444,17 +1499,18 @@ __global__ __launch_bounds__(256) void k_mlp_init(VarTab vt, T eps, int drift, i
   init_block<T>(vt, eps, drift, noise_mode, noise, seed, chain, step, part, (int)blockIdx.y, (int)blockIdx.x, prev_acc);
 }
 // Step start in one launch: rows y < 6 draw the momentum of variable y and the first drift (k_mlp_init),
-// rows y ≥ 6 the keep flags of forward y − 6 (k_mlp_keep) — independent work, one launch less per step.
+// rows y ≥ 6 the keep flags of the step's nf forwards (keep_flags; work item (y − 6, x, thread) in
+// row-major order) — independent work, one launch less per step.  grid.x = NPART.
 template <typename T>
 __global__ __launch_bounds__(256) void k_mlp_start(VarTab vt, T eps, int drift, int noise_mode, const double* noise,
                                                    uint64_t seed, uint32_t chain, uint32_t step, double* part,
-                                                   const int32_t* prev_acc, uint32_t* keep, int n3) {
+                                                   const int32_t* prev_acc, uint32_t* keep, int n3, int nf) {
   if (blockIdx.y < 6) {
-    if (blockIdx.x < NPART)
-      init_block<T>(vt, eps, drift, noise_mode, noise, seed, chain, step, part, (int)blockIdx.y, (int)blockIdx.x,
-                    prev_acc);
+    init_block<T>(vt, eps, drift, noise_mode, noise, seed, chain, step, part, (int)blockIdx.y, (int)blockIdx.x,
+                  prev_acc);
   } else {
-    keep_flags(keep, n3, seed, chain, step, (int)(blockIdx.x * blockDim.x + threadIdx.x), (int)blockIdx.y - 6);
+    keep_flags(keep, n3, nf, seed, chain, step,
+               ((size_t)(blockIdx.y - 6) * NPART + blockIdx.x) * 256 + threadIdx.x);
   }
 }
 
@@ -2286,7 +2342,7 @@ template <typename T>
 int mlp_masks_t(hmcx_ctx* ctx, int B, int n_mid, uint64_t seed, uint32_t chain, uint32_t step, uint32_t slot,
                 void* out) {
   const int n3 = 3 * B * n_mid;
-  hipLaunchKernelGGL(k_mlp_masks<T>, dim3((unsigned)(((n3 + 3) / 4 + 255) / 256)), dim3(256), 0, ctx->stream,
+  hipLaunchKernelGGL(k_mlp_masks<T>, dim3((unsigned)(((n3 + 63) / 64 + 255) / 256)), dim3(256), 0, ctx->stream,
                      (T*)out, n3, seed, chain, step, slot);
   HMCX_HIP(ctx, hipGetLastError());
   return HMCX_OK;
@@ -2586,9 +2642,10 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
     const int32_t* prev_acc = commit_pending ? accf : nullptr;   // the previous step's commit, folded in
     commit_pending = false;
     if (fused_start) {
-      const unsigned kb = (unsigned)((8 * kw + 255) / 256);
-      hipLaunchKernelGGL(k_mlp_start<T>, dim3(std::max(kb, (unsigned)NPART), (unsigned)(6 + F)), dim3(256), 0, st, vt, (T)eps,
-                         n > 0 ? 1 : 0, s->noise_mode, nz, s->seed, s->chain, step_id, part_cur, prev_acc, keep, n3);
+      const size_t items = (size_t)F * ((n3 + 63) / 64);            // one keep group per thread
+      const unsigned rows = (unsigned)((items + (size_t)NPART * 256 - 1) / ((size_t)NPART * 256));
+      hipLaunchKernelGGL(k_mlp_start<T>, dim3(NPART, 6 + rows), dim3(256), 0, st, vt, (T)eps,
+                         n > 0 ? 1 : 0, s->noise_mode, nz, s->seed, s->chain, step_id, part_cur, prev_acc, keep, n3, F);
     } else {
       hipLaunchKernelGGL(k_mlp_init<T>, dim3(NPART, 6), dim3(256), 0, st, vt, (T)eps, n > 0 ? 1 : 0, s->noise_mode,
                          nz, s->seed, s->chain, step_id, part_cur, prev_acc);

@@ -410,6 +410,62 @@ def test_mlp_timeout_reported_through_c_abi_without_out_abort(monkeypatch):
     torch.cuda.synchronize()
 
 
+def _philox_host(c0, c1, c2, c3, seed):
+    """Philox4x32-10 of counters (c0 vector, c1..c3 scalars) under key `seed`: the four output words."""
+    M0, M1, m32 = np.uint64(0xD2511F53), np.uint64(0xCD9E8D57), np.uint64(0xFFFFFFFF)
+    c0 = np.asarray(c0, dtype=np.uint64)
+    c1, c2, c3 = (np.full(c0.shape, v & 0xFFFFFFFF, dtype=np.uint64) for v in (c1, c2, c3))
+    k0, k1 = seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF
+    for _ in range(10):
+        p0, p1 = M0 * c0, M1 * c2
+        c0, c1, c2, c3 = (p1 >> np.uint64(32)) ^ c1 ^ np.uint64(k0), p1 & m32, \
+            (p0 >> np.uint64(32)) ^ c3 ^ np.uint64(k1), p0 & m32
+        k0, k1 = (k0 + 0x9E3779B9) & 0xFFFFFFFF, (k1 + 0xBB67AE85) & 0xFFFFFFFF
+    return c0, c1, c2, c3
+
+
+def _keep_group_host(seed, n3, slot, step, chain):
+    """Host twin of hmcx_mlp.hip::keep_group, written from its definition (per-byte compares, not the
+    kernel's SWAR form): the keep flags of elements 0 … n3 − 1 of one forward."""
+    nG = (n3 + 63) // 64
+    G = np.arange(nG, dtype=np.uint64)
+    words = []                                                     # word kk = 4k + q of the group
+    for k in range(4):
+        words.extend(_philox_host(4 * G + k, slot, step, chain, seed))
+    p = np.arange(64)
+    widx = 8 * (p // 32) + p % 8                                   # element p: word, byte
+    byte = np.stack([(words[w] >> np.uint64(8 * ((q // 8) % 4))) & np.uint64(0xFF)
+                     for q, w in zip(p, widx)], axis=1).astype(np.int64)          # [nG, 64]
+    keep = byte > 0x19
+    for g in np.nonzero((byte == 0x19).any(axis=1))[0]:
+        amb = np.nonzero(byte[g] == 0x19)[0]                       # ascending element order
+        for a, e in enumerate(amb):
+            r = _philox_host([0x80000000 | (int(g) << 3) | (a // 8)], slot, step, chain, seed)
+            h = a % 8
+            x = (int(r[h // 2][0]) >> (16 * (h % 2))) & 0xFFFF
+            keep[g, e] = x >= 0x999A
+    return keep.reshape(-1)[:n3]
+
+
+@pytest.mark.parametrize("B,n_mid", [(19, 37), (500, 256)])
+def test_api_masks_equal_host_keep_groups(B, n_mid):
+    """hmcx_mlp_masks (and with it every Philox keep flag of the sampler, test below) is bit for bit the
+    host restatement of the grouped keep-flag draw: 16 flags per Philox block, the byte == 0x19 ties
+    resolved from the fallback blocks — a ragged last group (n3 = 2109) and config 3's 384,000 flags,
+    among which ≈ 1,500 ties."""
+    from dropout_hamiltonian_montecarlo_amd import _native as nat
+    ctx = nat.context(0)
+    n3 = 3 * B * n_mid
+    out = torch.empty(n3, dtype=torch.float32, device="cuda:0")
+    seed, chain, step, slot = 0x123456789AB, 7, 11, (nat.MLP_MASK_SLOT0 + 5) & 0xFFFFFFFF
+    ctx.check(ctx.lib.hmcx_mlp_masks(ctx.h, nat.HMCX_F32, B, n_mid, seed, chain, step, slot, nat.ptr(out)),
+              "hmcx_mlp_masks")
+    got = out.cpu().numpy()
+    want = _keep_group_host(seed, n3, slot, step, chain)
+    np.testing.assert_array_equal(got != 0, want)
+    assert set(np.unique(got)) <= {np.float32(0), np.float32(1 / 0.9)}
+
+
 @pytest.mark.parametrize("variant", ["keep", "philox-h1"])
 def test_sampler_philox_masks_equal_api_masks(variant, monkeypatch):
     """In Philox mode the sampler's dropout flags — stored once per step by k_mlp_keep (default) or
