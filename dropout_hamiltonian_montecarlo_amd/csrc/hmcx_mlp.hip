@@ -109,6 +109,26 @@ __host__ __device__ inline KeepGroup keep_group(uint64_t seed, uint32_t G, uint3
   }
   return KeepGroup{f0, f1};
 }
+// Keep flags of a step's forwards, one bit per element (bit e % 32 of word e / 32; forward f's words start
+// at f·⌈n3/32⌉): work item gi = fl·⌈n3/64⌉ + G draws keep_group(G) of forward f (slot MASK_SLOT0 + f) and
+// stores its two words (flags past n3 zero).  The nf forwards drawn: f = f0 + fl for fl < nlo, then
+// fhi + (fl − nlo) — a contiguous range, or one range and the step's two energy forwards.
+struct KeepRange { int nf, f0, nlo, fhi; };
+__device__ inline void keep_flags(uint32_t* keep, int n3, KeepRange kr, uint64_t seed, uint32_t chain, uint32_t step,
+                                  size_t gi) {
+  const int W = (n3 + 31) / 32, ng = (n3 + 63) / 64;
+  if (gi >= (size_t)kr.nf * ng) return;
+  const int fl = (int)(gi / (size_t)ng), G = (int)(gi - (size_t)fl * ng);
+  const int f = fl < kr.nlo ? kr.f0 + fl : kr.fhi + (fl - kr.nlo);
+  const KeepGroup k = keep_group(seed, (uint32_t)G, MASK_SLOT0 + (uint32_t)f, step, chain);
+  const int e0 = 64 * G;
+  const uint32_t lo = n3 - e0 >= 32 ? k.lo : k.lo & ((1u << (n3 - e0)) - 1u);
+  const uint32_t hi = n3 - e0 >= 64 ? k.hi : n3 - e0 > 32 ? k.hi & ((1u << (n3 - e0 - 32)) - 1u) : 0u;
+  uint32_t* dst = keep + (size_t)f * W + 2 * G;
+  dst[0] = lo;
+  if (2 * G + 1 < W) dst[1] = hi;
+}
+
 // the keep word (32 flags) holding element e of a MK_PHILOX source: bit e % 32
 template <typename T> __device__ inline uint32_t philox_keep_word(const MaskSrc<T>& s, size_t e) {
   const KeepGroup g = keep_group(s.seed, (uint32_t)(e >> 6), s.slot, s.step, s.chain);
@@ -1052,6 +1072,9 @@ template <typename T> struct RbFwdArgs {
   RbFwdProb<T> p[FR_MAXP];
   PendSet<T> pend;                       // pending updates: run by the extra plane blockIdx.y == np
   unsigned long long* prof;              // HMCX_FWDR_PROF: FR_NPH s_memrealtime stamps per workgroup
+  // the NEXT iteration's keep flags, drawn by the rows after the problems and the pending plane (kr.nf == 0:
+  // none): they land on the CUs the problems leave free (192 + 32 workgroups on 256 CUs)
+  uint32_t* keep; int n3; KeepRange kr; uint64_t seed; uint32_t chain, step;
 };
 constexpr int FR_NPH = 8;
 
@@ -1065,6 +1088,12 @@ __global__ __launch_bounds__(FR_NW * 64) void k_fwdr(RbFwdArgs<T> a) {
   __shared__ T gzs[16][17];                                       // gz[r][o]
   __shared__ double rowl[FR_ROWS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lg = lane >> 4;
+  if ((int)blockIdx.y >= a.np + (a.pend.n > 0 ? 1 : 0)) {         // the next iteration's keep flags
+    const int y0 = a.np + (a.pend.n > 0 ? 1 : 0);
+    keep_flags(a.keep, a.n3, a.kr, a.seed, a.chain, a.step,
+               ((size_t)((int)blockIdx.y - y0) * gridDim.x + blockIdx.x) * blockDim.x + tid);
+    return;
+  }
   if ((int)blockIdx.y == a.np) {                                  // the pending updates' plane
     run_pendset(a.pend, (int)blockIdx.x, (int)gridDim.x);
     return;
@@ -1388,23 +1417,6 @@ __global__ __launch_bounds__(FR_NW * 64) void k_fwdr(RbFwdArgs<T> a) {
   stamp(7);
 }
 
-// Keep flags of a step's forwards, one bit per element (bit e % 32 of word e / 32; forward f's words start
-// at f·⌈n3/32⌉): work item gi = f·⌈n3/64⌉ + G draws keep_group(G) of forward f (slot MASK_SLOT0 + f) and
-// stores its two words (flags past n3 zero).
-__device__ inline void keep_flags(uint32_t* keep, int n3, int nf, uint64_t seed, uint32_t chain, uint32_t step,
-                                  size_t gi) {
-  const int W = (n3 + 31) / 32, ng = (n3 + 63) / 64;
-  if (gi >= (size_t)nf * ng) return;
-  const int f = (int)(gi / (size_t)ng), G = (int)(gi - (size_t)f * ng);
-  const KeepGroup k = keep_group(seed, (uint32_t)G, MASK_SLOT0 + (uint32_t)f, step, chain);
-  const int e0 = 64 * G;
-  const uint32_t lo = n3 - e0 >= 32 ? k.lo : k.lo & ((1u << (n3 - e0)) - 1u);
-  const uint32_t hi = n3 - e0 >= 64 ? k.hi : n3 - e0 > 32 ? k.hi & ((1u << (n3 - e0 - 32)) - 1u) : 0u;
-  uint32_t* dst = keep + (size_t)f * W + 2 * G;
-  dst[0] = lo;
-  if (2 * G + 1 < W) dst[1] = hi;
-}
-
 // Mask values of one forward (the API twin of the sampler's keep flags: same groups, value = keep·(1/0.9)).
 // Thread g: group g (64 elements), written as 16-byte vectors.
 template <typename T>
@@ -1504,14 +1516,18 @@ __global__ __launch_bounds__(256) void k_mlp_init(VarTab vt, T eps, int drift, i
 template <typename T>
 __global__ __launch_bounds__(256) void k_mlp_start(VarTab vt, T eps, int drift, int noise_mode, const double* noise,
                                                    uint64_t seed, uint32_t chain, uint32_t step, double* part,
-                                                   const int32_t* prev_acc, uint32_t* keep, int n3, int nf) {
+                                                   const int32_t* prev_acc, uint32_t* keep, int n3, KeepRange kr) {
   if (blockIdx.y < 6) {
     init_block<T>(vt, eps, drift, noise_mode, noise, seed, chain, step, part, (int)blockIdx.y, (int)blockIdx.x,
                   prev_acc);
   } else {
-    keep_flags(keep, n3, nf, seed, chain, step,
-               ((size_t)(blockIdx.y - 6) * NPART + blockIdx.x) * 256 + threadIdx.x);
+    keep_flags(keep, n3, kr, seed, chain, step, ((size_t)(blockIdx.y - 6) * NPART + blockIdx.x) * 256 + threadIdx.x);
   }
+}
+// The keep flags alone (the forwards a k_fwdr step left undrawn when it falls back to the k_mm forwards).
+static __global__ __launch_bounds__(256) void k_mlp_keep(uint32_t* keep, int n3, KeepRange kr, uint64_t seed, uint32_t chain,
+                                                  uint32_t step) {
+  keep_flags(keep, n3, kr, seed, chain, step, (size_t)blockIdx.x * 256 + threadIdx.x);
 }
 
 // End-of-trajectory partials: part[0][i] = Σp², part[1][i] = Σq² per variable (same layout as init).
@@ -2067,9 +2083,13 @@ bool fwdr_ok(const MlpNet<T>& net, const SubStep<T>* ss, int n) {
 // partials of its own bias / W3 gradient into its net's fpb2 / fpw3 / fpb3; energy forwards (v < 0)
 // only their loss partials.  net's pending updates run in the extra plane.
 template <typename T>
-hipError_t mlp_fwdr(MlpNet<T>& net, const SubStep<T>* const* ss, int np) {
+hipError_t mlp_fwdr(MlpNet<T>& net, const SubStep<T>* const* ss, int np, const RbFwdArgs<T>* flags = nullptr) {
   if (np < 1 || np > FR_MAXP) return hipErrorInvalidValue;
   RbFwdArgs<T> a{};
+  if (flags) {                                                   // keep-flag rows: keep, n3, kr, seed, chain, step
+    a.keep = flags->keep; a.n3 = flags->n3; a.kr = flags->kr; a.seed = flags->seed; a.chain = flags->chain;
+    a.step = flags->step;
+  }
   if (net.fr_prof && net.fr_prof_n < net.fr_prof_cap) {          // HMCX_FWDR_PROF: this launch's stamps
     a.prof = net.fr_prof + (size_t)net.fr_prof_n * net.nrb * FR_MAXP * FR_NPH;
     net.fr_prof_np[net.fr_prof_n++] = np;
@@ -2092,7 +2112,9 @@ hipError_t mlp_fwdr(MlpNet<T>& net, const SubStep<T>* const* ss, int np) {
   }
   a.pend = net.pend;
   net.pend.n = 0;
-  const dim3 grid((unsigned)net.nrb, (unsigned)(np + (a.pend.n > 0 ? 1 : 0)));
+  const size_t kitems = (size_t)a.kr.nf * ((a.n3 + 63) / 64), per_row = (size_t)net.nrb * FR_NW * 64;
+  const unsigned krows = (unsigned)((kitems + per_row - 1) / per_row);
+  const dim3 grid((unsigned)net.nrb, (unsigned)(np + (a.pend.n > 0 ? 1 : 0)) + krows);
   if constexpr (sizeof(T) == 4) {                              // float32 only (fwdr_ok)
     const int mk = mask_kind(a.p[0].ms);
     if (mk == MK_PHILOX) hipLaunchKernelGGL((k_fwdr<T, MK_PHILOX>), grid, dim3(FR_NW * 64), 0, net.st, a);
@@ -2513,6 +2535,8 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
   // (HMCX_MLP_H1=1) recovers most of it when drawn (6.76 k) and changes nothing when stored (7.19 k).
   const char* mk_env = getenv("HMCX_MLP_MASKS");
   const bool keep_arr = philox_masks && !(mk_env && !strcmp(mk_env, "philox"));
+  const char* ks_env = getenv("HMCX_MLP_KEEP_SPLIT");
+  const bool keep_split_on = !(ks_env && ks_env[0] == '0');
   const char* h1_env = getenv("HMCX_MLP_H1");
   const bool store_h1 = philox_masks && h1_env && h1_env[0] == '1';    // m0 ∈ {0, scale} only for Philox masks
   // Batched iterations.  Sub-step i of leapfrog iteration it (variable v = order[i]) evaluates the
@@ -2624,6 +2648,10 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
     // instead beside each iteration's last launch, in an extra plane, they lengthened that launch by as
     // much as they took off this one — 21.46 k vs 22.2 k leapfrog/s at config 3)
     const bool fused_start = philox_masks && keep_arr;
+    // On the k_fwdr path the step-start launch draws only iteration 0's flags and the two energy forwards';
+    // each iteration's k_fwdr draws the next iteration's in rows of its own, on the CUs its problems leave free
+    // (HMCX_MLP_KEEP_SPLIT=0: all at step start)
+    const bool keep_split = fused_start && fr_step && n > 1 && keep_split_on;
     auto masks_for = [&](int f) -> MaskSrc<T> {
       // PHILOX: the kernels draw the flags they read (MK_PHILOX, slot MASK_SLOT0 + f); with
       // HMCX_MLP_MASKS=keep, k_mlp_keep stores the same flags once per step and the kernels load them
@@ -2642,10 +2670,12 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
     const int32_t* prev_acc = commit_pending ? accf : nullptr;   // the previous step's commit, folded in
     commit_pending = false;
     if (fused_start) {
-      const size_t items = (size_t)F * ((n3 + 63) / 64);            // one keep group per thread
+      // forwards 0 … 5 and the energies 6n, 6n + 1 when split, else all F
+      const KeepRange kr = keep_split ? KeepRange{8, 0, 6, 6 * n} : KeepRange{F, 0, F, 0};
+      const size_t items = (size_t)kr.nf * ((n3 + 63) / 64);        // one keep group per thread
       const unsigned rows = (unsigned)((items + (size_t)NPART * 256 - 1) / ((size_t)NPART * 256));
       hipLaunchKernelGGL(k_mlp_start<T>, dim3(NPART, 6 + rows), dim3(256), 0, st, vt, (T)eps,
-                         n > 0 ? 1 : 0, s->noise_mode, nz, s->seed, s->chain, step_id, part_cur, prev_acc, keep, n3, F);
+                         n > 0 ? 1 : 0, s->noise_mode, nz, s->seed, s->chain, step_id, part_cur, prev_acc, keep, n3, kr);
     } else {
       hipLaunchKernelGGL(k_mlp_init<T>, dim3(NPART, 6), dim3(256), 0, st, vt, (T)eps, n > 0 ? 1 : 0, s->noise_mode,
                          nz, s->seed, s->chain, step_id, part_cur, prev_acc);
@@ -2727,6 +2757,12 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
           chk[6] = es[0];
           chk[7] = es[1];
           use_fr = fr_step && fwdr_ok(net, chk, 8);
+          if (keep_split && !use_fr) {                          // the k_mm forwards: draw the rest now
+            const KeepRange kr{6 * n - 6, 6, 6 * n - 6, 0};
+            const size_t items = (size_t)kr.nf * ((n3 + 63) / 64);
+            hipLaunchKernelGGL(k_mlp_keep, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, st, keep, n3, kr,
+                               s->seed, s->chain, step_id);
+          }
         }
         if (use_fr) {
           // 4 launches per iteration, the layer-1 GEMM and the W2 gradient as split-K partials:
@@ -2765,7 +2801,12 @@ int mlp_sghmc_t(hmcx_ctx* ctx, const hmcx_mlp_sghmc_args* s) {
             fa[na++] = &es[1];
             e_done[1] = e_fr[1] = true;
           }
-          HMCX_HIP(ctx, mlp_fwdr<T>(net, fa, na));
+          RbFwdArgs<T> kf{};                                    // the next iteration's flags, in k_fwdr's free rows
+          if (keep_split && it + 1 < n) {
+            kf.keep = keep; kf.n3 = n3; kf.kr = KeepRange{6, 6 * (it + 1), 6, 0};
+            kf.seed = s->seed; kf.chain = s->chain; kf.step = step_id;
+          }
+          HMCX_HIP(ctx, mlp_fwdr<T>(net, fa, na, &kf));
           HMCX_HIP(ctx, mlp_ga1_batch<T>(net, ga, nga));
           for (int i = 0; i < 6; ++i) {
             const int v = s->order[i];
