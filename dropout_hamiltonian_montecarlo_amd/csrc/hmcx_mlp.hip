@@ -1420,8 +1420,8 @@ __global__ __launch_bounds__(FR_NW * 64) void k_fwdr(RbFwdArgs<T> a) {
 // Mask values of one forward (the API twin of the sampler's keep flags: same groups, value = keep·(1/0.9)).
 // Thread g: group g (64 elements), written as 16-byte vectors.
 template <typename T>
-__global__ void k_mlp_masks(T* masks, int n3, uint64_t seed, uint32_t chain, uint32_t step, uint32_t slot) {
-  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ inline void mlp_masks_group(T* masks, int n3, uint64_t seed, uint32_t chain, uint32_t step, uint32_t slot,
+                                       int g) {
   if (64 * g >= n3) return;
   const KeepGroup k = keep_group(seed, (uint32_t)g, slot, step, chain);
   const T scale = (T)(1.0 / 0.9);
@@ -1439,6 +1439,52 @@ __global__ void k_mlp_masks(T* masks, int n3, uint64_t seed, uint32_t chain, uin
       for (int q = 0; q < V; ++q)
         if (p + q < n) masks[e0 + p + q] = v[q];
     }
+  }
+}
+template <typename T>
+__global__ void k_mlp_masks(T* masks, int n3, uint64_t seed, uint32_t chain, uint32_t step, uint32_t slot) {
+  mlp_masks_group<T>(masks, n3, seed, chain, step, slot, (int)(blockIdx.x * blockDim.x + threadIdx.x));
+}
+
+// The kicks and the drift between two gradient calls of the full-batch trajectory in one launch
+// (mlp_leapfrog_t; each row the per-element arithmetic of k_axpy, hmc.py:50-53): row 0 the previous
+// sub-step's second kick p_u −= ε·g_u, row 1 the next sub-step's first kick and drift p_v −= (ε/2)·g_v,
+// q_v += ε·p_v, row 2 the next gradient call's dropout masks (hmcx_mlp_masks).  u ≠ v always (consecutive
+// variables of the order), so the rows touch disjoint memory.
+template <typename T> struct MlpKicks {
+  T* pu; const T* gu; int64_t nu; T eu;
+  T* pv; const T* gv; T* qv; int64_t nv; T hv, ev;
+  T* masks; int n3; uint64_t seed; uint32_t chain, step, slot;   // masks null: no draw
+};
+template <typename T>
+__global__ __launch_bounds__(256) void k_mlp_kicks(MlpKicks<T> k) {
+  const int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x, st = (int64_t)gridDim.x * 256;
+  if (blockIdx.y == 0) {
+    for (int64_t i = i0; i < k.nu; i += st) {
+      const T ax = k.eu * k.gu[i];
+      k.pu[i] = k.pu[i] - ax;
+    }
+  } else if (blockIdx.y == 1) {
+    for (int64_t i = i0; i < k.nv; i += st) {
+      const T ax = k.hv * k.gv[i];
+      const T p = k.pv[i] - ax;
+      k.pv[i] = p;
+      const T aq = k.ev * p;
+      k.qv[i] = k.qv[i] + aq;
+    }
+  } else if (k.masks) {
+    for (int64_t g = i0; 64 * g < k.n3; g += st) mlp_masks_group<T>(k.masks, k.n3, k.seed, k.chain, k.step, k.slot, (int)g);
+  }
+}
+// p = −p of the six variables (hmc.py:55-56, k_axpy's p − 2·p), one launch (row = variable)
+template <typename T> struct Neg6 { T* p[6]; int64_t n[6]; };
+template <typename T>
+__global__ __launch_bounds__(256) void k_mlp_neg6(Neg6<T> a) {
+  T* p = a.p[blockIdx.y];
+  const T two = T(2);
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < a.n[blockIdx.y]; i += (int64_t)gridDim.x * 256) {
+    const T ax = two * p[i];
+    p[i] = p[i] - ax;
   }
 }
 
@@ -2428,10 +2474,13 @@ int mlp_leapfrog_t(hmcx_ctx* ctx, const hmcx_mlp_leapfrog_args* s) {
     dim[v] = net.nvar(v);
   }
   uint32_t slot = s->slot0;
+  const bool pmasks = s->mask_mode == HMCX_MLP_MASKS_PHILOX;
   // the gradient components `want` (bit v) at q, in mlp_grad_t's order: forward (+ the layer-3 backward
-  // pieces the wanted components use), layer-1 backward, W1 / W2 gradients, then the bias / W3 updates
-  auto grad = [&](unsigned want) -> int {
-    if (s->mask_mode == HMCX_MLP_MASKS_PHILOX)
+  // pieces the wanted components use), layer-1 backward, W1 / W2 gradients, then the bias / W3 updates (one
+  // k_pending launch for all of them: independent element-wise updates).  The call's masks are drawn by the
+  // kicks launch before it (draw = false), except for the first call.
+  auto grad = [&](unsigned want, bool draw) -> int {
+    if (pmasks && draw)
       if (int rc = mlp_masks_t<T>(ctx, s->B, s->n_mid, s->seed, s->chain, s->step, slot++, s->masks)) return rc;
     const bool l1 = want & 3u;
     HMCX_HIP(ctx, mlp_forward<T>(net, q, ms, lpart,
@@ -2448,27 +2497,53 @@ int mlp_leapfrog_t(hmcx_ctx* ctx, const hmcx_mlp_leapfrog_args* s) {
       if (want & (1u << v)) {
         u.W = q[v]; u.G = g[v];
         set_pending(net, v, UPD_GRAD, u);
-        HMCX_HIP(ctx, flush_pending(net));
       }
+    HMCX_HIP(ctx, flush_pending(net));
+    return HMCX_OK;
+  };
+  // one launch between two gradient calls: the second kick of variable pu (−1: none, hmc.py:53), the first
+  // kick and the drift of variable nv (−1: none, :50-51), and the next call's masks
+  auto kicks = [&](int pu, int nv, bool masks) -> int {
+    MlpKicks<T> k{};
+    int64_t n = 0;
+    if (pu >= 0) { k.pu = p[pu]; k.gu = g[pu]; k.nu = dim[pu]; k.eu = (T)s->eps; n = std::max(n, k.nu); }
+    if (nv >= 0) {
+      k.pv = p[nv]; k.gv = g[nv]; k.qv = q[nv]; k.nv = dim[nv]; k.hv = (T)(0.5 * s->eps); k.ev = (T)s->eps;
+      n = std::max(n, k.nv);
+    }
+    if (masks && pmasks) {
+      k.masks = (T*)s->masks; k.n3 = 3 * s->B * s->n_mid; k.seed = s->seed; k.chain = s->chain; k.step = s->step;
+      k.slot = slot++;
+      n = std::max(n, (int64_t)(k.n3 + 63) / 64);
+    }
+    if (n == 0) return HMCX_OK;
+    const unsigned nb = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_mlp_kicks<T>, dim3(nb, 3), dim3(256), 0, ctx->stream, k);
+    HMCX_HIP(ctx, hipGetLastError());
     return HMCX_OK;
   };
   const int* o = s->order;
   // the last gradient call computes all six components, so g is the full gradient at the final
   // position (as the header promises); every earlier call only the two the next kicks read
-  if (int rc = grad(s->n_iter > 0 ? 1u << o[0] : 63u)) return rc;
+  if (int rc = grad(s->n_iter > 0 ? 1u << o[0] : 63u, true)) return rc;
   for (int it = 0; it < s->n_iter; ++it)
     for (int i = 0; i < 6; ++i) {
       const int v = o[i];
       const bool tail = it == s->n_iter - 1 && i == 5;        // no next kick follows
-      int rc = axpy_t<T>(ctx, 0, dim[v], 0.5 * s->eps, g[v], p[v]);                    // hmc.py:50
-      if (!rc) rc = axpy_t<T>(ctx, 1, dim[v], s->eps, p[v], q[v]);                     // :51
+      // :53 of the previous sub-step (none before the first), :50-51 of this one, this call's masks
+      int rc = kicks(it == 0 && i == 0 ? -1 : o[(i + 5) % 6], v, true);
       if (v == 0) net.xw_valid = false;
-      if (!rc) rc = grad(tail ? 63u : (1u << v) | (1u << o[(i + 1) % 6]));            // :52
-      if (!rc) rc = axpy_t<T>(ctx, 0, dim[v], s->eps, g[v], p[v]);                     // :53
+      if (!rc) rc = grad(tail ? 63u : (1u << v) | (1u << o[(i + 1) % 6]), false);    // :52
       if (rc) return rc;
     }
-  for (int v = 0; v < 6; ++v)                                                           // :55-56
-    if (int rc = axpy_t<T>(ctx, 0, dim[v], 2.0, p[v], p[v])) return rc;
+  if (s->n_iter > 0)
+    if (int rc = kicks(o[5], -1, false)) return rc;                                   // :53 of the last sub-step
+  Neg6<T> ng{};                                                                         // :55-56
+  int64_t nmax = 0;
+  for (int v = 0; v < 6; ++v) { ng.p[v] = p[v]; ng.n[v] = dim[v]; nmax = std::max(nmax, dim[v]); }
+  hipLaunchKernelGGL(k_mlp_neg6<T>, dim3((unsigned)std::min<int64_t>((nmax + 255) / 256, 4096), 6), dim3(256), 0,
+                     ctx->stream, ng);
+  HMCX_HIP(ctx, hipGetLastError());
   return HMCX_OK;
 }
 

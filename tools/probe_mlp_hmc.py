@@ -2,7 +2,7 @@
 """Full-batch HMC on the config-3 MLP (784-256-256-10, B = 500): seconds per leapfrog iteration of
 hmc.step with the trajectory in one hmcx_mlp_hmc_leapfrog call vs the host loop it replaces
 (HMCX_HMC_HOST_LOOP=1: model.grad + hmcx_axpy per variable from Python).
-    python tools/probe_mlp_hmc.py [f32|f64] [steps]"""
+    python tools/probe_mlp_hmc.py [f32|f64] [steps] [device]   (device: skip the host loop)"""
 import os
 import sys
 import time
@@ -40,8 +40,9 @@ def run(host, dt, steps):
 if __name__ == "__main__":
     dt = torch.float64 if (len(sys.argv) > 1 and sys.argv[1] == "f64") else torch.float32
     steps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+    modes = (False,) if "device" in sys.argv else (True, False)
     for rep in range(2):
-        for host in (True, False):
+        for host in modes:
             t, n = run(host, dt, steps)
             print("%s %s: %d steps, %.3f s, %d leapfrogs, %.1f us per leapfrog"
                   % ("host-loop" if host else "device   ", str(dt), steps, t, n, 1e6 * t / max(n, 1)), flush=True)
