@@ -219,34 +219,36 @@ template <typename T> struct Pending {
   const T* part;
   Upd<T> u;
 };
+// the update of element i: the sum of its partials in fixed order (in-order sum of batches of 16 loads
+// that all go out before it: one memory round trip per 16 partials instead of one per partial)
+template <typename T>
+__device__ inline void pending_elem(const Pending<T>& pd, int i) {
+  constexpr int PB = 16;                                       // partials loaded per batch
+  T s = T(0);
+  if (pd.nparts == 4) {                                        // a split-K weight gradient (W2): 4 partials
+    T v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = pd.part[(size_t)q * pd.n + i];
+    s = ((v[0] + v[1]) + v[2]) + v[3];
+    apply_upd(pd.u, pd.mode, i, s);
+    return;
+  }
+  for (int b0 = 0; b0 < pd.nparts; b0 += PB) {
+    T v[PB];
+#pragma unroll
+    for (int q = 0; q < PB; ++q) v[q] = pd.part[(size_t)min(b0 + q, pd.nparts - 1) * pd.n + i];   // clamped, unconditional
+#pragma unroll
+    for (int q = 0; q < PB; ++q)
+      if (b0 + q < pd.nparts) s = (b0 + q == 0) ? v[q] : s + v[q];
+  }
+  apply_upd(pd.u, pd.mode, i, s);
+}
 // bid / nb: this workgroup's index among the nb workgroups that share the work
 template <typename T>
 __device__ inline void run_pending(const Pending<T>& pd, int bid, int nb) {
   if (pd.mode == UPD_NONE) return;
   const int nthr = nb * blockDim.x;
-  constexpr int PB = 16;                                       // partials loaded per batch
-  for (int i = bid * blockDim.x + threadIdx.x; i < pd.n; i += nthr) {
-    // all loads of a batch go out before the (in-order) sum: one memory round trip per 16
-    // partials instead of one per partial
-    T s = T(0);
-    if (pd.nparts == 4) {                                      // a split-K weight gradient (W2): 4 partials
-      T v[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) v[q] = pd.part[(size_t)q * pd.n + i];
-      s = ((v[0] + v[1]) + v[2]) + v[3];
-      apply_upd(pd.u, pd.mode, i, s);
-      continue;
-    }
-    for (int b0 = 0; b0 < pd.nparts; b0 += PB) {
-      T v[PB];
-#pragma unroll
-      for (int q = 0; q < PB; ++q) v[q] = pd.part[(size_t)min(b0 + q, pd.nparts - 1) * pd.n + i];   // clamped, unconditional
-#pragma unroll
-      for (int q = 0; q < PB; ++q)
-        if (b0 + q < pd.nparts) s = (b0 + q == 0) ? v[q] : s + v[q];
-    }
-    apply_upd(pd.u, pd.mode, i, s);
-  }
+  for (int i = bid * blockDim.x + threadIdx.x; i < pd.n; i += nthr) pending_elem(pd, i);
 }
 // The pending updates a launch applies first (up to four: the bias / W3 sub-steps of one batched
 // iteration).  A batched launch (blockIdx.z = problem) runs them in an extra plane of workgroups of
@@ -1450,22 +1452,36 @@ __global__ void k_mlp_masks(T* masks, int n3, uint64_t seed, uint32_t chain, uin
 // (mlp_leapfrog_t; each row the per-element arithmetic of k_axpy, hmc.py:50-53): row 0 the previous
 // sub-step's second kick p_u −= ε·g_u, row 1 the next sub-step's first kick and drift p_v −= (ε/2)·g_v,
 // q_v += ε·p_v, row 2 the next gradient call's dropout masks (hmcx_mlp_masks).  u ≠ v always (consecutive
-// variables of the order), so the rows touch disjoint memory.
+// variables of the order), so the rows touch disjoint memory.  A bias / W3 gradient the kick reads may still
+// be pending (its row-block partials, UPD_GRAD): the row computes it element by element first (k_pending's
+// arithmetic, the same thread reads back g[i]) — no k_pending launch of its own.
 template <typename T> struct MlpKicks {
   T* pu; const T* gu; int64_t nu; T eu;
   T* pv; const T* gv; T* qv; int64_t nv; T hv, ev;
   T* masks; int n3; uint64_t seed; uint32_t chain, step, slot;   // masks null: no draw
+  PendSet<T> ps;
 };
+template <typename T> __device__ inline int pend_of(const PendSet<T>& ps, const T* g) {
+  int pj = -1;
+#pragma unroll
+  for (int j = 0; j < MAXPEND; ++j)
+    if (j < ps.n && ps.p[j].mode == UPD_GRAD && ps.p[j].u.G == g) pj = j;
+  return pj;
+}
 template <typename T>
 __global__ __launch_bounds__(256) void k_mlp_kicks(MlpKicks<T> k) {
   const int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x, st = (int64_t)gridDim.x * 256;
   if (blockIdx.y == 0) {
+    const int pj = pend_of(k.ps, k.gu);
     for (int64_t i = i0; i < k.nu; i += st) {
+      if (pj >= 0) pending_elem(k.ps.p[pj], (int)i);
       const T ax = k.eu * k.gu[i];
       k.pu[i] = k.pu[i] - ax;
     }
   } else if (blockIdx.y == 1) {
+    const int pj = pend_of(k.ps, k.gv);
     for (int64_t i = i0; i < k.nv; i += st) {
+      if (pj >= 0) pending_elem(k.ps.p[pj], (int)i);
       const T ax = k.hv * k.gv[i];
       const T p = k.pv[i] - ax;
       k.pv[i] = p;
@@ -2479,7 +2495,7 @@ int mlp_leapfrog_t(hmcx_ctx* ctx, const hmcx_mlp_leapfrog_args* s) {
   // pieces the wanted components use), layer-1 backward, W1 / W2 gradients, then the bias / W3 updates (one
   // k_pending launch for all of them: independent element-wise updates).  The call's masks are drawn by the
   // kicks launch before it (draw = false), except for the first call.
-  auto grad = [&](unsigned want, bool draw) -> int {
+  auto grad = [&](unsigned want, bool draw, bool defer) -> int {
     if (pmasks && draw)
       if (int rc = mlp_masks_t<T>(ctx, s->B, s->n_mid, s->seed, s->chain, s->step, slot++, s->masks)) return rc;
     const bool l1 = want & 3u;
@@ -2498,7 +2514,7 @@ int mlp_leapfrog_t(hmcx_ctx* ctx, const hmcx_mlp_leapfrog_args* s) {
         u.W = q[v]; u.G = g[v];
         set_pending(net, v, UPD_GRAD, u);
       }
-    HMCX_HIP(ctx, flush_pending(net));
+    if (!defer) HMCX_HIP(ctx, flush_pending(net));            // else: the next kicks launch applies them
     return HMCX_OK;
   };
   // one launch between two gradient calls: the second kick of variable pu (−1: none, hmc.py:53), the first
@@ -2516,6 +2532,8 @@ int mlp_leapfrog_t(hmcx_ctx* ctx, const hmcx_mlp_leapfrog_args* s) {
       k.slot = slot++;
       n = std::max(n, (int64_t)(k.n3 + 63) / 64);
     }
+    k.ps = net.pend;                                           // the previous call's deferred bias / W3 gradients
+    net.pend.n = 0;
     if (n == 0) return HMCX_OK;
     const unsigned nb = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
     hipLaunchKernelGGL(k_mlp_kicks<T>, dim3(nb, 3), dim3(256), 0, ctx->stream, k);
@@ -2525,7 +2543,7 @@ int mlp_leapfrog_t(hmcx_ctx* ctx, const hmcx_mlp_leapfrog_args* s) {
   const int* o = s->order;
   // the last gradient call computes all six components, so g is the full gradient at the final
   // position (as the header promises); every earlier call only the two the next kicks read
-  if (int rc = grad(s->n_iter > 0 ? 1u << o[0] : 63u, true)) return rc;
+  if (int rc = grad(s->n_iter > 0 ? 1u << o[0] : 63u, true, s->n_iter > 0)) return rc;
   for (int it = 0; it < s->n_iter; ++it)
     for (int i = 0; i < 6; ++i) {
       const int v = o[i];
@@ -2533,7 +2551,7 @@ int mlp_leapfrog_t(hmcx_ctx* ctx, const hmcx_mlp_leapfrog_args* s) {
       // :53 of the previous sub-step (none before the first), :50-51 of this one, this call's masks
       int rc = kicks(it == 0 && i == 0 ? -1 : o[(i + 5) % 6], v, true);
       if (v == 0) net.xw_valid = false;
-      if (!rc) rc = grad(tail ? 63u : (1u << v) | (1u << o[(i + 1) % 6]), false);    // :52
+      if (!rc) rc = grad(tail ? 63u : (1u << v) | (1u << o[(i + 1) % 6]), false, !tail);   // :52
       if (rc) return rc;
     }
   if (s->n_iter > 0)

@@ -868,12 +868,17 @@ int sgd_run_t(hmcx_ctx* ctx, const hmcx_sgd_args* s) {
   return timing_end(ctx, ctx->stream);
 }
 
-// Σ x² in float64, one workgroup, fixed order (logistic.py:20's np.sum(np.square(θ))).
+// Σ x² in float64, fixed order (logistic.py:20's np.sum(np.square(θ))).  Up to SQ_ONE elements one workgroup
+// (lane t sums elements t, t + 256, …, then a fixed tree); above, SQ_NB workgroups each sum a contiguous slice
+// that way into part[b] and one more launch adds the SQ_NB partials in block order — one workgroup streaming
+// a 200,704-element W1 alone took 37.8 µs (one CU's pull rate), a quarter of the full-batch MLP accept.
+constexpr int64_t SQ_ONE = 16384;
+constexpr int SQ_NB = 64;
 template <typename T>
-__global__ __launch_bounds__(256) void k_sumsq(const T* x, int64_t n, double* out) {
+__device__ inline double sumsq_slice(const T* x, int64_t i0, int64_t i1) {
   __shared__ double sh[256];
   double acc = 0.0;
-  for (int64_t i = threadIdx.x; i < n; i += 256) {
+  for (int64_t i = i0 + threadIdx.x; i < i1; i += 256) {
     const double v = (double)x[i];
     acc += v * v;
   }
@@ -883,12 +888,32 @@ __global__ __launch_bounds__(256) void k_sumsq(const T* x, int64_t n, double* ou
     if ((int)threadIdx.x < w) sh[threadIdx.x] += sh[threadIdx.x + w];
     __syncthreads();
   }
-  if (threadIdx.x == 0) *out = sh[0];
+  return sh[0];
+}
+template <typename T>
+__global__ __launch_bounds__(256) void k_sumsq(const T* x, int64_t n, double* out) {
+  const int64_t per = (n + gridDim.x - 1) / gridDim.x, i0 = (int64_t)blockIdx.x * per;
+  const double v = sumsq_slice<T>(x, i0, i0 + per < n ? i0 + per : n);
+  if (threadIdx.x == 0) out[blockIdx.x] = v;
+}
+__global__ void k_sumsq_fin(const double* part, int nb, double* out) {
+  double s = part[0];
+  for (int b = 1; b < nb; ++b) s += part[b];
+  *out = s;
 }
 
 template <typename T>
 int sumsq_t(hmcx_ctx* ctx, const void* x, int64_t n, double* out) {
-  hipLaunchKernelGGL(k_sumsq<T>, dim3(1), dim3(256), 0, ctx->stream, (const T*)x, n, out);
+  if (n <= SQ_ONE) {
+    hipLaunchKernelGGL(k_sumsq<T>, dim3(1), dim3(256), 0, ctx->stream, (const T*)x, n, out);
+  } else {
+    Workspace ws(ctx);
+    double* part;
+    do { ws.reset(); part = ws.take<double>(SQ_NB); } while (ws.retry());
+    if (ws.failed) return set_error(ctx, HMCX_ENOMEM, "sumsq: workspace");
+    hipLaunchKernelGGL(k_sumsq<T>, dim3(SQ_NB), dim3(256), 0, ctx->stream, (const T*)x, n, part);
+    hipLaunchKernelGGL(k_sumsq_fin, dim3(1), dim3(1), 0, ctx->stream, (const double*)part, SQ_NB, out);
+  }
   HMCX_HIP(ctx, hipGetLastError());
   return HMCX_OK;
 }

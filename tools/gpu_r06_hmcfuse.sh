@@ -5,7 +5,7 @@ set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 O=gpurun_out/${TAG:-r06_hmcfuse}
 mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests/test_gpu_mlp.py -x -q --timeout 200 --timeout-method thread > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests/test_gpu_mlp.py tests/test_gpu_hmc.py tests/test_gpu_logistic_sgd.py tests/test_gpu_softmax.py -x -q --timeout 200 --timeout-method thread > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
 tail -2 $O/pytest.log
 for r in 1 2; do
   for L in libhmcx_base.so libhmcx.so; do
