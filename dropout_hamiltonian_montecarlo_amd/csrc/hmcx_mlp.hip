@@ -243,12 +243,35 @@ __device__ inline void pending_elem(const Pending<T>& pd, int i) {
   }
   apply_upd(pd.u, pd.mode, i, s);
 }
-// bid / nb: this workgroup's index among the nb workgroups that share the work
+// bid / nb: this workgroup's index among the nb workgroups that share the work (pending_elem's arithmetic,
+// written out: routed through pending_elem, the sampler's pending planes measured 0.4 % slower)
 template <typename T>
 __device__ inline void run_pending(const Pending<T>& pd, int bid, int nb) {
   if (pd.mode == UPD_NONE) return;
   const int nthr = nb * blockDim.x;
-  for (int i = bid * blockDim.x + threadIdx.x; i < pd.n; i += nthr) pending_elem(pd, i);
+  constexpr int PB = 16;                                       // partials loaded per batch
+  for (int i = bid * blockDim.x + threadIdx.x; i < pd.n; i += nthr) {
+    // all loads of a batch go out before the (in-order) sum: one memory round trip per 16
+    // partials instead of one per partial
+    T s = T(0);
+    if (pd.nparts == 4) {                                      // a split-K weight gradient (W2): 4 partials
+      T v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = pd.part[(size_t)q * pd.n + i];
+      s = ((v[0] + v[1]) + v[2]) + v[3];
+      apply_upd(pd.u, pd.mode, i, s);
+      continue;
+    }
+    for (int b0 = 0; b0 < pd.nparts; b0 += PB) {
+      T v[PB];
+#pragma unroll
+      for (int q = 0; q < PB; ++q) v[q] = pd.part[(size_t)min(b0 + q, pd.nparts - 1) * pd.n + i];   // clamped, unconditional
+#pragma unroll
+      for (int q = 0; q < PB; ++q)
+        if (b0 + q < pd.nparts) s = (b0 + q == 0) ? v[q] : s + v[q];
+    }
+    apply_upd(pd.u, pd.mode, i, s);
+  }
 }
 // The pending updates a launch applies first (up to four: the bias / W3 sub-steps of one batched
 // iteration).  A batched launch (blockIdx.z = problem) runs them in an extra plane of workgroups of
